@@ -1,0 +1,106 @@
+/*
+ * siren_amd.h — C ABI of the MI355X-native SIREN engine (libsiren_amd.so).
+ *
+ * This is the drop-in boundary for the reference's hot path: the SIREN MLP
+ *   z_0 = x W_0^T + b_0,  a_l = sin(w * z_l),  z_l = a_{l-1} W_l^T + b_l,  y = a_L W_out^T + b_out
+ * and its coordinate derivatives. In the reference (xvdp/siren, a pure-PyTorch code base with no native
+ * code of its own) the path is:
+ *   modules.py:16-25   BatchLinear.forward  (matmul, in-place bias add)      -> siren_forward*
+ *   modules.py:32-34   Sine.forward         (torch.sin(30 * input))          -> fused epilogue
+ *   modules.py:89-94   FCBlock.forward / modules.py:143-160 SingleBVPNet.forward
+ *   diff_operators.py:39-43 gradient (torch.autograd.grad, grad_outputs=ones) -> siren_forward_grad (gy = NULL)
+ *   autograd backward of the stack (training.py:95-96)                       -> siren_forward_grad (gy given)
+ *                                                                               + siren_backward (theta-gradients)
+ * There is no reference C ABI to mirror; the reference-side binding is the ctypes module
+ * siren_amd/_lib.py.
+ *
+ * Conventions
+ *  - Every entry point returns 0 on success, otherwise a SIREN_E* code; siren_last_error() then returns a
+ *    thread-local message. No C++ exception crosses this ABI.
+ *  - All buffers are device pointers owned by the caller (PyTorch caching allocator). The library never
+ *    allocates device memory. fp32, contiguous, row-major:
+ *      x (n, d_in); y (n, d_out); gy (n, d_out); gx (n, d_in).
+ *  - params is ONE flat fp32 buffer in nn.Linear / state_dict order:
+ *      W_0 (H, d_in), b_0 (H), [W_l (H, H), b_l (H)] for l = 1..n_hidden, W_out (d_out, H), b_out (d_out)
+ *    i.e. exactly torch.cat([p.flatten() for p in SingleBVPNet.parameters()]).
+ *  - Work is enqueued on `stream` (a hipStream_t; pass torch.cuda.current_stream().cuda_stream). Nothing
+ *    synchronises the host.
+ *  - Weights change every optimizer step, so they are re-packed into the caller's workspace by
+ *    siren_pack() once per step (a ~1 us kernel) before any compute entry point is used.
+ */
+#ifndef SIREN_AMD_H
+#define SIREN_AMD_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SIREN_ABI_VERSION 1
+
+enum {
+    SIREN_OK = 0,
+    SIREN_EINVAL = 1,       /* bad pointer / size / config value                        */
+    SIREN_EUNSUPPORTED = 2, /* valid SIREN config outside what the fused kernels cover  */
+    SIREN_EHIP = 3          /* a HIP runtime error (launch failure, ...)               */
+};
+
+/* Network description. Mirrors SingleBVPNet(out_features, type='sine', in_features, mode='mlp',
+ * hidden_features, num_hidden_layers) (modules.py:122-123) and the notebook Siren(in_features,
+ * hidden_features, hidden_layers, out_features, outermost_linear, first_omega_0, hidden_omega_0). */
+typedef struct siren_cfg {
+    int32_t d_in;             /* in_features, 1..4                                         */
+    int32_t hidden;           /* hidden_features (256 in the fused kernels)                */
+    int32_t n_hidden;         /* num_hidden_layers: H->H layers between first and last    */
+    int32_t d_out;            /* out_features, 1..4                                        */
+    float omega_first;        /* w of the first sine layer (30; Sine hard-codes 30)        */
+    float omega_hidden;       /* w of the hidden sine layers (30)                          */
+    int32_t outermost_linear; /* 1: last layer linear (SingleBVPNet); 0: sin(w*z) as well  */
+    int32_t reserved;
+} siren_cfg;
+
+/* Library ABI version (== SIREN_ABI_VERSION). */
+int32_t siren_abi_version(void);
+
+/* Message for the last failing call on this thread ("" if none). */
+const char* siren_last_error(void);
+
+/* Number of fp32 values in the flat parameter buffer. */
+int32_t siren_param_count(const siren_cfg* cfg, int64_t* count);
+
+/* Number of fp32 values of packed-weight workspace that siren_pack() fills. */
+int32_t siren_workspace_floats(const siren_cfg* cfg, int64_t* count);
+
+/* Repack params into the kernels' LDS-slice layout (workspace ws, siren_workspace_floats() floats). */
+int32_t siren_pack(const siren_cfg* cfg, const float* params, float* ws, void* stream);
+
+/* W0 (forward value): y = Phi(x). Replaces SingleBVPNet.forward's model_out (modules.py:143-160). */
+int32_t siren_forward(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y,
+                      void* stream);
+
+/* W1 (forward + coordinate vector-Jacobian product) in ONE launch:
+ *   y  = Phi(x)                       (skipped when y == NULL)
+ *   gx = sum_j gy_j * dPhi_j/dx       (gy == NULL means gy = ones: diff_operators.gradient, d.o.py:39-43)
+ * n_hidden must be 1..3 (cos(w z_l) of every layer stays in registers). */
+int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x, int64_t n,
+                           const float* gy, float* y, float* gx, void* stream);
+
+/* fp32 values of backward workspace siren_backward() needs for n coordinates (sin activations and deltas of
+ * every sine layer, plus the split-K partial gradient slabs). */
+int32_t siren_train_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count);
+
+/* W2 backward for one coordinate batch: given gy = dL/dy (n, d_out), writes
+ *   gx (n, d_in)             = dL/dx                       (model_in.grad, training.py:96)
+ *   gparams (param_count)    = dL/dtheta in flat param order (BatchLinear weight/bias .grad)
+ * Stages: the fused forward + reverse kernel in store mode, the split-K MFMA weight-gradient kernel and a
+ * deterministic slab reduction (no atomics: bitwise reproducible). `reserved` must be NULL.
+ * Replaces autograd's MmBackward/SinBackward/MulBackward chain of train_loss.backward() (training.py:95-96). */
+int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* gy,
+                       float* tws, void* reserved, float* gx, float* gparams, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIREN_AMD_H */

@@ -1,0 +1,202 @@
+"""CPU restatement of the reference's SIREN hot path — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module, and only as the
+checker / the timed CPU baseline. The product path (siren_amd) never imports it and has no CPU fallback.
+
+Two restatements of xvdp/siren (/root/reference, read as text only):
+
+* numpy fp64, analytic (the oracle proper):
+    forward            modules.py:16-25 (BatchLinear: x W^T, += b), modules.py:32-34 (Sine: sin(30 z)),
+                       modules.py:89-94 / 143-160 (FCBlock / SingleBVPNet: outermost layer linear),
+                       ipynb SineLayer/Siren (first_omega_0 / hidden_omega_0, optional final sine)
+    forward_grad       diff_operators.py:39-43 gradient = autograd.grad(y, x, grad_outputs=gy) -> reverse sweep
+    forward_laplace    diff_operators.py:27-36 laplace = divergence(gradient) -> second-order forward Taylor
+* torch (CPU), the reference's op sequence with autograd (torch_forward): used for the loss theta-gradients
+  (loss_functions.py:8-12 image_mse, :84-89 gradients_mse, :104-109 laplace_mse, :214-238 sdf) and as the
+  "reference CPU path" that bench.py times on the GPU box's host cores (cpu_baseline, kind "port").
+
+Parity is pinned: tests/test_oracle.py checks both restatements against the golden vectors that
+tests/golden/make_golden.py produced by running the reference itself.
+"""
+import numpy as np
+
+# ----------------------------------------------------------------------------------------------------------
+# parameter plumbing (flat buffer in nn.Linear / state_dict order, include/siren_amd.h)
+# ----------------------------------------------------------------------------------------------------------
+
+
+def layers_from_state(sd, prefix='w_'):
+    """[(W, b), ...] from a state dict (or fixture dict with key prefix) keyed net.net.{i}.0.{weight,bias}."""
+    out, i = [], 0
+    while True:
+        kw = '%snet.net.%d.0.weight' % (prefix, i)
+        if kw not in sd:
+            break
+        out.append((np.asarray(sd[kw]), np.asarray(sd['%snet.net.%d.0.bias' % (prefix, i)])))
+        i += 1
+    return out
+
+
+def flatten(layers):
+    return np.concatenate([np.concatenate([W.reshape(-1), b.reshape(-1)]) for W, b in layers])
+
+
+def unflatten(flat, d_in, hidden, n_hidden, d_out):
+    dims = [d_in] + [hidden] * (n_hidden + 1) + [d_out]
+    layers, off = [], 0
+    for fi, fo in zip(dims[:-1], dims[1:]):
+        W = flat[off:off + fo * fi].reshape(fo, fi)
+        off += fo * fi
+        b = flat[off:off + fo]
+        off += fo
+        layers.append((W, b))
+    assert off == flat.size
+    return layers
+
+
+# ----------------------------------------------------------------------------------------------------------
+# numpy fp64 analytic restatement
+# ----------------------------------------------------------------------------------------------------------
+
+
+def _omegas(n_layers, omega_first, omega_hidden):
+    return [omega_first] + [omega_hidden] * (n_layers - 1)
+
+
+def forward(x, layers, omega_first=30., omega_hidden=30., outermost_linear=True):
+    """Phi(x) in fp64 (modules.py:16-34, 89-94)."""
+    a = np.asarray(x, np.float64)
+    om = _omegas(len(layers), omega_first, omega_hidden)
+    for li, (W, b) in enumerate(layers):
+        z = a @ np.asarray(W, np.float64).T + np.asarray(b, np.float64)
+        last = li == len(layers) - 1
+        a = z if (last and outermost_linear) else np.sin(om[li] * z)
+    return a
+
+
+def forward_grad(x, layers, gy=None, omega_first=30., omega_hidden=30., outermost_linear=True):
+    """(y, gx) with gx = sum_j gy_j dy_j/dx (gy=None: ones) — what autograd.grad(y, x, gy) returns
+    (diff_operators.py:39-43), by an explicit reverse sweep in fp64."""
+    a = np.asarray(x, np.float64)
+    om = _omegas(len(layers), omega_first, omega_hidden)
+    cos_stack = []
+    for li, (W, b) in enumerate(layers):
+        z = a @ np.asarray(W, np.float64).T + np.asarray(b, np.float64)
+        last = li == len(layers) - 1
+        if last and outermost_linear:
+            a = z
+            cos_stack.append(None)
+        else:
+            a = np.sin(om[li] * z)
+            cos_stack.append(om[li] * np.cos(om[li] * z))
+    y = a
+    g = np.ones_like(y) if gy is None else np.asarray(gy, np.float64)
+    for li in range(len(layers) - 1, -1, -1):
+        if cos_stack[li] is not None:
+            g = g * cos_stack[li]
+        g = g @ np.asarray(layers[li][0], np.float64)
+    return y, g
+
+
+def forward_laplace(x, layers, omega_first=30., omega_hidden=30., outermost_linear=True):
+    """(y, grad, lap) for d_out == 1: value, gradient and Laplacian sum_i d2y/dx_i^2 (diff_operators.py:27-36)
+    by forward-mode Taylor propagation of (value, d tangents, Laplacian) in fp64."""
+    x = np.asarray(x, np.float64)
+    n, d = x.shape
+    om = _omegas(len(layers), omega_first, omega_hidden)
+    v = x
+    t = np.broadcast_to(np.eye(d)[None], (n, d, d)).copy()  # t[c, i, k] = d v_k / d x_i
+    s = np.zeros_like(x)                                     # s[c, k]   = sum_i d2 v_k / d x_i^2
+    for li, (W, b) in enumerate(layers):
+        W = np.asarray(W, np.float64)
+        z = v @ W.T + np.asarray(b, np.float64)
+        tz = t @ W.T
+        sz = s @ W.T
+        last = li == len(layers) - 1
+        if last and outermost_linear:
+            v, t, s = z, tz, sz
+        else:
+            w = om[li]
+            sn, cs = np.sin(w * z), np.cos(w * z)
+            v = sn
+            t = (w * cs)[:, None, :] * tz
+            s = w * cs * sz - w * w * sn * np.sum(tz * tz, axis=1)
+    assert v.shape[1] == 1, 'forward_laplace restates the o == 1 case'
+    return v, t[:, :, 0], s
+
+
+# ----------------------------------------------------------------------------------------------------------
+# torch restatement (reference op sequence + autograd), CPU
+# ----------------------------------------------------------------------------------------------------------
+
+
+def torch_forward(x, params, omega_first=30., omega_hidden=30., outermost_linear=True):
+    """The reference's op sequence on torch tensors: x.matmul(W^T), += b (modules.py:23-24), sin(w*z)
+    (modules.py:34). `params` is the list [W0, b0, W1, b1, ...]."""
+    a = x
+    nl = len(params) // 2
+    for li in range(nl):
+        W, b = params[2 * li], params[2 * li + 1]
+        z = a.matmul(W.permute(1, 0))
+        z = z + b.unsqueeze(-2)
+        last = li == nl - 1
+        if not (last and outermost_linear):
+            z = (omega_first if li == 0 else omega_hidden) * z
+            z = z.sin()
+        a = z
+    return a
+
+
+def torch_gradient(y, x):
+    import torch
+    return torch.autograd.grad(y, [x], grad_outputs=torch.ones_like(y), create_graph=True)[0]
+
+
+def torch_laplace(y, x):
+    import torch
+    g = torch_gradient(y, x)
+    div = 0.
+    for i in range(g.shape[-1]):
+        div = div + torch.autograd.grad(g[..., i], x, torch.ones_like(g[..., i]), create_graph=True)[0][..., i:i + 1]
+    return div
+
+
+def torch_loss_terms(name, y, x, gt):
+    """Loss terms as in loss_functions.py (image_mse 8-12, gradients_mse 84-89, laplace_mse 104-109, sdf 214-238)."""
+    import torch
+    import torch.nn.functional as F
+    if name == 'image_mse':
+        return {'img_loss': ((y - gt['img']) ** 2).mean()}
+    if name == 'gradients_mse':
+        g = torch_gradient(y, x)
+        return {'gradients_loss': torch.mean((g - gt['gradients']).pow(2).sum(-1))}
+    if name == 'laplace_mse':
+        return {'laplace_loss': torch.mean((torch_laplace(y, x) - gt['laplace']) ** 2)}
+    if name == 'sdf':
+        g = torch_gradient(y, x)
+        on = gt['sdf'] != -1
+        sdf_c = torch.where(on, y, torch.zeros_like(y))
+        inter = torch.where(on, torch.zeros_like(y), torch.exp(-1e2 * torch.abs(y)))
+        normal = torch.where(on, 1 - F.cosine_similarity(g, gt['normals'], dim=-1)[..., None],
+                             torch.zeros_like(g[..., :1]))
+        gradc = torch.abs(g.norm(dim=-1) - 1)
+        return {'sdf': torch.abs(sdf_c).mean() * 3e3, 'inter': inter.mean() * 1e2,
+                'normal_constraint': normal.mean() * 1e2, 'grad_constraint': gradc.mean() * 5e1}
+    raise KeyError(name)
+
+
+def torch_param_grads(name, x, layers, gt, dtype='float64', **kw):
+    """Flat theta-gradient of sum(loss.mean()) (training.py:75-96) through the torch restatement."""
+    import torch
+    dt = getattr(torch, dtype)
+    params = []
+    for W, b in layers:
+        params += [torch.tensor(np.asarray(W), dtype=dt, requires_grad=True),
+                   torch.tensor(np.asarray(b), dtype=dt, requires_grad=True)]
+    xt = torch.tensor(np.asarray(x), dtype=dt, requires_grad=True)
+    y = torch_forward(xt, params, **kw)
+    gtt = {k: torch.tensor(np.asarray(v), dtype=dt) for k, v in gt.items()}
+    terms = torch_loss_terms(name, y, xt, gtt)
+    total = sum(v.mean() for v in terms.values())
+    grads = torch.autograd.grad(total, params)
+    return np.concatenate([g.detach().numpy().reshape(-1) for g in grads]), float(total)

@@ -1,0 +1,82 @@
+"""ctypes binding of the C ABI in include/siren_amd.h (libsiren_amd.so, built in-tree by __graft_entry__.build()).
+
+This is the "reference-side binding" of the drop-in boundary: the reference (xvdp/siren) is pure PyTorch, so
+its FFI for this path is a Python module. Everything here is plain pointers and sizes; torch only supplies
+device memory and the current HIP stream (see siren_amd/engine.py).
+
+The library is REQUIRED: importing the engine without it raises, there is no CPU or eager fallback.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('SIREN_AMD_LIB', os.path.join(_HERE, 'libsiren_amd.so'))
+ABI_VERSION = 1
+
+# Error codes (include/siren_amd.h)
+SIREN_OK, SIREN_EINVAL, SIREN_EUNSUPPORTED, SIREN_EHIP = 0, 1, 2, 3
+
+
+class SirenCfg(ctypes.Structure):
+    """struct siren_cfg (include/siren_amd.h)."""
+    _fields_ = [('d_in', ctypes.c_int32), ('hidden', ctypes.c_int32), ('n_hidden', ctypes.c_int32),
+                ('d_out', ctypes.c_int32), ('omega_first', ctypes.c_float), ('omega_hidden', ctypes.c_float),
+                ('outermost_linear', ctypes.c_int32), ('reserved', ctypes.c_int32)]
+
+
+class SirenUnsupported(RuntimeError):
+    """A valid SIREN configuration that the fused kernels do not cover (SIREN_EUNSUPPORTED)."""
+
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_CFG = ctypes.POINTER(SirenCfg)
+
+# name -> argtypes; every entry point returns int32 status
+_SIGS = {
+    'siren_param_count': [_CFG, ctypes.POINTER(_I64)],
+    'siren_workspace_floats': [_CFG, ctypes.POINTER(_I64)],
+    'siren_pack': [_CFG, _P, _P, _P],
+    'siren_forward': [_CFG, _P, _P, _I64, _P, _P],
+    'siren_forward_grad': [_CFG, _P, _P, _I64, _P, _P, _P, _P],
+    'siren_train_ws_floats': [_CFG, _I64, ctypes.POINTER(_I64)],
+    'siren_backward': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P, _P],
+}
+EXPORTED = ('siren_abi_version', 'siren_last_error') + tuple(_SIGS)
+
+_lib = None
+
+
+def load():
+    """Load libsiren_amd.so once; raise ImportError (loudly) when it is missing or stale."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError('siren_amd: %s not found - build it with `python -c "import __graft_entry__ as g; '
+                          'g.build()"` (hipcc --offload-arch=gfx950). There is no CPU fallback.' % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    lib.siren_abi_version.restype = ctypes.c_int32
+    lib.siren_abi_version.argtypes = []
+    lib.siren_last_error.restype = ctypes.c_char_p
+    lib.siren_last_error.argtypes = []
+    if lib.siren_abi_version() != ABI_VERSION:
+        raise ImportError('siren_amd: ABI version mismatch (lib %d, python %d); rebuild'
+                          % (lib.siren_abi_version(), ABI_VERSION))
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = ctypes.c_int32
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc == SIREN_OK:
+        return
+    msg = '%s failed (%d): %s' % (what, rc, load().siren_last_error().decode(errors='replace'))
+    if rc == SIREN_EUNSUPPORTED:
+        raise SirenUnsupported(msg)
+    if rc == SIREN_EINVAL:
+        raise ValueError(msg)
+    raise RuntimeError(msg)

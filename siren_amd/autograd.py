@@ -1,0 +1,130 @@
+"""Autograd Functions that put the HIP kernels under the reference's autograd contract.
+
+The reference never calls its model's derivatives directly: losses call torch.autograd.grad(model_out,
+model_in, ones, create_graph=True) (diff_operators.py:42, :35) and training calls train_loss.backward()
+(training.py:96). So the fused kernels sit behind torch.autograd.Function nodes:
+
+  SirenFunction      y = Phi(x; theta)                        forward: W0 kernel, or the W1 kernel in "jet"
+                                                              mode (y and dPhi/dx in ONE launch, d_out == 1)
+    .backward(gy)    no create_graph: gx via the W1 kernel (or gy*J from jet mode), (gx, gtheta) via the
+                     W2 pipeline (fused reverse sweep + split-K MFMA weight-gradient + slab reduction)
+                     create_graph:    differentiable gx through SirenJacobian / SirenVJP nodes
+  SirenJacobian      J (jet-mode dPhi/dx, already computed by the forward launch) as a graph node
+  SirenVJP           gx = J^T gy computed by the W1 kernel as a graph node
+
+Which gradients autograd actually wants is read from the engine (torch._C._will_engine_execute_node on the
+next nodes), because ctx.needs_input_grad is static: autograd.grad(y, [x]) must not pay for weight gradients.
+
+Second- and third-order adjoints (SirenJacobian/SirenVJP.backward: the gradients_mse/sdf/laplace_mse training
+steps) are, in this round, recomputed through siren_amd._torch_path on the device — the
+HIP W3/W4 kernels are the next rows.
+"""
+import torch
+
+from . import _torch_path
+
+
+def _will_execute(ctx, i):
+    """Does the autograd engine need the gradient of tensor input i (in forward-argument order of tensors)?"""
+    try:
+        node = ctx.next_functions[i][0]
+    except (AttributeError, IndexError):
+        return True
+    if node is None:
+        return False
+    try:
+        return bool(torch._C._will_engine_execute_node(node))
+    except Exception:  # private API absent/changed: compute everything the inputs allow
+        return True
+
+
+class JetState:
+    """Per-module switch for jet mode ('auto' turns it on after the first create_graph x-gradient request)."""
+
+    def __init__(self, mode='auto'):
+        self.mode = mode
+        self.active = mode is True
+
+    def observe_x_gradient_request(self):
+        if self.mode == 'auto':
+            self.active = True
+
+
+class SirenFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, engine, jet, x, flat):
+        ws = engine.pack(flat)
+        J = None
+        use_jet = (jet is not None and jet.active and engine.cfg.d_out == 1 and engine.grad_supported
+                   and x.requires_grad)
+        if use_jet:
+            y, J = engine.forward_grad(ws, x)
+        else:
+            y = engine.forward(ws, x)
+        ctx.engine, ctx.jet, ctx.ws, ctx.J = engine, jet, ws, J
+        ctx.save_for_backward(x, flat)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, flat = ctx.saved_tensors
+        engine, ws, J = ctx.engine, ctx.ws, ctx.J
+        need_x = ctx.needs_input_grad[2] and _will_execute(ctx, 0)
+        need_p = ctx.needs_input_grad[3] and _will_execute(ctx, 1)
+        gx = gp = None
+        gy = gy.contiguous()
+        if not torch.is_grad_enabled():
+            if need_p:
+                gx, gp = engine.backward_params(ws, x, gy)
+                if not need_x:
+                    gx = None
+            elif need_x:
+                if J is not None:
+                    gx = gy * J
+                else:
+                    _, gx = engine.forward_grad(ws, x, gy, want_y=False)
+            return None, None, gx, gp
+        # create_graph=True: results must be differentiable functions of (x, theta, gy)
+        if need_x:
+            if ctx.jet is not None and not need_p:
+                ctx.jet.observe_x_gradient_request()
+            if J is not None:
+                gx = gy * SirenJacobian.apply(engine, [J], x, flat)
+            else:
+                gx = SirenVJP.apply(engine, ws, x, flat, gy)
+        if need_p:
+            gp = _torch_path.vjp_params(engine.cfg, x, flat, gy, create_graph=True)
+        return None, None, gx, gp
+
+
+class SirenJacobian(torch.autograd.Function):
+    """J(x; theta) = dPhi/dx (d_out == 1) as a graph node; the value comes from the jet-mode forward launch."""
+
+    @staticmethod
+    def forward(ctx, engine, holder, x, flat):
+        ctx.engine = engine
+        ctx.save_for_backward(x, flat)
+        return holder[0].clone()  # a fresh output tensor per node (J may feed several gradient() calls)
+
+    @staticmethod
+    def backward(ctx, gJ):
+        x, flat = ctx.saved_tensors
+        gx, gp = _torch_path.jacobian_vjp(ctx.engine.cfg, x, flat, gJ, create_graph=torch.is_grad_enabled())
+        return None, None, gx, gp
+
+
+class SirenVJP(torch.autograd.Function):
+    """gx = sum_j gy_j dPhi_j/dx as a graph node; forward is the fused W1 kernel."""
+
+    @staticmethod
+    def forward(ctx, engine, ws, x, flat, gy):
+        _, gx = engine.forward_grad(ws, x, gy, want_y=False)
+        ctx.engine = engine
+        ctx.save_for_backward(x, flat, gy)
+        return gx
+
+    @staticmethod
+    def backward(ctx, ggx):
+        x, flat, gy = ctx.saved_tensors
+        gx, gp, ggy = _torch_path.vjp_vjp(ctx.engine.cfg, x, flat, gy, ggx, create_graph=torch.is_grad_enabled())
+        return None, None, gx, gp, ggy

@@ -1,0 +1,92 @@
+// siren_common.h — shared constants and device helpers of the MI355X SIREN engine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace siren {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------------------------------------
+// Geometry of the fused H=256 kernels.
+//   * MFMA v_mfma_f32_16x16x4_f32: A = weights (16 out-neurons x 4 in-neurons), B = activations
+//     (4 in-neurons x 16 coordinates), C/D = 16 out-neurons x 16 coordinates.
+//   * One wave owns 16 coordinates; its activation tile (256 neurons x 16 coords) is 16 blocks x f32x4 in
+//     C/D layout: lane l = 16*g + c holds neuron 16*blk + 4*g + r of coordinate c in element r.
+//     That C/D tile IS the B operand of the next layer's K-step (blk, r) — no data movement between layers.
+//   * Weights stream through LDS in 16 KiB "slices": 16 K-neurons x 256 out-neurons, pre-packed by
+//     siren_pack so that lane l's A operands for 4 consecutive K-steps are one ds_read_b128 at l*16 B.
+// ---------------------------------------------------------------------------------------------------------
+constexpr int H = 256;            // hidden width of the fused kernels
+constexpr int NB = H / 16;        // neuron blocks per activation tile
+constexpr int SLICE = 16 * H;     // floats per weight slice (16 KiB)
+constexpr int NBUF = 3;           // LDS ring slots
+constexpr int WAVES = 4;          // waves per workgroup (one per SIMD)
+constexpr int THREADS = 64 * WAVES;
+constexpr int TILE = 16 * WAVES;  // coordinates per workgroup
+constexpr int MAXD = 4;           // max in_features of the fused kernels
+constexpr int MAXO = 4;           // max out_features of the fused kernels
+constexpr int MAX_LH_FWD = 8;     // max hidden layers of the forward-only kernel
+constexpr int MAX_LH_GRAD = 3;    // max hidden layers of the forward+grad kernel (cos kept in VGPRs)
+
+// Small-parameter block (head of the workspace, copied to LDS by every workgroup):
+//   [SM_W0,  +4H)  W0T[k][n] = W_0[n][k]  (k < d_in, zero padded to 4 rows)
+//   [SM_WO,  +4H)  WoT[j][n] = W_out[j][n] (j < d_out, zero padded)
+//   [SM_SEED, +H)  seed[n]   = sum_j W_out[j][n]  (vjp seed for gy == ones)
+//   [SM_BOUT, +4)  b_out
+//   [SM_BIAS, +(LH+1)H) bias[l][n], l = 0 (first layer) .. LH (last hidden layer)
+constexpr int SM_W0 = 0;
+constexpr int SM_WO = 4 * H;
+constexpr int SM_SEED = 8 * H;
+constexpr int SM_BOUT = 9 * H;
+constexpr int SM_BIAS = 9 * H + 4;
+constexpr int SMALL_MAX = SM_BIAS + (MAX_LH_FWD + 1) * H;
+
+__host__ __device__ inline int small_floats(int lh) { return SM_BIAS + (lh + 1) * H; }
+__host__ __device__ inline int64_t small_pad(int lh) { return ((int64_t)small_floats(lh) + 1023) / 1024 * 1024; }
+
+// sin/cos of a fp32 phase t = w*z, to ~1 ulp of the true values (what torch.sin/torch.cos return on the
+// reference's CPU path). Cody-Waite reduction by pi/2 with a 3-part constant (exact products for
+// |quadrant| < 2^16), then minimax polynomials on [-pi/4, pi/4]. Phases beyond 1e5 rad (never produced
+// by SIREN weights in practice) take the precise OCML path.
+__device__ __forceinline__ void sincos_phase(float t, float& sn, float& cs) {
+    if (__builtin_expect(__builtin_fabsf(t) > 1.0e5f, 0)) {
+        sn = sinf(t);
+        cs = cosf(t);
+        return;
+    }
+    const float q = __builtin_rintf(t * 0.636619772367581343f);
+    float r = __builtin_fmaf(-q, 1.5703125f, t);
+    r = __builtin_fmaf(-q, 4.837512969970703125e-4f, r);
+    r = __builtin_fmaf(-q, 7.54978995489188216e-8f, r);
+    const float r2 = r * r;
+    const float ps = __builtin_fmaf(__builtin_fmaf(-1.9515295891e-4f, r2, 8.3321608736e-3f), r2, -1.6666654611e-1f);
+    const float sr = __builtin_fmaf(ps * r2, r, r);
+    const float pc = __builtin_fmaf(__builtin_fmaf(2.443315711809948e-5f, r2, -1.388731625493765e-3f), r2,
+                                    4.166664568298827e-2f);
+    const float cr = __builtin_fmaf(pc * r2, r2, __builtin_fmaf(-0.5f, r2, 1.0f));
+    const int qi = (int)q;
+    const float sv = (qi & 1) ? cr : sr;
+    const float cv = (qi & 1) ? sr : cr;
+    sn = (qi & 2) ? -sv : sv;
+    cs = ((qi + 1) & 2) ? -cv : cv;
+}
+
+__device__ __forceinline__ float sin_phase(float t) {
+    float s, c;
+    sincos_phase(t, s, c);
+    return s;
+}
+
+// Sum over the 4 lane groups g (lanes c, c+16, c+32, c+48 hold partial sums of one coordinate).
+__device__ __forceinline__ float sum_groups(float v) {
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    return v;
+}
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+}  // namespace siren

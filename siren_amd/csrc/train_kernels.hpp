@@ -1,0 +1,157 @@
+#pragma once
+// train_kernels.hpp — weight-gradient stage of the W2 (image-fit train step) backward for gfx950.
+//
+// Replaces the reference's MmBackward grad-weight GEMMs ([H,N] x [N,H], K = N) and bias-grad sums that
+// autograd runs for train_loss.backward() (training.py:95-96) on the BatchLinear stack (modules.py:23-24).
+// Input: the per-layer sin activations a_l and deltas delta_l that the fused kernel wrote in STORE mode, in
+// the coordinate-tile layout [l][tile][neuron][16 coords] (siren_fused.hip).
+//   wgrad_kernel : dW_l = delta_l^T a_{l-1}, db_l = sum delta_l   (l = 1..LH), v_mfma_f32_16x16x4_f32, split-K
+//   small_kernel : dW_0 = delta_0^T x, db_0, dW_out = gy^T a_LH, db_out  (VALU; K = d_in / d_out <= 4)
+//   reduce_kernel: deterministic sum of the per-split partial slabs into the flat gradient (param order)
+#include "siren_common.h"
+#include "siren_params.h"
+
+namespace siren {
+
+constexpr int WG_TILE_FLOATS = H * 16;          // one 16-coordinate tile of one layer (16 KiB)
+constexpr int WG_SLOT = 2 * WG_TILE_FLOATS;     // delta tile + activation tile
+constexpr int WG_NBUF = 3;
+
+__device__ __forceinline__ void wg_issue(const float* __restrict__ dsrc, const float* __restrict__ asrc, float* ring,
+                                         int64_t t, int64_t t1, int k, int wave, int lane) {
+    if (t < t1) {
+        float* slot = ring + (k % WG_NBUF) * WG_SLOT;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int chunk = wave * 8 + q;  // 32 chunks of 1 KiB: 0..15 delta tile, 16..31 activation tile
+            const float* src = (chunk < 16 ? dsrc + t * WG_TILE_FLOATS + chunk * 256
+                                           : asrc + t * WG_TILE_FLOATS + (chunk - 16) * 256) + lane * 4;
+            __builtin_amdgcn_global_load_lds((const void*)src,
+                                             (__attribute__((address_space(3))) void*)(slot + chunk * 256), 16, 0, 0);
+        }
+    }
+}
+
+// grid (S, LH): block (s, l-1) reduces coordinate tiles [s*tps, min(T, (s+1)*tps)) of layer l.
+// Wave w owns the 128x128 quadrant (rows 128*(w>>1), cols 128*(w&1)) of the 256x256 dW_l.
+__global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restrict__ abuf,
+                                                          const float* __restrict__ dbuf, int64_t n_pad,
+                                                          int64_t tps, float* __restrict__ partial, int64_t P,
+                                                          int d, int o, int lh) {
+    __shared__ __attribute__((aligned(16))) float ring[WG_NBUF * WG_SLOT];
+    const ParamOffsets off(d, o, lh);
+    const int s = blockIdx.x, l = blockIdx.y + 1;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane >> 4, i = lane & 15;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int64_t T = n_pad / 16;
+    const int64_t t0 = (int64_t)s * tps, t1 = t0 + tps < T ? t0 + tps : T;
+    const float* dsrc = dbuf + (int64_t)l * n_pad * H;
+    const float* asrc = abuf + (int64_t)(l - 1) * n_pad * H;
+
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float bsum = 0.f;
+
+    wg_issue(dsrc, asrc, ring, t0, t1, 0, wave, lane);
+    wg_issue(dsrc, asrc, ring, t0 + 1, t1, 1, wave, lane);
+    int k = 0;
+    for (int64_t t = t0; t < t1; ++t, ++k) {
+        if (t + 1 < t1)
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        wg_issue(dsrc, asrc, ring, t + 2, t1, k + 2, wave, lane);
+        const float* sd = ring + (k % WG_NBUF) * WG_SLOT;
+        const float* sa = sd + WG_TILE_FLOATS;
+        // bias gradient: thread t owns neuron t
+        {
+            const f32x4* row = (const f32x4*)(sd + threadIdx.x * 16);
+            const f32x4 v = row[0] + row[1] + row[2] + row[3];
+            bsum += (v[0] + v[1]) + (v[2] + v[3]);
+        }
+        f32x4 av[8], bv[8];
+#pragma unroll
+        for (int rb = 0; rb < 8; ++rb) av[rb] = *(const f32x4*)(sd + (128 * wr + 16 * rb + i) * 16 + 4 * g);
+#pragma unroll
+        for (int cb = 0; cb < 8; ++cb) bv[cb] = *(const f32x4*)(sa + (128 * wc + 16 * cb + i) * 16 + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+                for (int cb = 0; cb < 8; ++cb) acc[rb][cb] = mfma4(av[rb][r], bv[cb][r], acc[rb][cb]);
+    }
+
+    float* out = partial + (int64_t)s * P;
+    float* dW = out + off.w(l);
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < 8; ++cb)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                dW[(int64_t)(128 * wr + 16 * rb + 4 * g + q) * H + 128 * wc + 16 * cb + i] = acc[rb][cb][q];
+    out[off.b(l) + threadIdx.x] = bsum;
+}
+
+// grid (S): first-layer weight/bias grads from (delta_0, x) and output-layer grads from (gy, a_LH).
+__global__ __launch_bounds__(THREADS) void small_kernel(const float* __restrict__ abuf, const float* __restrict__ dbuf,
+                                                        const float* __restrict__ x, const float* __restrict__ gy,
+                                                        int64_t n, int64_t n_pad, int64_t tps,
+                                                        float* __restrict__ partial, int64_t P, int d, int o,
+                                                        int lh) {
+    const ParamOffsets off(d, o, lh);
+    const int s = blockIdx.x, t = threadIdx.x;  // thread t owns neuron t
+    const int64_t T = n_pad / 16;
+    const int64_t t0 = (int64_t)s * tps, t1 = t0 + tps < T ? t0 + tps : T;
+    const float* d0 = dbuf;                               // delta_0
+    const float* aL = abuf + (int64_t)lh * n_pad * H;     // a_LH
+    float gw0[MAXD] = {0.f, 0.f, 0.f, 0.f}, gb0 = 0.f;
+    float gwo[MAXO] = {0.f, 0.f, 0.f, 0.f}, gbo = 0.f;
+    for (int64_t tile = t0; tile < t1; ++tile) {
+        const f32x4* drow = (const f32x4*)(d0 + tile * WG_TILE_FLOATS + t * 16);
+        const f32x4* arow = (const f32x4*)(aL + tile * WG_TILE_FLOATS + t * 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const f32x4 dv = drow[q], av = arow[q];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t c = tile * 16 + 4 * q + r;
+                if (c < n) {
+                    gb0 += dv[r];
+#pragma unroll
+                    for (int k = 0; k < MAXD; ++k)
+                        if (k < d) gw0[k] += dv[r] * x[c * d + k];
+#pragma unroll
+                    for (int j = 0; j < MAXO; ++j)
+                        if (j < o) gwo[j] += gy[c * o + j] * av[r];
+                    if (t < o) gbo += gy[c * o + t];
+                }
+            }
+        }
+    }
+    float* out = partial + (int64_t)s * P;
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k)
+        if (k < d) out[off.w0 + (int64_t)t * d + k] = gw0[k];
+    out[off.b0 + t] = gb0;
+#pragma unroll
+    for (int j = 0; j < MAXO; ++j)
+        if (j < o) out[off.wout + (int64_t)j * H + t] = gwo[j];
+    if (t < o) out[off.bout + t] = gbo;
+}
+
+__global__ void reduce_kernel(const float* __restrict__ partial, int64_t S, int64_t P, float* __restrict__ gp) {
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < P; idx += (int64_t)gridDim.x * blockDim.x) {
+        float acc = 0.f;
+        for (int64_t s = 0; s < S; ++s) acc += partial[s * P + idx];
+        gp[idx] = acc;
+    }
+}
+
+}  // namespace siren

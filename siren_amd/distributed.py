@@ -1,0 +1,69 @@
+"""Data parallelism over the coordinate batch: one process per GPU, torch.distributed over RCCL
+("nccl" backend on ROCm; "gloo" for the CPU tests).
+
+Every coordinate's value and derivatives depend only on that coordinate and the replicated weights, and every
+hot-path loss is a mean over coordinates, so with equal shards the global loss gradient is the average of the
+per-rank gradients. The only collective on the data path is ONE all-reduce of the flat weight-gradient bucket
+per step (0.79 MB for 5x256 d2; 3.2 MB for 5x512): a ring all-reduce over xGMI is latency-bound at that size,
+so the whole model's gradients travel as a single bucket rather than per-parameter calls.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_world():
+    return int(os.environ.get('WORLD_SIZE', '1')), int(os.environ.get('RANK', '0')), \
+        int(os.environ.get('LOCAL_RANK', '0'))
+
+
+def init(backend=None):
+    """Initialise the default process group from torchrun's environment (MASTER_ADDR=127.0.0.1 etc.)."""
+    world, rank, local = env_world()
+    if world <= 1 or dist.is_initialized():
+        return world, rank, local
+    if backend is None:
+        backend = 'nccl' if torch.cuda.is_available() else 'gloo'
+    if backend == 'nccl':
+        torch.cuda.set_device(local)
+    dist.init_process_group(backend=backend)
+    return world, rank, local
+
+
+def shard(n, world, rank, align=64):
+    """[start, stop) of rank's share of n coordinates; shares are multiples of `align` except the last."""
+    per = -(-n // world)
+    per = -(-per // align) * align
+    start = min(rank * per, n)
+    return start, min(start + per, n)
+
+
+def broadcast_parameters(module, src=0):
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    with torch.no_grad():
+        flat = torch.cat([p.detach().reshape(-1) for p in module.parameters()])
+        dist.broadcast(flat, src)
+        off = 0
+        for p in module.parameters():
+            p.copy_(flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+
+
+def allreduce_gradients(params, world=None):
+    """Average .grad of `params` over ranks with ONE all-reduce of a flat bucket (in place)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    world = world or dist.get_world_size()
+    params = [p for p in params if p.grad is not None]
+    if not params:
+        return
+    flat = torch.cat([p.grad.reshape(-1) for p in params])
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+    flat.div_(world)
+    off = 0
+    for p in params:
+        n = p.numel()
+        p.grad.copy_(flat[off:off + n].view_as(p.grad))
+        off += n

@@ -1,0 +1,134 @@
+"""SirenEngine: torch-side plumbing around the C ABI (include/siren_amd.h).
+
+torch supplies device memory (caching allocator) and the current HIP stream; every byte of SIREN arithmetic
+runs in libsiren_amd.so. Inputs are validated here (shape / dtype / device) before any pointer crosses the ABI,
+mirroring the reference's behaviour of raising on bad inputs (a torch shape error in BatchLinear.forward,
+modules.py:23).
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+_ALIGN = 64  # the fused kernels process coordinates in tiles of 64 (TILE in siren_common.h)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class SirenEngine:
+    """One SIREN architecture (d_in -> H x (n_hidden+1) -> d_out, sine activations) on the HIP kernels.
+
+    Parameters follow SingleBVPNet / FCBlock (modules.py:37-160) and the notebook Siren (ipynb:110-166).
+    """
+
+    def __init__(self, d_in, hidden, n_hidden, d_out, omega_first=30., omega_hidden=30., outermost_linear=True):
+        self.lib = _lib.load()
+        self.cfg = _lib.SirenCfg(int(d_in), int(hidden), int(n_hidden), int(d_out), float(omega_first),
+                                 float(omega_hidden), 1 if outermost_linear else 0, 0)
+        cnt = ctypes.c_int64()
+        _lib.check(self.lib.siren_param_count(ctypes.byref(self.cfg), ctypes.byref(cnt)), 'siren_param_count')
+        self.param_count = cnt.value
+        rc = self.lib.siren_workspace_floats(ctypes.byref(self.cfg), ctypes.byref(cnt))
+        self.supported = rc == _lib.SIREN_OK
+        self.unsupported_reason = None if self.supported else self.lib.siren_last_error().decode()
+        self.ws_floats = cnt.value if self.supported else 0
+        self.grad_supported = self.supported and 1 <= n_hidden <= 3
+
+    # ------------------------------------------------------------------------------------------------------
+    def _require(self):
+        if not self.supported:
+            raise _lib.SirenUnsupported('siren_amd fused kernels do not cover this network: %s'
+                                        % self.unsupported_reason)
+
+    def _check_x(self, x):
+        if not isinstance(x, torch.Tensor):
+            raise TypeError('coords must be a torch.Tensor')
+        if x.device.type != 'cuda':
+            raise RuntimeError('siren_amd runs on ROCm devices (MI355X) only; got a %s tensor. The CPU restatement '
+                               'of the reference lives in oracle/ and is test infrastructure.' % x.device.type)
+        if x.dtype != torch.float32:
+            raise TypeError('siren_amd computes in fp32; got %s' % x.dtype)
+        if x.dim() != 2 or x.shape[1] != self.cfg.d_in:
+            raise ValueError('coords must be (n, %d); got %s' % (self.cfg.d_in, tuple(x.shape)))
+        return x.contiguous()
+
+    def _check_params(self, flat, device):
+        if flat.dtype != torch.float32 or flat.dim() != 1 or flat.numel() != self.param_count:
+            raise ValueError('flat params must be fp32 with %d values; got %s %s'
+                             % (self.param_count, flat.dtype, tuple(flat.shape)))
+        if flat.device != device:
+            raise ValueError('params on %s but coords on %s' % (flat.device, device))
+        return flat.contiguous()
+
+    # ------------------------------------------------------------------------------------------------------
+    def pack(self, flat):
+        """Repack the flat parameter vector into the kernels' slice layout (one small kernel launch)."""
+        self._require()
+        if flat.device.type != 'cuda':
+            raise RuntimeError('siren_amd: parameters must live on a ROCm device')
+        flat = self._check_params(flat, flat.device)
+        ws = torch.empty(self.ws_floats, dtype=torch.float32, device=flat.device)
+        _lib.check(self.lib.siren_pack(ctypes.byref(self.cfg), _ptr(flat), _ptr(ws), _stream(flat.device)),
+                   'siren_pack')
+        return ws
+
+    def forward(self, ws, x, out=None):
+        """W0: y = Phi(x) for x (n, d_in) -> y (n, d_out)."""
+        self._require()
+        x = self._check_x(x)
+        n = x.shape[0]
+        y = out if out is not None else torch.empty(n, self.cfg.d_out, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_forward(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(y), _stream(x.device)),
+                   'siren_forward')
+        return y
+
+    def forward_grad(self, ws, x, gy=None, want_y=True, out_y=None, out_gx=None):
+        """W1 in one launch: y = Phi(x) and gx = sum_j gy_j dPhi_j/dx (gy=None: ones, i.e. the gradient
+        diff_operators.gradient returns, diff_operators.py:39-43)."""
+        self._require()
+        if not self.grad_supported:
+            raise _lib.SirenUnsupported('siren_forward_grad needs 1 <= num_hidden_layers <= 3')
+        x = self._check_x(x)
+        n = x.shape[0]
+        if gy is not None:
+            if gy.shape != (n, self.cfg.d_out) or gy.dtype != torch.float32 or gy.device != x.device:
+                raise ValueError('gy must be fp32 (%d, %d) on %s' % (n, self.cfg.d_out, x.device))
+            gy = gy.contiguous()
+        y = None
+        if want_y:
+            y = out_y if out_y is not None else torch.empty(n, self.cfg.d_out, dtype=torch.float32, device=x.device)
+        gx = out_gx if out_gx is not None else torch.empty(n, self.cfg.d_in, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_forward_grad(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(gy), _ptr(y),
+                                               _ptr(gx), _stream(x.device)), 'siren_forward_grad')
+        return y, gx
+
+    # ------------------------------------------------------------------------------------------------------
+    def backward_params(self, ws, x, gy):
+        """W2 backward: (gx, gparams) for one coordinate batch, gparams flat in parameter order.
+
+        Three launches: the fused forward+reverse kernel in store mode (sin activations and deltas of every
+        layer to HBM), the split-K MFMA weight-gradient kernel, and the deterministic partial-slab reduction.
+        """
+        self._require()
+        if not self.grad_supported:
+            raise _lib.SirenUnsupported('siren_backward needs 1 <= num_hidden_layers <= 3')
+        x = self._check_x(x)
+        n = x.shape[0]
+        gy = gy.contiguous()
+        cnt = ctypes.c_int64()
+        _lib.check(self.lib.siren_train_ws_floats(ctypes.byref(self.cfg), n, ctypes.byref(cnt)),
+                   'siren_train_ws_floats')
+        tws = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
+        gx = torch.empty(n, self.cfg.d_in, dtype=torch.float32, device=x.device)
+        gp = torch.empty(self.param_count, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_backward(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(gy), _ptr(tws),
+                                           ctypes.c_void_p(0), _ptr(gx), _ptr(gp), _stream(x.device)),
+                   'siren_backward')
+        return gx, gp

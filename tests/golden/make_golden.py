@@ -1,0 +1,248 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE (xvdp/siren) on CPU.
+
+Test infrastructure only.  This script is the single place that imports the read-only reference tree at
+/root/reference; it runs in the build container (never on the GPU box, where the reference does not exist)
+and writes plain .npz/.json data: inputs, weights and the reference's outputs.  No reference source is copied.
+
+Import recipe: `torchmeta/__init__.py` pulls in h5py/torchvision through its datasets package,
+so a bare package object is registered for `torchmeta` and only `torchmeta.modules` is imported from the tree.
+`training.py`/`utils.py` need tensorboard and hard-code `.cuda()`, so the fit loop of G5 is restated here,
+mirroring training.py:50-104 (Adam, sum of loss means, zero_grad, backward, step).
+
+Fixtures:
+  G1  5x256 d2 o1, seed-0 init, 4096 coords U[-1,1] (seed 1): model_out / gradient / laplace (fp32 and fp64) and
+      fp64 theta-grads of image_mse, gradients_mse, laplace_mse for fixed synthetic targets.
+  G2  same net after the 300-step G5 fit (large-derivative regime), same outputs.
+  G3  5x256 d3 o1 SDF batch (sphere, 2048 on + 2048 off surface): the four `sdf` loss terms and theta-grads.
+  G4  5x512 d3 o3, 1024 coords: model_out and image_mse theta-grads.
+  G5  config-1 trajectory: 256^2 synthetic image, 300 full-batch Adam steps (lr 1e-4), loss every 10 steps, PSNR.
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--skip-fit]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+import types
+
+import numpy as np
+import torch
+
+REF = '/root/reference'
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def import_reference():
+    if not os.path.isdir(REF):
+        raise SystemExit('make_golden.py needs the reference tree at %s (build container only)' % REF)
+    pkg = types.ModuleType('torchmeta')
+    pkg.__path__ = [os.path.join(REF, 'torchmeta')]
+    sys.modules['torchmeta'] = pkg
+    sys.path.insert(0, REF)
+    import modules, diff_operators, loss_functions  # noqa: E401
+    return modules, diff_operators, loss_functions
+
+
+def synth_image(coords):
+    """Closed-form synthetic image on [-1,1]^2: 0.6*(sin 8x cos 5y + 0.5 sign(sin 20xy))."""
+    x, y = coords[..., 0:1], coords[..., 1:2]
+    return 0.6 * (torch.sin(8 * x) * torch.cos(5 * y) + 0.5 * torch.sign(torch.sin(20 * x * y)))
+
+
+def psnr(pred, gt):
+    """PSNR as utils.py:578-587 (skimage compare_psnr, data_range=1) on the [-1,1] -> [0,1] mapping."""
+    p = np.clip(pred / 2. + 0.5, 0., 1.)
+    t = gt / 2. + 0.5
+    mse = np.mean((p.astype(np.float64) - t.astype(np.float64)) ** 2)
+    return float(10. * np.log10(1. / mse))
+
+
+def state_to_np(sd):
+    return {k: v.detach().cpu().numpy().astype(np.float32) for k, v in sd.items()}
+
+
+def grads_of(net, loss_dict):
+    net.zero_grad()
+    total = 0.
+    for v in loss_dict.values():
+        total = total + v.mean()
+    total.backward()
+    return {k: (p.grad.detach().cpu().numpy() if p.grad is not None else np.zeros(tuple(p.shape))).astype(np.float32)
+            for k, p in net.named_parameters()}, float(total)
+
+
+def eval_net(modules, D, net, coords, dtype):
+    net = net.to(dtype)
+    out = net({'coords': coords.to(dtype)})
+    y = out['model_out']
+    g = D.gradient(y, out['model_in'])
+    lap = D.laplace(y, out['model_in'])
+    return out, y, g, lap
+
+
+def fixture_outputs(modules, D, L, net, coords, targets, prefix, store, meta, losses=('image_mse', 'gradients_mse', 'laplace_mse')):
+    res = {}
+    for dtype, tag in ((torch.float32, 'f32'), (torch.float64, 'f64')):
+        out, y, g, lap = eval_net(modules, D, net, coords, dtype)
+        res[tag] = (y.detach().numpy(), g.detach().numpy(), lap.detach().numpy())
+        store[f'{prefix}_model_out_{tag}'] = y.detach().numpy().astype(np.float64 if tag == 'f64' else np.float32)
+        store[f'{prefix}_gradient_{tag}'] = g.detach().numpy().astype(np.float64 if tag == 'f64' else np.float32)
+        store[f'{prefix}_laplace_{tag}'] = lap.detach().numpy().astype(np.float64 if tag == 'f64' else np.float32)
+        if tag == 'f64':
+            gt = {k: v.to(torch.float64) for k, v in targets.items()}
+            for lname in losses:
+                fn = getattr(L, lname)
+                if lname == 'image_mse':
+                    fn = (lambda f: (lambda mo, g: f(None, mo, g)))(fn)
+                out = net({'coords': coords.to(torch.float64)})
+                grads, total = grads_of(net, fn(out, gt))
+                for k, v in grads.items():
+                    store[f'{prefix}_{lname}_grad_{k}'] = v
+                meta[f'{prefix}_{lname}_loss_f64'] = total
+    net.float()
+    for name, idx in (('model_out', 0), ('gradient', 1), ('laplace', 2)):
+        a32, a64 = res['f32'][idx], res['f64'][idx]
+        meta[f'{prefix}_{name}_f32_vs_f64_maxabs'] = float(np.max(np.abs(a32 - a64)))
+        meta[f'{prefix}_{name}_f64_maxabs'] = float(np.max(np.abs(a64)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--skip-fit', action='store_true', help='reuse the G5 weights already in golden_fit.npz')
+    args = ap.parse_args()
+    modules, D, L = import_reference()
+    torch.set_num_threads(os.cpu_count())
+    meta = {'torch': torch.__version__, 'generated_by': 'tests/golden/make_golden.py', 'reference': REF}
+
+    # ---------------- G5: config-1 fit (also provides the G2 weights) -----------------
+    fit_path = os.path.join(OUT, 'golden_fit.npz')
+    grid = get_grid = None
+    side = 256
+    # get_mgrid restated inline (dataio.py:20-40 needs skimage/torchvision at import): ij order, /(s-1), -0.5, *2
+    ii, jj = np.mgrid[:side, :side]
+    grid = np.stack([ii, jj], -1).astype(np.float32)
+    grid[..., 0] /= (side - 1)
+    grid[..., 1] /= (side - 1)
+    grid -= 0.5
+    grid *= 2.
+    grid = torch.from_numpy(grid.reshape(1, -1, 2))
+    img = synth_image(grid)
+    if args.skip_fit and os.path.exists(fit_path):
+        fit = dict(np.load(fit_path))
+        trained = {k[len('w_'):]: torch.from_numpy(v) for k, v in fit.items() if k.startswith('w_')}
+        meta['G5_fit_seconds'] = float(fit['fit_seconds']) if 'fit_seconds' in fit else None
+        torch.manual_seed(0)
+        net = modules.SingleBVPNet(type='sine', in_features=2, out_features=1)
+        net.load_state_dict(trained)
+        with torch.no_grad():
+            final = net({'coords': grid})['model_out'].numpy()
+        meta['G5_psnr_final'] = psnr(final, img.numpy())
+        meta['G5_loss_final_eval'] = float(np.mean((final - img.numpy()) ** 2))
+    else:
+        torch.manual_seed(0)
+        net = modules.SingleBVPNet(type='sine', in_features=2, out_features=1)
+        init_sd = state_to_np(net.state_dict())
+        optim = torch.optim.Adam(lr=1e-4, params=net.parameters())
+        losses, t0 = [], time.time()
+        for step in range(300):
+            out = net({'coords': grid})
+            ld = L.image_mse(None, out, {'img': img})
+            train_loss = 0.
+            for v in ld.values():
+                train_loss += v.mean()
+            losses.append(float(train_loss))
+            optim.zero_grad()
+            train_loss.backward()
+            optim.step()
+        with torch.no_grad():
+            final = net({'coords': grid})['model_out'].numpy()
+        meta['G5_fit_seconds'] = time.time() - t0
+        meta['G5_psnr_final'] = psnr(final, img.numpy())
+        meta['G5_loss_final_eval'] = float(np.mean((final - img.numpy()) ** 2))
+        trained = {k: v.detach().clone() for k, v in net.state_dict().items()}
+        np.savez_compressed(fit_path, losses=np.array(losses, np.float64), fit_seconds=meta['G5_fit_seconds'],
+                            **{'w_' + k: v.numpy() for k, v in trained.items()},
+                            **{'init_' + k: v for k, v in init_sd.items()})
+        print('G5 fit done in %.1fs, psnr %.3f' % (meta['G5_fit_seconds'], meta['G5_psnr_final']))
+
+    # ---------------- G1 / G2: 5x256 d2 o1 -----------------
+    gen = torch.Generator().manual_seed(1)
+    coords = torch.rand(1, 4096, 2, generator=gen) * 2 - 1
+    gt = {'img': synth_image(coords),
+          'gradients': torch.randn(1, 4096, 2, generator=gen) * 10.,
+          'laplace': torch.randn(1, 4096, 1, generator=gen) * 100.}
+    store = {'coords': coords.numpy(), 'gt_img': gt['img'].numpy(), 'gt_gradients': gt['gradients'].numpy(),
+             'gt_laplace': gt['laplace'].numpy()}
+    torch.manual_seed(0)
+    net = modules.SingleBVPNet(type='sine', in_features=2, out_features=1)
+    meta['state_dict_keys_5x256_d2'] = list(net.state_dict().keys())
+    for k, v in state_to_np(net.state_dict()).items():
+        store['w_' + k] = v
+    fixture_outputs(modules, D, L, net, coords, gt, 'G1', store, meta)
+    np.savez_compressed(os.path.join(OUT, 'golden_g1.npz'), **store)
+
+    store = {}
+    net.load_state_dict(trained)
+    for k, v in state_to_np(net.state_dict()).items():
+        store['w_' + k] = v
+    fixture_outputs(modules, D, L, net, coords, gt, 'G2', store, meta)
+    np.savez_compressed(os.path.join(OUT, 'golden_g2.npz'), **store)
+
+    # ---------------- G3: SDF batch, 5x256 d3 o1 -----------------
+    gen = torch.Generator().manual_seed(3)
+    on = torch.randn(2048, 3, generator=gen, dtype=torch.float64)
+    on_n = on / on.norm(dim=-1, keepdim=True)
+    on_c = (on_n * 0.5)
+    off_c = torch.rand(2048, 3, generator=gen, dtype=torch.float64) * 2 - 1
+    coords3 = torch.cat([on_c, off_c], 0).float()[None]
+    normals = torch.cat([on_n, -torch.ones(2048, 3, dtype=torch.float64)], 0).float()[None]
+    sdf = torch.cat([torch.zeros(2048, 1), -torch.ones(2048, 1)], 0)[None]
+    store = {'coords': coords3.numpy(), 'gt_sdf': sdf.numpy(), 'gt_normals': normals.numpy()}
+    torch.manual_seed(0)
+    net3 = modules.SingleBVPNet(type='sine', in_features=3, out_features=1)
+    for k, v in state_to_np(net3.state_dict()).items():
+        store['w_' + k] = v
+    for dtype, tag in ((torch.float32, 'f32'), (torch.float64, 'f64')):
+        net3 = net3.to(dtype)
+        out = net3({'coords': coords3.to(dtype)})
+        ld = L.sdf(out, {'sdf': sdf.to(dtype), 'normals': normals.to(dtype)})
+        for k, v in ld.items():
+            meta[f'G3_sdf_{k}_{tag}'] = float(v)
+        store[f'G3_model_out_{tag}'] = out['model_out'].detach().numpy()
+        store[f'G3_gradient_{tag}'] = D.gradient(out['model_out'], out['model_in']).detach().numpy()
+        if tag == 'f64':
+            grads, total = grads_of(net3, ld)
+            meta['G3_sdf_total_f64'] = total
+            for k, v in grads.items():
+                store[f'G3_sdf_grad_{k}'] = v
+    np.savez_compressed(os.path.join(OUT, 'golden_g3.npz'), **store)
+
+    # ---------------- G4: 5x512 d3 o3 -----------------
+    gen = torch.Generator().manual_seed(4)
+    coords4 = torch.rand(1, 1024, 3, generator=gen) * 2 - 1
+    gt4 = 0.5 + 0.5 * torch.sin(3 * coords4 + torch.tensor([0., 1., 2.]))
+    store = {'coords': coords4.numpy(), 'gt_img': gt4.numpy()}
+    torch.manual_seed(0)
+    net4 = modules.SingleBVPNet(type='sine', in_features=3, out_features=3, hidden_features=512, num_hidden_layers=3)
+    for k, v in state_to_np(net4.state_dict()).items():
+        store['w_' + k] = v
+    for dtype, tag in ((torch.float32, 'f32'), (torch.float64, 'f64')):
+        net4 = net4.to(dtype)
+        out = net4({'coords': coords4.to(dtype)})
+        store[f'G4_model_out_{tag}'] = out['model_out'].detach().numpy()
+        store[f'G4_gradient_{tag}'] = D.gradient(out['model_out'], out['model_in']).detach().numpy()
+        if tag == 'f64':
+            grads, total = grads_of(net4, L.image_mse(None, out, {'img': gt4.to(dtype)}))
+            meta['G4_image_mse_f64'] = total
+            for k, v in grads.items():
+                store[f'G4_image_mse_grad_{k}'] = v
+    np.savez_compressed(os.path.join(OUT, 'golden_g4.npz'), **store)
+
+    with open(os.path.join(OUT, 'manifest.json'), 'w') as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print(json.dumps(meta, indent=1, sort_keys=True))
+
+
+if __name__ == '__main__':
+    main()
