@@ -1,0 +1,232 @@
+"""bench.py — the headline benchmark: Mcoords/s of the fused 5x256 SIREN forward + coordinate gradient (W1).
+
+Workload (BASELINE.json configs[1]): SingleBVPNet defaults (d_in 2, hidden 256, 3 hidden layers, out 1, w0 30),
+N = 2^20 uniform random 2-D coordinates per GPU per step (weak scaling), seed-0 reference-distributed weights.
+One step = repack the weights (siren_pack) + ONE fused fwd+grad launch (siren_forward_grad: y and dPhi/dx)
+over the GPU's whole batch, inputs resident in HBM. N GPUs: one process per GPU (torchrun), coordinates
+sharded per rank with no collective on the data path (the W1 path has no exchange step); the timed region is
+bracketed by barrier + synchronize and the max over ranks is used.
+
+Also reported: roofline of the fused kernel (HIP events on the launch stream), the oracle's CPU restatement
+timed on the host cores (cpu_baseline), a short W2 training-step rate and the PSNR of a 300-step image fit
+against the reference's (tests/golden manifest), all on the same JSON line.
+
+python bench.py [--gpus N] [--steps K] [--warmup W] [--n COORDS] [--no-cpu] [--no-extra]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense peak (measured 155)
+HBM_PEAK_GBS = 8000.
+H, LH, D_IN, D_OUT = 256, 3, 2, 1
+F_PER_COORD = 2 * (D_IN * H + LH * H * H + H * D_OUT)   # 394,752 FLOP
+W1_FLOP = 2 * F_PER_COORD                             # 789,504 FLOP / coord
+REF_PSNR_DB = 39.13                                    # BASELINE.md §2 (reference, 300 steps, CPU)
+
+
+def seed0_params(device):
+    """Reference-distributed weights (modules.py:622-635 + nn.Linear bias init), generated on the host."""
+    from siren_amd.modules import FCBlock
+    torch.manual_seed(0)
+    net = FCBlock(D_IN, D_OUT, LH, H, outermost_linear=True, nonlinearity='sine')
+    return torch.cat([p.detach().reshape(-1) for p in net.parameters()]).to(device)
+
+
+def cpu_baseline(seconds=15.):
+    """The oracle's torch restatement (reference op sequence + autograd gradient) on the host cores."""
+    from oracle import siren_oracle as O
+    torch.manual_seed(0)
+    dims = [D_IN] + [H] * (LH + 1) + [D_OUT]
+    params = []
+    for i, (fi, fo) in enumerate(zip(dims[:-1], dims[1:])):
+        bound = 1. / fi if i == 0 else np.sqrt(6. / fi) / 30.
+        params += [((torch.rand(fo, fi) * 2 - 1) * bound), ((torch.rand(fo) * 2 - 1) / np.sqrt(fi))]
+    n = 1 << 15
+    x0 = torch.rand(1, n, D_IN) * 2 - 1
+    done, t0 = 0, time.perf_counter()
+    while True:
+        x = x0.clone().requires_grad_(True)
+        y = O.torch_forward(x, params)
+        g = O.torch_gradient(y, x)
+        _ = float(g.sum())
+        done += n
+        el = time.perf_counter() - t0
+        if el > seconds:
+            break
+    return {'value': round(done / el / 1e6, 4), 'unit': 'Mcoords/s', 'cores': torch.get_num_threads(),
+            'kind': 'port',
+            'sample': '%d x %d coords (5x256 d2 o1, fwd + autograd gradient, torch CPU fp32, %.1f s)'
+                      % (done // n, n, el)}
+
+
+def kernel_roofline(eng, ws, x, reps=10):
+    """Average duration of the fused W1 launch from HIP events on the stream it is enqueued on."""
+    st = torch.cuda.current_stream()
+    y = torch.empty(x.shape[0], 1, device=x.device)
+    gx = torch.empty_like(x)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record(st)
+        eng.forward_grad(ws, x, out_y=y, out_gx=gx)
+        b.record(st)
+    torch.cuda.synchronize()
+    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    achieved = W1_FLOP * x.shape[0] / (ms * 1e-3) / 1e12
+    return ms, achieved
+
+
+def pmc_traffic(n):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/*_pmc.json), if it matches."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, 'profiles', '*pmc*.json')), reverse=True):
+        try:
+            rec = json.load(open(path))
+        except Exception:
+            continue
+        k = rec.get('kernels', {}).get('fused_kernel<3,true,false>')
+        if k and rec.get('n') == n:
+            return k.get('hbm_bytes_per_launch')
+    return None
+
+
+def train_step_rate(device, n=1 << 18, steps=5):
+    """W2: image_mse training steps (fused forward, fused backward + MFMA wgrad, Adam) in Mcoords/s."""
+    from siren_amd.modules import SingleBVPNet
+    torch.manual_seed(0)
+    model = SingleBVPNet(verbose=False, jet=False).to(device)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    x = torch.rand(1, n, 2, device=device) * 2 - 1
+    gt = torch.sin(5 * x[..., :1])
+    def step():
+        out = model({'coords': x})
+        loss = ((out['model_out'] - gt) ** 2).mean()
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    return n * steps / (time.perf_counter() - t0) / 1e6
+
+
+def psnr_fit(device, steps=300):
+    """Config-1 fit (256^2 synthetic image, full batch, Adam lr 1e-4, image_mse) on the fused engine."""
+    from siren_amd.modules import SingleBVPNet
+    from siren_amd import dataio
+    torch.manual_seed(0)
+    model = SingleBVPNet(verbose=False, jet=False).to(device)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    grid = dataio.get_mgrid(256)[None].to(device)
+    img = dataio.synthetic_image(grid)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = model({'coords': grid})
+        loss = ((out['model_out'] - img) ** 2).mean()
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    with torch.no_grad():
+        pred = model({'coords': grid})['model_out']
+    torch.cuda.synchronize()
+    return dataio.psnr(pred, img), time.perf_counter() - t0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--n', type=int, default=1 << 20, help='coordinates per GPU per step')
+    ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--no-extra', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl')
+    device = torch.device('cuda', local)
+
+    import __graft_entry__
+    __graft_entry__.build()
+    from siren_amd.engine import SirenEngine
+    eng = SirenEngine(D_IN, H, LH, D_OUT)
+    flat = seed0_params(device)
+    g = torch.Generator(device='cpu').manual_seed(1000 + rank)
+    x = (torch.rand(args.n, D_IN, generator=g) * 2 - 1).to(device)
+    y = torch.empty(args.n, D_OUT, device=device)
+    gx = torch.empty_like(x)
+
+    def step():
+        ws = eng.pack(flat)
+        eng.forward_grad(ws, x, out_y=y, out_gx=gx)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    value = world * args.n * args.steps / el / 1e6
+
+    ws = eng.pack(flat)
+    kms, achieved = kernel_roofline(eng, ws, x)
+    extra = {}
+    if rank == 0 and not args.no_extra:
+        extra['w2_image_mse_train_mcoords_s'] = round(train_step_rate(device), 3)
+        p, secs = psnr_fit(device)
+        extra['psnr_db'] = {'value': round(p, 3), 'reference_cpu': REF_PSNR_DB, 'steps': 300,
+                            'fit_seconds': round(secs, 2)}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline()
+
+    if rank == 0:
+        traffic = pmc_traffic(args.n)
+        line = {
+            'metric': 'Mcoords/sec fwd+∇ (5×256 SIREN) at 1/2/4/8 MI355X; PSNR vs ref',
+            'value': round(value, 3), 'unit': 'Mcoords/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(el / args.steps * 1e3, 4), 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
+            'config': {'workload': 'W1 fused fwd+grad, SingleBVPNet 5x256 (d_in 2, 3 hidden, out 1, w0 30), '
+                                   'N=%d random coords per GPU per step' % args.n,
+                       'coords_per_gpu': args.n, 'parallelism': 'dp%d' % world},
+            'roofline': {'bound': 'mfma', 'achieved': round(achieved, 3), 'peak': PEAK_FP32_MFMA_TFLOPS,
+                         'unit': 'TFLOP/s', 'frac': round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
+                         'traffic': traffic, 'kernel_ms': round(kms, 4),
+                         'flop_per_coord': W1_FLOP},
+            'cpu_baseline': cpu,
+        }
+        line.update(extra)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()
