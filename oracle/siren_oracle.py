@@ -198,5 +198,6 @@ def torch_param_grads(name, x, layers, gt, dtype='float64', **kw):
     gtt = {k: torch.tensor(np.asarray(v), dtype=dt) for k, v in gt.items()}
     terms = torch_loss_terms(name, y, xt, gtt)
     total = sum(v.mean() for v in terms.values())
-    grads = torch.autograd.grad(total, params)
+    grads = torch.autograd.grad(total, params, allow_unused=True)
+    grads = [torch.zeros_like(p) if g is None else g for g, p in zip(grads, params)]
     return np.concatenate([g.detach().numpy().reshape(-1) for g in grads]), float(total)

@@ -1,0 +1,69 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, 'tests', 'golden')
+sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs an MI355X (ROCm device) and libsiren_amd.so')
+    config.addinivalue_line('markers', 'slow: long-running (still part of the default selection)')
+
+
+def load_golden(name):
+    path = os.path.join(GOLDEN, 'golden_%s.npz' % name)
+    if not os.path.exists(path):
+        pytest.skip('golden fixture %s missing (run tests/golden/make_golden.py in the build container)' % name)
+    return dict(np.load(path))
+
+
+@pytest.fixture(scope='session')
+def g1():
+    return load_golden('g1')
+
+
+@pytest.fixture(scope='session')
+def g2():
+    return load_golden('g2')
+
+
+@pytest.fixture(scope='session')
+def g3():
+    return load_golden('g3')
+
+
+@pytest.fixture(scope='session')
+def g4():
+    return load_golden('g4')
+
+
+@pytest.fixture(scope='session')
+def manifest():
+    import json
+    with open(os.path.join(GOLDEN, 'manifest.json')) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope='session')
+def cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no ROCm device')
+    import __graft_entry__
+    __graft_entry__.build()
+    return torch.device('cuda:0')
+
+
+def weights_of(fx):
+    """Fixture weights as a flat fp32 vector in state_dict order, plus the (W, b) list."""
+    from oracle import siren_oracle as O
+    layers = O.layers_from_state(fx)
+    return O.flatten(layers).astype(np.float32), layers
+
+
+def g1_layers(fx):
+    return weights_of(fx)[1]

@@ -1,0 +1,81 @@
+"""Data parallelism over coordinates with world_size 2 on the gloo backend (CPU).
+
+The sharded path must reproduce the single-process full-batch gradient: each rank takes an equal coordinate
+shard, computes its local mean-loss gradient, and ONE all-reduce of the flat bucket averages them; the clip
+then runs on the reduced gradient. The model here is the non-sine FCBlock (plain torch layers run on CPU);
+the fused-kernel DP path is the same code with the 'nccl' (RCCL) backend, exercised by bench.py --gpus N.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, ret):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from siren_amd import distributed as sd
+    from siren_amd.modules import SingleBVPNet
+    sd.init('gloo')
+    torch.manual_seed(rank + 5)        # deliberately different init per rank: broadcast must fix it
+    m = SingleBVPNet(type='tanh', hidden_features=32, num_hidden_layers=2, verbose=False)
+    sd.broadcast_parameters(m)
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(1, 1000, 2, generator=g) * 2 - 1
+    t = torch.sin(3 * x[..., :1])
+    a, b = sd.shard(1000, world, rank, align=100)
+    out = m({'coords': x[:, a:b]})
+    loss = ((out['model_out'] - t[:, a:b]) ** 2).mean()
+    loss.backward()
+    sd.allreduce_gradients(list(m.parameters()))
+    torch.nn.utils.clip_grad_norm_(m.parameters(), max_norm=1e-3)
+    ret[rank] = torch.cat([p.grad.reshape(-1) for p in m.parameters()]).clone()
+    ret['p%d' % rank] = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).clone()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_gloo_world2_matches_full_batch():
+    world, port = 2, _free_port()
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_worker, args=(world, port, ret), nprocs=world, join=True)
+    assert torch.equal(ret['p0'], ret['p1'])
+    assert torch.allclose(ret[0], ret[1])
+    from siren_amd.modules import SingleBVPNet
+    torch.manual_seed(5)
+    m = SingleBVPNet(type='tanh', hidden_features=32, num_hidden_layers=2, verbose=False)
+    with torch.no_grad():
+        off = 0
+        for p in m.parameters():
+            p.copy_(ret['p0'][off:off + p.numel()].view_as(p))
+            off += p.numel()
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(1, 1000, 2, generator=g) * 2 - 1
+    t = torch.sin(3 * x[..., :1])
+    loss = ((m({'coords': x})['model_out'] - t) ** 2).mean()
+    loss.backward()
+    torch.nn.utils.clip_grad_norm_(m.parameters(), max_norm=1e-3)
+    ref = torch.cat([p.grad.reshape(-1) for p in m.parameters()])
+    assert torch.allclose(ret[0], ref, atol=1e-7, rtol=1e-5)
+
+
+def test_shard_covers_range():
+    from siren_amd.distributed import shard
+    for n in (1, 63, 64, 1000, 1 << 20):
+        for world in (1, 2, 3, 8):
+            parts = [shard(n, world, r) for r in range(world)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            for (a, b), (c, d) in zip(parts[:-1], parts[1:]):
+                assert b == c and a <= b

@@ -1,0 +1,132 @@
+"""Host-side checks that need no GPU: the C ABI library loads and exports every symbol include/siren_amd.h
+declares, host-only ABI queries, module API / parameter names / init parity with the reference, the product
+path refusing CPU tensors, get_mgrid."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, 'include', 'siren_amd.h')).read()
+    return sorted(set(re.findall(r'^\s*(?:int32_t|const char\*)\s+(siren_\w+)\s*\(', src, re.M)))
+
+
+@pytest.fixture(scope='module')
+def lib():
+    import __graft_entry__
+    __graft_entry__.build()
+    from siren_amd import _lib
+    return _lib.load()
+
+
+def test_library_exports_every_header_symbol(lib):
+    names = header_functions()
+    assert len(names) >= 9, names
+    for n in names:
+        assert hasattr(lib, n), n
+    from siren_amd import _lib
+    assert set(names) == set(_lib.EXPORTED)
+
+
+def test_library_is_gfx950_code_object():
+    import subprocess
+    so = os.path.join(ROOT, 'siren_amd', 'libsiren_amd.so')
+    out = subprocess.run(['/opt/rocm/lib/llvm/bin/llvm-readelf', '-S', so], capture_output=True, text=True).stdout
+    assert '.hip_fatbin' in out
+
+
+def test_param_count_and_workspace(lib):
+    from siren_amd import _lib
+    cfg = _lib.SirenCfg(2, 256, 3, 1, 30., 30., 1, 0)
+    c = ctypes.c_int64()
+    assert lib.siren_param_count(ctypes.byref(cfg), ctypes.byref(c)) == 0 and c.value == 198401
+    assert lib.siren_workspace_floats(ctypes.byref(cfg), ctypes.byref(c)) == 0
+    assert c.value == 4096 + 2 * 3 * 16 * 4096
+    assert lib.siren_train_ws_floats(ctypes.byref(cfg), 1000, ctypes.byref(c)) == 0 and c.value > 0
+    bad = _lib.SirenCfg(2, 128, 3, 1, 30., 30., 1, 0)
+    assert lib.siren_workspace_floats(ctypes.byref(bad), ctypes.byref(c)) == _lib.SIREN_EUNSUPPORTED
+    assert b'256' in lib.siren_last_error()
+    assert lib.siren_param_count(None, ctypes.byref(c)) == _lib.SIREN_EINVAL
+    wide = _lib.SirenCfg(3, 512, 3, 3, 30., 30., 1, 0)
+    assert lib.siren_param_count(ctypes.byref(wide), ctypes.byref(c)) == 0 and c.value == 791555
+
+
+def test_zero_coords_is_a_noop(lib):
+    from siren_amd import _lib
+    cfg = _lib.SirenCfg(2, 256, 3, 1, 30., 30., 1, 0)
+    assert lib.siren_forward(ctypes.byref(cfg), None, None, 0, None, None) == 0
+    assert lib.siren_forward(ctypes.byref(cfg), None, None, -1, None, None) == _lib.SIREN_EINVAL
+
+
+def test_state_dict_keys_and_seed0_init_match_reference(g1, manifest):
+    from siren_amd.modules import SingleBVPNet
+    torch.manual_seed(0)
+    m = SingleBVPNet(type='sine', in_features=2, out_features=1, verbose=False)
+    sd = m.state_dict()
+    assert list(sd.keys()) == manifest['state_dict_keys_5x256_d2']
+    for k, v in sd.items():
+        assert np.array_equal(v.numpy(), g1['w_' + k]), k   # bit-identical RNG replay of the reference init
+
+
+def test_g4_init_matches(g4):
+    from siren_amd.modules import SingleBVPNet
+    torch.manual_seed(0)
+    m = SingleBVPNet(out_features=3, in_features=3, hidden_features=512, num_hidden_layers=3, verbose=False)
+    for k, v in m.state_dict().items():
+        assert np.array_equal(v.numpy(), g4['w_' + k]), k
+
+
+def test_cpu_tensors_are_refused():
+    from siren_amd.modules import SingleBVPNet
+    m = SingleBVPNet(verbose=False)
+    with pytest.raises(RuntimeError, match='ROCm'):
+        m({'coords': torch.zeros(1, 10, 2)})
+
+
+def test_unsupported_modes_raise():
+    from siren_amd.modules import SingleBVPNet
+    from siren_amd._lib import SirenUnsupported
+    with pytest.raises(SirenUnsupported):
+        SingleBVPNet(mode='nerf', verbose=False)
+
+
+def test_notebook_siren_api():
+    from siren_amd.modules import Siren, SineLayer
+    torch.manual_seed(0)
+    s = Siren(2, 64, 2, 1, outermost_linear=True, first_omega_0=30, hidden_omega_0=30.)
+    keys = list(s.state_dict().keys())
+    assert keys[0] == 'net.0.linear.weight' and keys[-1] == 'net.3.bias'
+    assert isinstance(s.net[0], SineLayer) and s.net[0].is_first
+    assert float(s.net[0].linear.weight.abs().max()) <= 0.5
+
+
+def test_relu_baseline_runs_on_cpu():
+    """Non-sine baselines keep the reference's plain torch layers (not the SIREN hot path)."""
+    from siren_amd.modules import SingleBVPNet
+    m = SingleBVPNet(type='relu', verbose=False)
+    out = m({'coords': torch.rand(1, 5, 2)})
+    assert out['model_out'].shape == (1, 5, 1) and out['model_in'].requires_grad
+
+
+def test_get_subdict():
+    from collections import OrderedDict
+    from siren_amd.modules import get_subdict
+    d = OrderedDict([('net.0.weight', 1), ('net.0.bias', 2), ('net.10.weight', 3), ('other', 4)])
+    assert get_subdict(d, 'net.0') == OrderedDict([('weight', 1), ('bias', 2)])
+    assert get_subdict(d, None) is d and get_subdict(None, 'x') is None
+
+
+def test_get_mgrid_matches_reference_formula():
+    from siren_amd.dataio import get_mgrid
+    g = get_mgrid(256)
+    assert g.shape == (65536, 2) and g.dtype == torch.float32
+    assert torch.allclose(g[1], torch.tensor([-1., -0.99215686]))
+    assert float(g.min()) == -1. and float(g.max()) == 1.
+    g3 = get_mgrid((1, 4, 5), 3)
+    assert g3.shape == (20, 3) and float(g3[:, 0].max()) == -1.   # dim 0 divides by max(s0 - 1, 1)
