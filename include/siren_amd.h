@@ -47,6 +47,12 @@ enum {
     SIREN_EHIP = 3          /* a HIP runtime error (launch failure, ...)               */
 };
 
+/* cfg.reserved flags (benchmarking only): run the round-1 kernel whose sin/cos epilogues are not
+ * interleaved with the MFMA stream, for in-process A/B timing. */
+#define SIREN_FLAG_LEGACY_KERNEL 1
+/* ... and an alternative instruction schedule of the W1 kernel (sched_group_barrier interleave). */
+#define SIREN_FLAG_ALT_SCHEDULE 2
+
 /* Network description. Mirrors SingleBVPNet(out_features, type='sine', in_features, mode='mlp',
  * hidden_features, num_hidden_layers) (modules.py:122-123) and the notebook Siren(in_features,
  * hidden_features, hidden_layers, out_features, outermost_linear, first_omega_0, hidden_omega_0). */
@@ -58,7 +64,7 @@ typedef struct siren_cfg {
     float omega_first;        /* w of the first sine layer (30; Sine hard-codes 30)        */
     float omega_hidden;       /* w of the hidden sine layers (30)                          */
     int32_t outermost_linear; /* 1: last layer linear (SingleBVPNet); 0: sin(w*z) as well  */
-    int32_t reserved;
+    int32_t reserved;         /* flags: 0 for normal use; SIREN_FLAG_LEGACY_KERNEL = A/B   */
 } siren_cfg;
 
 /* Library ABI version (== SIREN_ABI_VERSION). */

@@ -131,20 +131,6 @@ __device__ __forceinline__ void layer_mma(const float* __restrict__ stream, floa
     }
 }
 
-// STORE-mode writers: element (neuron 16*rb + 4*g + r, coord c) of a 16-coordinate tile lives at
-// neuron*16 + c, so lane (g, c) writes 4 floats 64 B apart per block; p already points at 4*g*16 + c.
-__device__ __forceinline__ void store_block(float* p, int rb, const f32x4& v) {
-    p += 16 * rb * 16;
-    p[0] = v[0];
-    p[16] = v[1];
-    p[32] = v[2];
-    p[48] = v[3];
-}
-__device__ __forceinline__ void store_tile(float* p, const f32x4 (&v)[NB]) {
-#pragma unroll
-    for (int rb = 0; rb < NB; ++rb) store_block(p, rb, v[rb]);
-}
-
 // Hidden-layer epilogue: z = acc + b; t = w z; act = sin(t); cs = cos(t)  (modules.py:24, :34).
 __device__ __forceinline__ void epilogue_sincos(const f32x4 (&acc)[NB], const float* bl, float w, f32x4 (&act)[NB],
                                                 f32x4 (&cs)[NB]) {

@@ -2,6 +2,7 @@
 // kernel launches. Single translation unit over the kernel headers.
 #include "fused_kernels.hpp"
 #include "train_kernels.hpp"
+#include "w1_kernel.hpp"
 // ==========================================================================================================
 // C ABI
 // ==========================================================================================================
@@ -125,6 +126,26 @@ int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x
     if (blocks > 0x7fffffffll) return fail(SIREN_EINVAL, "n too large");
     const dim3 grid((unsigned)blocks), block(siren::THREADS);
     const int fs = cfg->outermost_linear ? 0 : 1;
+    const bool legacy = (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) != 0 || fs;
+    if (!legacy) {
+#define SIREN_LAUNCH_W1(LHV)                                                                                    \
+    hipLaunchKernelGGL((siren::w1_kernel<LHV, false>), grid, block, 0, (hipStream_t)stream, ws, x, n, gy, y, gx, \
+                       cfg->d_in, cfg->d_out, cfg->omega_first, cfg->omega_hidden, (float*)nullptr, (float*)nullptr, \
+                       (int64_t)0)
+        if (cfg->n_hidden == 3 && (cfg->reserved & SIREN_FLAG_ALT_SCHEDULE)) {
+            hipLaunchKernelGGL((siren::w1_kernel<3, false, 1>), grid, block, 0, (hipStream_t)stream, ws, x, n, gy, y,
+                               gx, cfg->d_in, cfg->d_out, cfg->omega_first, cfg->omega_hidden, (float*)nullptr,
+                               (float*)nullptr, (int64_t)0);
+            return hip_status("siren_forward_grad");
+        }
+        switch (cfg->n_hidden) {
+            case 1: SIREN_LAUNCH_W1(1); break;
+            case 2: SIREN_LAUNCH_W1(2); break;
+            default: SIREN_LAUNCH_W1(3); break;
+        }
+#undef SIREN_LAUNCH_W1
+        return hip_status("siren_forward_grad");
+    }
 #define SIREN_LAUNCH_GRAD(LHV)                                                                                   \
     hipLaunchKernelGGL((siren::fused_kernel<LHV, true>), grid, block, 0, (hipStream_t)stream, ws, x, n, gy, y, gx, \
                        cfg->d_in, cfg->d_out, LHV, cfg->omega_first, cfg->omega_hidden, fs)
@@ -166,6 +187,17 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
     float* partial = tws + 2 * plan.act_floats;
     const dim3 grid((unsigned)(plan.n_pad / siren::TILE)), block(siren::THREADS);
     const int fs = cfg->outermost_linear ? 0 : 1;
+    if ((cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0 && !fs) {
+#define SIREN_LAUNCH_W1S(LHV)                                                                               \
+    hipLaunchKernelGGL((siren::w1_kernel<LHV, true>), grid, block, 0, st, ws, x, n, gy, (float*)nullptr, gx, \
+                       cfg->d_in, cfg->d_out, cfg->omega_first, cfg->omega_hidden, abuf, dbuf, plan.n_pad)
+        switch (cfg->n_hidden) {
+            case 1: SIREN_LAUNCH_W1S(1); break;
+            case 2: SIREN_LAUNCH_W1S(2); break;
+            default: SIREN_LAUNCH_W1S(3); break;
+        }
+#undef SIREN_LAUNCH_W1S
+    } else {
 #define SIREN_LAUNCH_STORE(LHV)                                                                                    \
     hipLaunchKernelGGL((siren::fused_kernel<LHV, true, true>), grid, block, 0, st, ws, x, n, gy, (float*)nullptr, gx, \
                        cfg->d_in, cfg->d_out, LHV, cfg->omega_first, cfg->omega_hidden, fs, abuf, dbuf, plan.n_pad)
@@ -175,6 +207,7 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
         default: SIREN_LAUNCH_STORE(3); break;
     }
 #undef SIREN_LAUNCH_STORE
+    }
     if (int rc = hip_status("siren_backward (fused store)")) return rc;
     hipLaunchKernelGGL(siren::wgrad_kernel, dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden), block, 0, st, abuf,
                        dbuf, plan.n_pad, plan.tps, partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden);

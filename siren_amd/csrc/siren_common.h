@@ -72,6 +72,31 @@ __device__ __forceinline__ void sincos_phase(float t, float& sn, float& cs) {
     cs = ((qi + 1) & 2) ? -cv : cv;
 }
 
+// Branch-free variant for the MFMA-interleaved epilogues (w1_kernel.hpp): fma Cody-Waite with a
+// full-precision pi/2 (C1 = fp32(pi/2), C2 = fp32(pi/2 - C1)); the product q*C1 is exact inside the fma, so
+// the reduction stays accurate while q is exact (|t| < 1e6 rad measured: <= 1.1e-7 absolute error on sin and
+// cos, vs 3.3e-8 for libm sinf). No data-dependent branch, so the compiler can interleave it with MFMAs.
+__device__ __forceinline__ void sincos_fast(float t, float& sn, float& cs) {
+    const float q = __builtin_rintf(t * 0.636619772367581343f);
+    float r = __builtin_fmaf(-q, 1.57079637050628662109375f, t);
+    r = __builtin_fmaf(-q, -4.37113900018624283e-8f, r);
+    const float r2 = r * r;
+    const float ps = __builtin_fmaf(__builtin_fmaf(-1.9515295891e-4f, r2, 8.3321608736e-3f), r2, -1.6666654611e-1f);
+    const float sr = __builtin_fmaf(ps * r2, r, r);
+    const float pc = __builtin_fmaf(__builtin_fmaf(2.443315711809948e-5f, r2, -1.388731625493765e-3f), r2,
+                                    4.166664568298827e-2f);
+    const float cr = __builtin_fmaf(pc * r2, r2, __builtin_fmaf(-0.5f, r2, 1.0f));
+    // quadrant select and sign flip with integer bit operations (v_bfi / v_xor): no lane masks, so nothing
+    // lands in SGPR pairs when many epilogues are in flight
+    const int qi = (int)q;
+    const int odd = -(qi & 1);  // all ones when the quadrant is odd
+    const int si = __float_as_int(sr), ci = __float_as_int(cr);
+    const int sv = (ci & odd) | (si & ~odd);
+    const int cv = (si & odd) | (ci & ~odd);
+    sn = __int_as_float(sv ^ ((qi & 2) << 30));
+    cs = __int_as_float(cv ^ (((qi + 1) & 2) << 30));
+}
+
 __device__ __forceinline__ float sin_phase(float t) {
     float s, c;
     sincos_phase(t, s, c);
@@ -87,6 +112,20 @@ __device__ __forceinline__ float sum_groups(float v) {
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// STORE-mode writers: element (neuron 16*rb + 4*g + r, coord c) of a 16-coordinate tile lives at
+// neuron*16 + c, so lane (g, c) writes 4 floats 64 B apart per block; p already points at 4*g*16 + c.
+__device__ __forceinline__ void store_block(float* p, int rb, const f32x4& v) {
+    p += 16 * rb * 16;
+    p[0] = v[0];
+    p[16] = v[1];
+    p[32] = v[2];
+    p[48] = v[3];
+}
+__device__ __forceinline__ void store_tile(float* p, const f32x4 (&v)[NB]) {
+#pragma unroll
+    for (int rb = 0; rb < NB; ++rb) store_block(p, rb, v[rb]);
 }
 
 }  // namespace siren

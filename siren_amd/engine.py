@@ -28,10 +28,11 @@ class SirenEngine:
     Parameters follow SingleBVPNet / FCBlock (modules.py:37-160) and the notebook Siren (ipynb:110-166).
     """
 
-    def __init__(self, d_in, hidden, n_hidden, d_out, omega_first=30., omega_hidden=30., outermost_linear=True):
+    def __init__(self, d_in, hidden, n_hidden, d_out, omega_first=30., omega_hidden=30., outermost_linear=True,
+                 flags=0):
         self.lib = _lib.load()
         self.cfg = _lib.SirenCfg(int(d_in), int(hidden), int(n_hidden), int(d_out), float(omega_first),
-                                 float(omega_hidden), 1 if outermost_linear else 0, 0)
+                                 float(omega_hidden), 1 if outermost_linear else 0, int(flags))
         cnt = ctypes.c_int64()
         _lib.check(self.lib.siren_param_count(ctypes.byref(self.cfg), ctypes.byref(cnt)), 'siren_param_count')
         self.param_count = cnt.value
