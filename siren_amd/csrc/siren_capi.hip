@@ -132,12 +132,6 @@ int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x
     hipLaunchKernelGGL((siren::w1_kernel<LHV, false>), grid, block, 0, (hipStream_t)stream, ws, x, n, gy, y, gx, \
                        cfg->d_in, cfg->d_out, cfg->omega_first, cfg->omega_hidden, (float*)nullptr, (float*)nullptr, \
                        (int64_t)0)
-        if (cfg->n_hidden == 3 && (cfg->reserved & SIREN_FLAG_ALT_SCHEDULE)) {
-            hipLaunchKernelGGL((siren::w1_kernel<3, false, 1>), grid, block, 0, (hipStream_t)stream, ws, x, n, gy, y,
-                               gx, cfg->d_in, cfg->d_out, cfg->omega_first, cfg->omega_hidden, (float*)nullptr,
-                               (float*)nullptr, (int64_t)0);
-            return hip_status("siren_forward_grad");
-        }
         switch (cfg->n_hidden) {
             case 1: SIREN_LAUNCH_W1(1); break;
             case 2: SIREN_LAUNCH_W1(2); break;

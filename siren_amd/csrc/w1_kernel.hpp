@@ -1,15 +1,20 @@
 // w1_kernel.hpp — the headline kernel: fused SIREN forward + coordinate vector-Jacobian product (W1) for
 // gfx950, with every sin/cos epilogue interleaved into the NEXT layer's MFMA stream.
 //
-// Same math and tiling as fused_kernels.hpp (see there and DESIGN.md §3.1): v_mfma_f32_16x16x4_f32,
-// weights as A operands from a 3-slot LDS ring of 16 KiB slices, activations as B operands in C/D layout.
-// What is different:
-//   * The L forward and L reverse GEMMs are fully unrolled (G = 0 .. 2L-1), so every slice index, ring slot
-//     and register-array index is a compile-time constant: no branches inside the hot loop at all.
+// Same math and tiling as fused_kernels.hpp: v_mfma_f32_16x16x4_f32, weights as A operands
+// from an LDS ring of 16 KiB slices, activations as B operands kept in C/D layout. On top of it:
+//   * The L forward and L reverse GEMMs are fully unrolled (G = 0 .. 2L-1): every slice index, ring slot and
+//     register-array index is a compile-time constant, so the hot loop has no branches.
 //   * Ping-pong accumulators acc[G & 1]: while GEMM G accumulates into acc[G&1] slice by slice, the epilogue
-//     of GEMM G-1 (held in acc[(G+1)&1]) is applied one 16-neuron block ahead: during slice kb the wave
-//     turns block kb+1 of the previous pre-activation into the B operand of slice kb+1. The ~25 VALU of each
-//     sin/cos thus issue in the MFMA shadow (one wave per SIMD: the matrix pipe runs 32 cycles per MFMA).
+//     of GEMM G-1 (held in acc[(G+1)&1]) runs one 16-neuron block ahead: during slice kb the wave turns block
+//     kb+1 of the previous pre-activation into the B operand of slice kb+1, so the ~25 VALU of each sin/cos
+//     issue in the MFMA shadow (one wave per SIMD; the matrix pipe takes 32 cycles per MFMA).
+//   * A operands are read by inline-asm ds_read_b128 one pair of output blocks ahead, and the consumer MFMAs
+//     are tied to a counted s_waitcnt lgkmcnt(N) through "+v" operands (hipcc would otherwise read each pair
+//     right before use and wait lgkmcnt(0)).
+//   * 4-slot ring, ONE barrier per slice placed mid-slice: it publishes slice s+1 (landed two slices after its
+//     global_load_lds) and frees slot s-1 for slice s+3, so the first operands of slice s+1 are read while the
+//     second half of slice s still computes — no operand latency is exposed at slice boundaries.
 //   * Epilogue per GEMM G (L = LH hidden layers):
 //       G = 0         FIRST : z0 = x W0^T + b0 (VALU, K = d_in)  -> a_0 = sin(w0 z0), C[0] = cos(w0 z0)
 //       1 <= G < L    SINCOS: z_G = acc + b_G                   -> a_G, C[G]
@@ -17,21 +22,48 @@
 //       L < G < 2L    DELTA : delta_{2L-G} = u . C[2L-G] . w
 //     then after the last GEMM: delta_0 = u_0 . C[0] . w0 and gx = delta_0 W0.
 //   * sincos_fast (siren_common.h) is branch-free: fma Cody-Waite with a full-precision pi/2, valid for
-//     |w z| < 1e6 rad (|z| < 3.3e4 at w = 30), ~1e-7 absolute error.
+//     |w z| < 1e6 rad (|z| < 3.3e4 at w = 30), <= 1.1e-7 absolute error.
+//   * STORE (W2 backward stage 1) additionally writes a_l and delta_l in 16-coordinate tiles.
 // Requires outermost_linear (SingleBVPNet); the notebook Siren's final sine uses fused_kernel.
 #pragma once
+#include <type_traits>
+
 #include "siren_common.h"
 
 namespace siren {
 
+constexpr int W1_NBUF = 4;  // ring slots of this kernel (64 KiB)
+
 enum { EPI_FIRST = 0, EPI_SINCOS = 1, EPI_SEED = 2, EPI_DELTA = 3 };
 
+template <int G, int LH>
+constexpr int epi_kind() {
+    return G == 0 ? EPI_FIRST : (G < LH ? EPI_SINCOS : (G == LH ? EPI_SEED : EPI_DELTA));
+}
+// LDS parameter reads an epilogue block needs: FIRST W0T[0..3] + b0; SINCOS b_G; SEED b_L + WoutT[0..3] + seed
+template <int KIND>
+constexpr int epi_nparams() {
+    return KIND == EPI_FIRST ? 5 : (KIND == EPI_SINCOS ? 1 : (KIND == EPI_SEED ? 6 : 0));
+}
+
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
 // cos(w z_l) of layers l >= 1 is parked in AGPRs (the accumulator half of the unified register file): it is
-// only read back once, by the reverse epilogue, while the VGPR half holds the B operands and the epilogue
-// temporaries. The empty asm statements pin the register class; the moves are v_accvgpr_write/read.
+// only read back once, by the reverse epilogue. The empty asm statements pin the register class.
 __device__ __forceinline__ f32x4 to_agpr(f32x4 v) {
     f32x4 r;
     asm("; park in agpr" : "=a"(r) : "0"(v));
+    return r;
+}
+__device__ __forceinline__ f32x4 from_agpr(f32x4 v) {
+    f32x4 r;
+    asm("; unpark" : "=v"(r) : "0"(v));
     return r;
 }
 // Opaque identity: materialises v here (LLVM would otherwise sink the cos bit-select to its use in the
@@ -40,23 +72,31 @@ __device__ __forceinline__ f32x4 pin(f32x4 v) {
     asm("; pin" : "+v"(v));
     return v;
 }
-__device__ __forceinline__ f32x4 from_agpr(f32x4 v) {
+
+// ds_read_b128 at a compile-time byte offset from a VGPR base (not visible to hipcc's waitcnt insertion).
+template <int OFF>
+__device__ __forceinline__ f32x4 lds_read4(unsigned vaddr) {
+    static_assert(OFF >= 0 && OFF < 65536, "ds offset field is 16 bits");
     f32x4 r;
-    asm("; unpark" : "=v"(r) : "0"(v));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(vaddr), "i"(OFF));
     return r;
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait(f32x4& a, f32x4& b) {
+    asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N));
 }
 
 template <int LH, bool STORE>
 struct W1State {
-    f32x4 act[NB];        // B operand of the current GEMM (filled one block ahead)
-    f32x4 acc[2][NB];     // ping-pong accumulators
-    f32x4 C[LH][NB];      // cos(w z_l), l = 0 .. LH-1
-    float xv[MAXD];       // this lane's coordinate
-    float gyv[MAXO];      // this lane's output cotangent
-    float yp[MAXO];       // partial y over this lane's neurons
+    f32x4 act[NB];     // B operand of the current GEMM (filled one block ahead)
+    f32x4 acc[2][NB];  // ping-pong accumulators
+    f32x4 C[LH][NB];   // cos(w z_l), l = 0 .. LH-1
+    f32x4 pa0, pa1;    // prefetched first operand pair of the next slice
+    float xv[MAXD];    // this lane's coordinate
+    float gyv[MAXO];   // this lane's output cotangent
+    float yp[MAXO];    // partial y over this lane's neurons
 };
 
-template <int LH, bool STORE>
 struct W1Ctx {
     const float* stream;
     float* ring;
@@ -64,35 +104,63 @@ struct W1Ctx {
     int d, o, wave, lane, g;
     float w0, w;
     bool seed_ones;
-    float* abuf;      // STORE: tile base (lane-adjusted) of layer 0; layer l at + l * lstride
+    float* abuf;  // STORE: lane-adjusted tile base of layer 0; layer l at + l * lstride
     float* dbuf;
     int64_t lstride;
+    unsigned ring_vaddr;  // LDS byte address of this lane's 16 B in slot 0 of the ring
+    unsigned sm_vaddr;    // LDS byte address of the small-parameter block + this lane's 4*g neuron offset
 };
 
-__device__ __forceinline__ void ring_issue_s(const float* __restrict__ stream, float* ring, int s, int wave, int lane) {
+__device__ __forceinline__ void ring_issue4(const float* __restrict__ stream, float* ring, int s, int wave, int lane) {
     const float* src = stream + (int64_t)s * SLICE + wave * 1024 + lane * 4;
-    float* dst = ring + (s % NBUF) * SLICE + wave * 1024;
+    float* dst = ring + (s % W1_NBUF) * SLICE + wave * 1024;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
         __builtin_amdgcn_global_load_lds((const void*)(src + q * 256),
                                          (__attribute__((address_space(3))) void*)(dst + q * 256), 16, 0, 0);
 }
 
+// ---- epilogue parameters (LDS) -------------------------------------------------------------------------
+template <int KIND, int G, int LH>
+struct EpiParams {
+    f32x4 v[epi_nparams<KIND>() > 0 ? epi_nparams<KIND>() : 1];
+};
+
+// Byte offset (inside the small block, relative to this lane's neuron offset 4*g) of parameter i, block b.
+template <int KIND, int G, int LH>
+constexpr int epi_param_off(int i, int b) {
+    return 4 * (16 * b) + 4 * (KIND == EPI_FIRST ? (i < 4 ? SM_W0 + i * H : SM_BIAS)
+                                : KIND == EPI_SINCOS ? SM_BIAS + G * H
+                                : (i == 0 ? SM_BIAS + LH * H : (i < 5 ? SM_WO + (i - 1) * H : SM_SEED)));
+}
+
+// asm reads (counted by the caller's lgkmcnt) of block B's parameters
+template <int KIND, int G, int LH, int B>
+__device__ __forceinline__ void epi_issue(EpiParams<KIND, G, LH>& ep, unsigned sm_vaddr) {
+    static_for<0, epi_nparams<KIND>()>([&](auto I) {
+        ep.v[decltype(I)::value] = lds_read4<epi_param_off<KIND, G, LH>(decltype(I)::value, B)>(sm_vaddr);
+    });
+}
+
+// plain loads (block 0, outside the pipelined slice loop)
+template <int KIND, int G, int LH>
+__device__ __forceinline__ void epi_load(EpiParams<KIND, G, LH>& ep, const W1Ctx& cx, int b) {
+#pragma unroll
+    for (int i = 0; i < epi_nparams<KIND>(); ++i)
+        ep.v[i] = *(const f32x4*)((const char*)cx.sm + epi_param_off<KIND, G, LH>(i, b) + 16 * cx.g);
+}
+
 // Epilogue for one 16-neuron block b of GEMM G (see the table at the top).
 template <int G, int LH, bool STORE>
-__device__ __forceinline__ void w1_epilogue(W1State<LH, STORE>& st, const W1Ctx<LH, STORE>& cx, int b) {
-    constexpr int KIND = G == 0 ? EPI_FIRST : (G < LH ? EPI_SINCOS : (G == LH ? EPI_SEED : EPI_DELTA));
-    const int nb = 16 * b + 4 * cx.g;
+__device__ __forceinline__ void w1_epilogue(W1State<LH, STORE>& st, const W1Ctx& cx, int b,
+                                            const EpiParams<epi_kind<G, LH>(), G, LH>& ep) {
+    constexpr int KIND = epi_kind<G, LH>();
     if constexpr (KIND == EPI_FIRST) {
-        f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        f32x4 z = st.xv[0] * ep.v[0];
 #pragma unroll
-        for (int k = 0; k < MAXD; ++k) {
-            if (k < cx.d) {
-                const f32x4 wk = *(const f32x4*)(cx.sm + SM_W0 + k * H + nb);
-                z = k == 0 ? st.xv[0] * wk : z + st.xv[k] * wk;
-            }
-        }
-        z += *(const f32x4*)(cx.sm + SM_BIAS + nb);
+        for (int k = 1; k < MAXD; ++k)
+            if (k < cx.d) z += st.xv[k] * ep.v[k];
+        z += ep.v[4];
         f32x4 cs4;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -104,7 +172,7 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, STORE>& st, const W1Ctx<
         st.C[0][b] = pin(cs4);
         if constexpr (STORE) store_block(cx.abuf, b, st.act[b]);
     } else if constexpr (KIND == EPI_SINCOS) {
-        const f32x4 z = st.acc[(G + 1) & 1][b] + *(const f32x4*)(cx.sm + SM_BIAS + G * H + nb);
+        const f32x4 z = st.acc[(G + 1) & 1][b] + ep.v[0];
         f32x4 cs4;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -116,7 +184,7 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, STORE>& st, const W1Ctx<
         st.C[G][b] = to_agpr(cs4);
         if constexpr (STORE) store_block(cx.abuf + G * cx.lstride, b, st.act[b]);
     } else if constexpr (KIND == EPI_SEED) {
-        const f32x4 z = st.acc[(G + 1) & 1][b] + *(const f32x4*)(cx.sm + SM_BIAS + LH * H + nb);
+        const f32x4 z = st.acc[(G + 1) & 1][b] + ep.v[0];
         f32x4 sn, cs;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -130,12 +198,12 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, STORE>& st, const W1Ctx<
 #pragma unroll
         for (int j = 0; j < MAXO; ++j) {
             if (j < cx.o) {
-                const f32x4 wj = *(const f32x4*)(cx.sm + SM_WO + j * H + nb);
+                const f32x4 wj = ep.v[1 + j];
                 st.yp[j] += wj[0] * sn[0] + wj[1] * sn[1] + wj[2] * sn[2] + wj[3] * sn[3];
                 if (!cx.seed_ones) ga += st.gyv[j] * wj;
             }
         }
-        if (cx.seed_ones) ga = *(const f32x4*)(cx.sm + SM_SEED + nb);
+        if (cx.seed_ones) ga = ep.v[5];
         st.act[b] = (ga * cs) * cx.w;
         if constexpr (STORE) store_block(cx.dbuf + LH * cx.lstride, b, st.act[b]);
     } else {
@@ -145,80 +213,104 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, STORE>& st, const W1Ctx<
     }
 }
 
-// GEMM G: 16 slices; slice kb multiplies B = act[kb] into acc[G & 1] while block kb+1 of the previous
-// epilogue is produced.
-template <int G, int LH, bool STORE, int SCHED>
-__device__ __forceinline__ void w1_gemm(W1State<LH, STORE>& st, const W1Ctx<LH, STORE>& cx) {
+// One slice s = 16 G + KB: 8 operand pairs x 8 MFMAs, the mid-slice ring barrier after pair 3, the next
+// slice's first pair prefetched during pair 7, and epilogue block KB+1 of GEMM G-1 in the MFMA shadow.
+template <int G, int KB, int LH, bool STORE>
+__device__ __forceinline__ void w1_slice(W1State<LH, STORE>& st, const W1Ctx& cx) {
     constexpr int NS = 2 * LH * NB;
+    constexpr int S = G * NB + KB;
+    constexpr int SLOT = (S % W1_NBUF) * SLICE * 4;
+    constexpr int NSLOT = ((S + 1) % W1_NBUF) * SLICE * 4;
+    constexpr int KIND = epi_kind<G, LH>();
+    constexpr bool EPI = KB + 1 < NB;
+    f32x4 (&acc)[NB] = st.acc[G & 1];
+    const f32x4 bop = st.act[KB];
+    EpiParams<KIND, G, LH> ep;
+    if constexpr (EPI && epi_nparams<KIND>() > 0) epi_issue<KIND, G, LH, KB + 1>(ep, cx.sm_vaddr);
+    f32x4 a0 = st.pa0, a1 = st.pa1;
+    static_for<0, NB / 2>([&](auto P) {
+        constexpr int p = decltype(P)::value;
+        if constexpr (p == 4 && S + 1 < NS) {
+            // publish slice S+1 (own part landed: at most slice S+2's 4 loads still outstanding) and free the
+            // slot of slice S-1 (every wave is past its last read of it) for slice S+3
+            if constexpr (S + 2 < NS)
+                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if constexpr (S + 3 < NS) {
+                const float* sp = cx.stream;
+                asm volatile("" : "+s"(sp));  // keep slice addresses from being hoisted into SGPRs
+                ring_issue4(sp, cx.ring, S + 3, cx.wave, cx.lane);
+            }
+        }
+        f32x4 n0, n1;
+        constexpr bool NEXT_IN_SLICE = p + 1 < NB / 2;
+        constexpr bool NEXT_SLICE = !NEXT_IN_SLICE && S + 1 < NS;
+        if constexpr (NEXT_IN_SLICE) {
+            n0 = lds_read4<SLOT + (2 * p + 2) * 1024>(cx.ring_vaddr);
+            n1 = lds_read4<SLOT + (2 * p + 3) * 1024>(cx.ring_vaddr);
+        } else if constexpr (NEXT_SLICE) {
+            n0 = lds_read4<NSLOT>(cx.ring_vaddr);
+            n1 = lds_read4<NSLOT + 1024>(cx.ring_vaddr);
+        }
+        if constexpr (NEXT_IN_SLICE || NEXT_SLICE)
+            lgkm_wait<2>(a0, a1);
+        else
+            lgkm_wait<0>(a0, a1);
+        if constexpr (p == 0 && EPI) {
+            // the epilogue parameters were issued before pair 1's reads: the wait above covered them
+#pragma unroll
+            for (int i = 0; i < epi_nparams<KIND>(); ++i) asm volatile("" : "+v"(ep.v[i]));
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            acc[2 * p] = mfma4(a0[r], bop[r], acc[2 * p]);
+            acc[2 * p + 1] = mfma4(a1[r], bop[r], acc[2 * p + 1]);
+        }
+        if constexpr (NEXT_IN_SLICE || NEXT_SLICE) {
+            a0 = n0;
+            a1 = n1;
+        }
+    });
+    st.pa0 = a0;
+    st.pa1 = a1;
+    if constexpr (EPI) w1_epilogue<G, LH, STORE>(st, cx, KB + 1, ep);
+}
+
+template <int G, int LH, bool STORE>
+__device__ __forceinline__ void w1_gemm(W1State<LH, STORE>& st, const W1Ctx& cx) {
+    constexpr int KIND = epi_kind<G, LH>();
     f32x4 (&acc)[NB] = st.acc[G & 1];
 #pragma unroll
     for (int ob = 0; ob < NB; ++ob) acc[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
-    w1_epilogue<G, LH, STORE>(st, cx, 0);
-#pragma unroll
-    for (int kb = 0; kb < NB; ++kb) {
-        const int s = G * NB + kb;
-        // this wave's part of slice s has landed (slice s+1 may be in flight); barrier: all parts landed and
-        // every wave is done with slice s-1's slot, which slice s+2 refills
-        if (s + 1 < NS)
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);  // nothing crosses the barrier (the scheduler would sink epilogues)
-        if (s + 2 < NS) {
-            const float* sp = cx.stream;
-            asm volatile("" : "+s"(sp));  // keep the 96 slice addresses from being hoisted into SGPRs
-            ring_issue_s(sp, cx.ring, s + 2, cx.wave, cx.lane);
-        }
-        const float* sl = cx.ring + (s % NBUF) * SLICE + cx.lane * 4;
-        const f32x4 bop = st.act[kb];
-        f32x4 a[NB];
-#pragma unroll
-        for (int ob = 0; ob < NB; ++ob) a[ob] = *(const f32x4*)(sl + ob * 256);
-#pragma unroll
-        for (int ob = 0; ob < NB; ob += 2) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                acc[ob] = mfma4(a[ob][r], bop[r], acc[ob]);
-                acc[ob + 1] = mfma4(a[ob + 1][r], bop[r], acc[ob + 1]);
-            }
-        }
-        if (kb + 1 < NB) w1_epilogue<G, LH, STORE>(st, cx, kb + 1);
-        if constexpr (SCHED == 1) {
-            // A operands two pairs ahead, then per pair 8 MFMAs each followed by a few epilogue VALU
-            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // DS_READ: pairs 0, 1
-#pragma unroll
-            for (int p = 0; p < NB / 2; ++p) {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
-                }
-                if (p + 2 < NB / 2) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS_READ: pair p+2
-            }
-        }
+    {
+        EpiParams<KIND, G, LH> ep;
+        epi_load<KIND, G, LH>(ep, cx, 0);
+        w1_epilogue<G, LH, STORE>(st, cx, 0, ep);
     }
+    static_for<0, NB>([&](auto KB) { w1_slice<G, decltype(KB)::value, LH, STORE>(st, cx); });
 }
 
-template <int G, int LH, bool STORE, int SCHED>
-__device__ __forceinline__ void w1_run(W1State<LH, STORE>& st, const W1Ctx<LH, STORE>& cx) {
+template <int G, int LH, bool STORE>
+__device__ __forceinline__ void w1_run(W1State<LH, STORE>& st, const W1Ctx& cx) {
     if constexpr (G < 2 * LH) {
-        w1_gemm<G, LH, STORE, SCHED>(st, cx);
-        w1_run<G + 1, LH, STORE, SCHED>(st, cx);
+        w1_gemm<G, LH, STORE>(st, cx);
+        w1_run<G + 1, LH, STORE>(st, cx);
     }
 }
 
-template <int LH, bool STORE, int SCHED = 0>
+template <int LH, bool STORE>
 __global__ __launch_bounds__(THREADS, 1) void w1_kernel(const float* __restrict__ ws, const float* __restrict__ x,
                                                         int64_t n, const float* __restrict__ gy, float* __restrict__ y,
                                                         float* __restrict__ gx, int d, int o, float w0, float w,
                                                         float* __restrict__ abuf, float* __restrict__ dbuf,
                                                         int64_t n_pad) {
-    __shared__ __attribute__((aligned(16))) float lds[NBUF * SLICE + SMALL_MAX];
-    W1Ctx<LH, STORE> cx;
+    __shared__ __attribute__((aligned(16))) float lds[W1_NBUF * SLICE + SMALL_MAX];
+    W1Ctx cx;
     W1State<LH, STORE> st;
     cx.ring = lds;
-    float* sm = lds + NBUF * SLICE;
+    float* sm = lds + W1_NBUF * SLICE;
     cx.sm = sm;
     cx.lane = threadIdx.x & 63;
     cx.wave = threadIdx.x >> 6;
@@ -231,6 +323,9 @@ __global__ __launch_bounds__(THREADS, 1) void w1_kernel(const float* __restrict_
     cx.seed_ones = gy == nullptr;
     cx.stream = ws + small_pad(LH);
     cx.lstride = n_pad * H;
+    const unsigned lds_base = (unsigned)(uintptr_t)((__attribute__((address_space(3))) float*)lds);
+    cx.ring_vaddr = lds_base + cx.lane * 16;
+    cx.sm_vaddr = lds_base + W1_NBUF * SLICE * 4 + 16 * cx.g;
     const int64_t toff = ((int64_t)blockIdx.x * WAVES + cx.wave) * (H * 16) + 4 * cx.g * 16 + c;
     cx.abuf = STORE ? abuf + toff : nullptr;
     cx.dbuf = STORE ? dbuf + toff : nullptr;
@@ -249,10 +344,16 @@ __global__ __launch_bounds__(THREADS, 1) void w1_kernel(const float* __restrict_
         st.gyv[j] = (gy != nullptr && valid && j < o) ? gy[coord * o + j] : 0.f;
     }
     __syncthreads();
-    ring_issue_s(cx.stream, cx.ring, 0, cx.wave, cx.lane);
-    ring_issue_s(cx.stream, cx.ring, 1, cx.wave, cx.lane);
+    // ring prologue: slices 0..2 in flight; slice 0 published; its first operand pair read
+    ring_issue4(cx.stream, cx.ring, 0, cx.wave, cx.lane);
+    ring_issue4(cx.stream, cx.ring, 1, cx.wave, cx.lane);
+    ring_issue4(cx.stream, cx.ring, 2, cx.wave, cx.lane);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    st.pa0 = lds_read4<0>(cx.ring_vaddr);
+    st.pa1 = lds_read4<1024>(cx.ring_vaddr);
 
-    w1_run<0, LH, STORE, SCHED>(st, cx);
+    w1_run<0, LH, STORE>(st, cx);
 
     // y (reduced over the 4 lane groups)
 #pragma unroll
