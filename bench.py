@@ -85,17 +85,21 @@ def kernel_roofline(eng, ws, x, reps=10):
     return ms, achieved
 
 
+HEADLINE_KERNEL = 'w1_kernel<3,false>'   # kernel name as tools/pmc_summary.py shortens it
+
+
 def pmc_traffic(n):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/*_pmc.json), if it matches."""
+    """HBM bytes per launch of the headline kernel from the committed rocprofv3 PMC summary
+    (profiles/*pmc*.json, written by tools/run_pmc.sh + tools/pmc_summary.py), if one matches this kernel and N."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, 'profiles', '*pmc*.json')), reverse=True):
         try:
             rec = json.load(open(path))
         except Exception:
             continue
-        k = rec.get('kernels', {}).get('fused_kernel<3,true,false>')
-        if k and rec.get('n') == n:
-            return k.get('hbm_bytes_per_launch')
+        k = rec.get('kernels', {}).get(HEADLINE_KERNEL)
+        if k and rec.get('n') == n and 'hbm_bytes_per_launch' in k:
+            return round(k['hbm_bytes_per_launch'])
     return None
 
 
