@@ -108,7 +108,23 @@ int32_t siren_forward(const siren_cfg* cfg, const float* ws, const float* x, int
     if (ws == nullptr || x == nullptr || y == nullptr) return fail(SIREN_EINVAL, "ws/x/y is NULL");
     const int64_t blocks = (n + siren::TILE - 1) / siren::TILE;
     if (blocks > 0x7fffffffll) return fail(SIREN_EINVAL, "n too large");
-    hipLaunchKernelGGL((siren::fused_kernel<0, false>), dim3((unsigned)blocks), dim3(siren::THREADS), 0,
+    const dim3 grid((unsigned)blocks), block(siren::THREADS);
+    if (cfg->outermost_linear && cfg->n_hidden <= 5 && (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0) {
+#define SIREN_LAUNCH_FWD(LHV)                                                                                    \
+    hipLaunchKernelGGL((siren::w1_kernel<LHV, siren::MODE_FWD>), grid, block, 0, (hipStream_t)stream, ws, x, n,      \
+                       (const float*)nullptr, y, (float*)nullptr, cfg->d_in, cfg->d_out, cfg->omega_first,         \
+                       cfg->omega_hidden, (float*)nullptr, (float*)nullptr, (int64_t)0)
+        switch (cfg->n_hidden) {
+            case 1: SIREN_LAUNCH_FWD(1); break;
+            case 2: SIREN_LAUNCH_FWD(2); break;
+            case 3: SIREN_LAUNCH_FWD(3); break;
+            case 4: SIREN_LAUNCH_FWD(4); break;
+            default: SIREN_LAUNCH_FWD(5); break;
+        }
+#undef SIREN_LAUNCH_FWD
+        return hip_status("siren_forward");
+    }
+    hipLaunchKernelGGL((siren::fused_kernel<0, false>), grid, block, 0,
                        (hipStream_t)stream, ws, x, n, nullptr, y, nullptr, cfg->d_in, cfg->d_out, cfg->n_hidden,
                        cfg->omega_first, cfg->omega_hidden, cfg->outermost_linear ? 0 : 1);
     return hip_status("siren_forward");
@@ -129,7 +145,7 @@ int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x
     const bool legacy = (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) != 0 || fs;
     if (!legacy) {
 #define SIREN_LAUNCH_W1(LHV)                                                                                    \
-    hipLaunchKernelGGL((siren::w1_kernel<LHV, false>), grid, block, 0, (hipStream_t)stream, ws, x, n, gy, y, gx, \
+    hipLaunchKernelGGL((siren::w1_kernel<LHV, siren::MODE_W1>), grid, block, 0, (hipStream_t)stream, ws, x, n, gy, y, gx, \
                        cfg->d_in, cfg->d_out, cfg->omega_first, cfg->omega_hidden, (float*)nullptr, (float*)nullptr, \
                        (int64_t)0)
         switch (cfg->n_hidden) {
@@ -183,7 +199,7 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
     const int fs = cfg->outermost_linear ? 0 : 1;
     if ((cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0 && !fs) {
 #define SIREN_LAUNCH_W1S(LHV)                                                                               \
-    hipLaunchKernelGGL((siren::w1_kernel<LHV, true>), grid, block, 0, st, ws, x, n, gy, (float*)nullptr, gx, \
+    hipLaunchKernelGGL((siren::w1_kernel<LHV, siren::MODE_STORE>), grid, block, 0, st, ws, x, n, gy, (float*)nullptr, gx, \
                        cfg->d_in, cfg->d_out, cfg->omega_first, cfg->omega_hidden, abuf, dbuf, plan.n_pad)
         switch (cfg->n_hidden) {
             case 1: SIREN_LAUNCH_W1S(1); break;

@@ -36,6 +36,10 @@ constexpr int W1_NBUF = 4;  // ring slots of this kernel (64 KiB)
 
 enum { EPI_FIRST = 0, EPI_SINCOS = 1, EPI_SEED = 2, EPI_DELTA = 3 };
 
+// Kernel modes: W1 (forward + vjp_x), W1 STORE (W2 backward stage 1), FWD (W0: forward only, sin epilogues
+// without cos, output layer folded into a final serial epilogue).
+enum { MODE_W1 = 0, MODE_STORE = 1, MODE_FWD = 2 };
+
 template <int G, int LH>
 constexpr int epi_kind() {
     return G == 0 ? EPI_FIRST : (G < LH ? EPI_SINCOS : (G == LH ? EPI_SEED : EPI_DELTA));
@@ -86,11 +90,11 @@ __device__ __forceinline__ void lgkm_wait(f32x4& a, f32x4& b) {
     asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N));
 }
 
-template <int LH, bool STORE>
+template <int LH, int MODE>
 struct W1State {
     f32x4 act[NB];     // B operand of the current GEMM (filled one block ahead)
     f32x4 acc[2][NB];  // ping-pong accumulators
-    f32x4 C[LH][NB];   // cos(w z_l), l = 0 .. LH-1
+    f32x4 C[MODE == MODE_FWD ? 1 : LH][NB];  // cos(w z_l), l = 0 .. LH-1 (unused in FWD mode)
     f32x4 pa0, pa1;    // prefetched first operand pair of the next slice
     float xv[MAXD];    // this lane's coordinate
     float gyv[MAXO];   // this lane's output cotangent
@@ -151,10 +155,12 @@ __device__ __forceinline__ void epi_load(EpiParams<KIND, G, LH>& ep, const W1Ctx
 }
 
 // Epilogue for one 16-neuron block b of GEMM G (see the table at the top).
-template <int G, int LH, bool STORE>
-__device__ __forceinline__ void w1_epilogue(W1State<LH, STORE>& st, const W1Ctx& cx, int b,
+template <int G, int LH, int MODE>
+__device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& cx, int b,
                                             const EpiParams<epi_kind<G, LH>(), G, LH>& ep) {
     constexpr int KIND = epi_kind<G, LH>();
+    constexpr bool STORE = MODE == MODE_STORE;
+    constexpr bool FWD = MODE == MODE_FWD;
     if constexpr (KIND == EPI_FIRST) {
         f32x4 z = st.xv[0] * ep.v[0];
 #pragma unroll
@@ -169,7 +175,7 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, STORE>& st, const W1Ctx&
             st.act[b][r] = sn;
             cs4[r] = cs;
         }
-        st.C[0][b] = pin(cs4);
+        if constexpr (!FWD) st.C[0][b] = pin(cs4);
         if constexpr (STORE) store_block(cx.abuf, b, st.act[b]);
     } else if constexpr (KIND == EPI_SINCOS) {
         const f32x4 z = st.acc[(G + 1) & 1][b] + ep.v[0];
@@ -181,7 +187,7 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, STORE>& st, const W1Ctx&
             st.act[b][r] = sn;
             cs4[r] = cs;
         }
-        st.C[G][b] = to_agpr(cs4);
+        if constexpr (!FWD) st.C[G][b] = to_agpr(cs4);
         if constexpr (STORE) store_block(cx.abuf + G * cx.lstride, b, st.act[b]);
     } else if constexpr (KIND == EPI_SEED) {
         const f32x4 z = st.acc[(G + 1) & 1][b] + ep.v[0];
@@ -215,9 +221,9 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, STORE>& st, const W1Ctx&
 
 // One slice s = 16 G + KB: 8 operand pairs x 8 MFMAs, the mid-slice ring barrier after pair 3, the next
 // slice's first pair prefetched during pair 7, and epilogue block KB+1 of GEMM G-1 in the MFMA shadow.
-template <int G, int KB, int LH, bool STORE>
-__device__ __forceinline__ void w1_slice(W1State<LH, STORE>& st, const W1Ctx& cx) {
-    constexpr int NS = 2 * LH * NB;
+template <int G, int KB, int LH, int MODE>
+__device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx) {
+    constexpr int NS = (MODE == MODE_FWD ? 1 : 2) * LH * NB;
     constexpr int S = G * NB + KB;
     constexpr int SLOT = (S % W1_NBUF) * SLICE * 4;
     constexpr int NSLOT = ((S + 1) % W1_NBUF) * SLICE * 4;
@@ -275,11 +281,11 @@ __device__ __forceinline__ void w1_slice(W1State<LH, STORE>& st, const W1Ctx& cx
     });
     st.pa0 = a0;
     st.pa1 = a1;
-    if constexpr (EPI) w1_epilogue<G, LH, STORE>(st, cx, KB + 1, ep);
+    if constexpr (EPI) w1_epilogue<G, LH, MODE>(st, cx, KB + 1, ep);
 }
 
-template <int G, int LH, bool STORE>
-__device__ __forceinline__ void w1_gemm(W1State<LH, STORE>& st, const W1Ctx& cx) {
+template <int G, int LH, int MODE>
+__device__ __forceinline__ void w1_gemm(W1State<LH, MODE>& st, const W1Ctx& cx) {
     constexpr int KIND = epi_kind<G, LH>();
     f32x4 (&acc)[NB] = st.acc[G & 1];
 #pragma unroll
@@ -287,28 +293,32 @@ __device__ __forceinline__ void w1_gemm(W1State<LH, STORE>& st, const W1Ctx& cx)
     {
         EpiParams<KIND, G, LH> ep;
         epi_load<KIND, G, LH>(ep, cx, 0);
-        w1_epilogue<G, LH, STORE>(st, cx, 0, ep);
+        w1_epilogue<G, LH, MODE>(st, cx, 0, ep);
     }
-    static_for<0, NB>([&](auto KB) { w1_slice<G, decltype(KB)::value, LH, STORE>(st, cx); });
+    static_for<0, NB>([&](auto KB) { w1_slice<G, decltype(KB)::value, LH, MODE>(st, cx); });
 }
 
-template <int G, int LH, bool STORE>
-__device__ __forceinline__ void w1_run(W1State<LH, STORE>& st, const W1Ctx& cx) {
-    if constexpr (G < 2 * LH) {
-        w1_gemm<G, LH, STORE>(st, cx);
-        w1_run<G + 1, LH, STORE>(st, cx);
+template <int G, int LH, int MODE>
+__device__ __forceinline__ void w1_run(W1State<LH, MODE>& st, const W1Ctx& cx) {
+    if constexpr (G < (MODE == MODE_FWD ? 1 : 2) * LH) {
+        w1_gemm<G, LH, MODE>(st, cx);
+        w1_run<G + 1, LH, MODE>(st, cx);
     }
 }
 
-template <int LH, bool STORE>
-__global__ __launch_bounds__(THREADS, 1) void w1_kernel(const float* __restrict__ ws, const float* __restrict__ x,
+constexpr int small_floats_ct(int lh) { return SM_BIAS + (lh + 1) * H; }
+
+template <int LH, int MODE>
+__global__ __launch_bounds__(THREADS, MODE == MODE_FWD ? 2 : 1) void w1_kernel(const float* __restrict__ ws, const float* __restrict__ x,
                                                         int64_t n, const float* __restrict__ gy, float* __restrict__ y,
                                                         float* __restrict__ gx, int d, int o, float w0, float w,
                                                         float* __restrict__ abuf, float* __restrict__ dbuf,
                                                         int64_t n_pad) {
-    __shared__ __attribute__((aligned(16))) float lds[W1_NBUF * SLICE + SMALL_MAX];
+    constexpr bool STORE = MODE == MODE_STORE;
+    constexpr int NS = (MODE == MODE_FWD ? 1 : 2) * LH * NB;
+    __shared__ __attribute__((aligned(16))) float lds[W1_NBUF * SLICE + small_floats_ct(LH)];
     W1Ctx cx;
-    W1State<LH, STORE> st;
+    W1State<LH, MODE> st;
     cx.ring = lds;
     float* sm = lds + W1_NBUF * SLICE;
     cx.sm = sm;
@@ -345,6 +355,7 @@ __global__ __launch_bounds__(THREADS, 1) void w1_kernel(const float* __restrict_
     }
     __syncthreads();
     // ring prologue: slices 0..2 in flight; slice 0 published; its first operand pair read
+    static_assert(NS >= 3, "ring prologue issues three slices");
     ring_issue4(cx.stream, cx.ring, 0, cx.wave, cx.lane);
     ring_issue4(cx.stream, cx.ring, 1, cx.wave, cx.lane);
     ring_issue4(cx.stream, cx.ring, 2, cx.wave, cx.lane);
@@ -353,7 +364,39 @@ __global__ __launch_bounds__(THREADS, 1) void w1_kernel(const float* __restrict_
     st.pa0 = lds_read4<0>(cx.ring_vaddr);
     st.pa1 = lds_read4<1024>(cx.ring_vaddr);
 
-    w1_run<0, LH, STORE>(st, cx);
+    w1_run<0, LH, MODE>(st, cx);
+
+    if constexpr (MODE == MODE_FWD) {
+        // last hidden layer: z_L = acc + b_L, a_L = sin(w z_L), y = a_L Wout^T + bout (serial epilogue)
+        constexpr int GL = (LH - 1) & 1;
+#pragma unroll
+        for (int rb = 0; rb < NB; ++rb) {
+            const int nb = 16 * rb + 4 * cx.g;
+            const f32x4 z = st.acc[GL][rb] + *(const f32x4*)(sm + SM_BIAS + LH * H + nb);
+            f32x4 sn;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float a, cc;
+                sincos_fast(w * z[r], a, cc);
+                sn[r] = a;
+            }
+#pragma unroll
+            for (int j = 0; j < MAXO; ++j) {
+                if (j < o) {
+                    const f32x4 wj = *(const f32x4*)(sm + SM_WO + j * H + nb);
+                    st.yp[j] += wj[0] * sn[0] + wj[1] * sn[1] + wj[2] * sn[2] + wj[3] * sn[3];
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < MAXO; ++j) {
+            if (j < o) {
+                const float yj = sum_groups(st.yp[j]) + sm[SM_BOUT + j];
+                if (valid && cx.g == 0) y[coord * o + j] = yj;
+            }
+        }
+        return;
+    }
 
     // y (reduced over the 4 lane groups)
 #pragma unroll

@@ -15,7 +15,8 @@ def main():
     ap.add_argument('--n', type=int, default=1 << 20)
     ap.add_argument('--rounds', type=int, default=8)
     ap.add_argument('--reps', type=int, default=5)
-    ap.add_argument('--variants', default='0,1,2')
+    ap.add_argument('--variants', default='0,1')
+    ap.add_argument('--fwd', action='store_true', help='time siren_forward (W0) instead of W1')
     a = ap.parse_args()
     import __graft_entry__
     __graft_entry__.build()
@@ -45,13 +46,21 @@ def main():
             s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s0.record()
             for _ in range(a.reps):
-                e.forward_grad(ws, x, out_y=outs[v][0], out_gx=outs[v][1])
+                if a.fwd:
+                    e.forward(ws, x, out=outs[v][0])
+                else:
+                    e.forward_grad(ws, x, out_y=outs[v][0], out_gx=outs[v][1])
             s1.record()
             torch.cuda.synchronize()
             times[v].append(s0.elapsed_time(s1) / a.reps)
+    flop = W1_FLOP // 2 if a.fwd else W1_FLOP
+    for v, (y, g) in outs.items():
+        if a.fwd:
+            y0 = e.forward(ws, x)
+            print('variant %d forward: max|dy| %.2e' % (v, np.max(np.abs(engs[v].forward(ws, x)[idx].cpu().numpy() - ry))))
     for v, t in times.items():
         t = np.array(t)
-        tf = W1_FLOP * a.n / (np.median(t) * 1e-3) / 1e12
+        tf = flop * a.n / (np.median(t) * 1e-3) / 1e12
         print('variant %d: median %.3f ms  min %.3f ms  -> %.1f TFLOP/s (%.1f%% of 157.3)  %.1f Mcoords/s'
               % (v, np.median(t), t.min(), tf, tf / 157.3 * 100, a.n / np.median(t) / 1e3), flush=True)
 
