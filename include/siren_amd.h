@@ -104,6 +104,20 @@ int32_t siren_train_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count);
 int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* gy,
                        float* tws, void* reserved, float* gx, float* gparams, void* stream);
 
+/* fp32 values of workspace siren_second_order() needs (per-layer spill, and with want_theta the tangent /
+ * primal activations and adjoints of every layer plus 2*S partial slabs). */
+int32_t siren_second_order_ws_floats(const siren_cfg* cfg, int64_t n, int32_t want_theta, int64_t* count);
+
+/* W3, second-order adjoint for d_out == 1 (the backward of the dPhi/dx graph node that gradients_mse / sdf /
+ * divergence differentiate, diff_operators.py:27-43, loss_functions.py:84-89, 214-238): with v (n, d_in) the
+ * cotangent of J = dPhi/dx,
+ *   gx (n, d_in)          = H(x) v                      (Hessian-vector product)
+ *   gparams (param_count) = d/dtheta sum_c <v_c, J(x_c)> (skipped when gparams == NULL)
+ * Forward primal+tangent sweep and reverse sweep in one kernel (per-layer state spilled to tws), then the split-K
+ * MFMA weight-gradient kernel over K = 2n and a deterministic slab reduction. */
+int32_t siren_second_order(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
+                           float* tws, float* gx, float* gparams, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -71,3 +71,16 @@ def vjp_vjp(cfg, x, flat, gy, ggx, create_graph):
     if not gy.requires_grad:
         rgy = None
     return rx, rp, rgy
+
+
+def hvp_vjp(cfg, x, flat, v, g, create_graph):
+    """d/d(x, theta, v) of <g, H(x) v> (d_out == 1)."""
+    with torch.enable_grad():
+        vr = v if v.requires_grad else v.detach().requires_grad_(True)
+        y = forward(cfg, x, flat)
+        J = torch.autograd.grad(y, x, torch.ones_like(y), create_graph=True)[0]
+        hv = torch.autograd.grad(J, x, vr, create_graph=True)[0]
+        rx, rp, rv = _grads(hv, [x, flat, vr], g, create_graph)
+    if not v.requires_grad:
+        rv = None
+    return rx, rp, rv

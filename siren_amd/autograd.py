@@ -89,7 +89,7 @@ class SirenFunction(torch.autograd.Function):
             if ctx.jet is not None and not need_p:
                 ctx.jet.observe_x_gradient_request()
             if J is not None:
-                gx = gy * SirenJacobian.apply(engine, [J], x, flat)
+                gx = gy * SirenJacobian.apply(engine, [J], x, flat, ws)
             else:
                 gx = SirenVJP.apply(engine, ws, x, flat, gy)
         if need_p:
@@ -98,33 +98,80 @@ class SirenFunction(torch.autograd.Function):
 
 
 class SirenJacobian(torch.autograd.Function):
-    """J(x; theta) = dPhi/dx (d_out == 1) as a graph node; the value comes from the jet-mode forward launch."""
+    """J(x; theta) = dPhi/dx (d_out == 1) as a graph node; the value comes from the jet-mode forward launch.
+
+    backward(gJ) is the second-order adjoint: (H gJ, d/dtheta <gJ, J>) from the W3 kernel
+    (siren_second_order). Under create_graph (laplace/divergence, third-order losses) the Hessian-vector product
+    becomes a SirenHVP node whose forward is the same kernel."""
 
     @staticmethod
-    def forward(ctx, engine, holder, x, flat):
-        ctx.engine = engine
+    def forward(ctx, engine, holder, x, flat, ws):
+        ctx.engine, ctx.ws = engine, ws
         ctx.save_for_backward(x, flat)
         return holder[0].clone()  # a fresh output tensor per node (J may feed several gradient() calls)
 
     @staticmethod
     def backward(ctx, gJ):
         x, flat = ctx.saved_tensors
-        gx, gp = _torch_path.jacobian_vjp(ctx.engine.cfg, x, flat, gJ, create_graph=torch.is_grad_enabled())
-        return None, None, gx, gp
+        need_x = ctx.needs_input_grad[2] and _will_execute(ctx, 0)
+        need_p = ctx.needs_input_grad[3] and _will_execute(ctx, 1)
+        gJ = gJ.contiguous()
+        if not torch.is_grad_enabled():
+            gx, gp = ctx.engine.second_order(ctx.ws, x, gJ, want_theta=need_p)
+            return None, None, (gx if need_x else None), gp, None
+        gx = SirenHVP.apply(ctx.engine, ctx.ws, x, flat, gJ) if need_x else None
+        gp = None
+        if need_p:
+            _, gp = _torch_path.jacobian_vjp(ctx.engine.cfg, x, flat, gJ, create_graph=True)
+        return None, None, gx, gp, None
+
+
+class SirenHVP(torch.autograd.Function):
+    """H(x; theta) v (d_out == 1) as a graph node: forward = W3 kernel (x part only); its own backward (a third
+    derivative: laplace_mse training) is recomputed with device torch ops."""
+
+    @staticmethod
+    def forward(ctx, engine, ws, x, flat, v):
+        gx, _ = engine.second_order(ws, x, v.contiguous(), want_theta=False)
+        ctx.engine = engine
+        ctx.save_for_backward(x, flat, v)
+        return gx
+
+    @staticmethod
+    def backward(ctx, g):
+        x, flat, v = ctx.saved_tensors
+        rx, rp, rv = _torch_path.hvp_vjp(ctx.engine.cfg, x, flat, v, g, create_graph=torch.is_grad_enabled())
+        return None, None, rx, rp, rv
 
 
 class SirenVJP(torch.autograd.Function):
-    """gx = sum_j gy_j dPhi_j/dx as a graph node; forward is the fused W1 kernel."""
+    """gx = sum_j gy_j dPhi_j/dx as a graph node; forward is the fused W1 kernel. For d_out == 1 its backward is
+    the W3 kernel with v = gy * ggx (plus <ggx, J> for gy, from the W1 kernel)."""
 
     @staticmethod
     def forward(ctx, engine, ws, x, flat, gy):
         _, gx = engine.forward_grad(ws, x, gy, want_y=False)
-        ctx.engine = engine
+        ctx.engine, ctx.ws = engine, ws
         ctx.save_for_backward(x, flat, gy)
         return gx
 
     @staticmethod
     def backward(ctx, ggx):
         x, flat, gy = ctx.saved_tensors
-        gx, gp, ggy = _torch_path.vjp_vjp(ctx.engine.cfg, x, flat, gy, ggx, create_graph=torch.is_grad_enabled())
-        return None, None, gx, gp, ggy
+        eng = ctx.engine
+        w3_ok = eng.cfg.d_out == 1 and eng.cfg.outermost_linear and eng.grad_supported
+        if torch.is_grad_enabled() or not w3_ok:
+            gx, gp, ggy = _torch_path.vjp_vjp(eng.cfg, x, flat, gy, ggx, create_graph=torch.is_grad_enabled())
+            return None, None, gx, gp, ggy
+        # tensor inputs in order: ws (0), x (1), flat (2), gy (3)
+        need_x = ctx.needs_input_grad[2] and _will_execute(ctx, 1)
+        need_p = ctx.needs_input_grad[3] and _will_execute(ctx, 2)
+        need_gy = ctx.needs_input_grad[4] and _will_execute(ctx, 3)
+        ggx = ggx.contiguous()
+        gx = gp = ggy = None
+        if need_x or need_p:
+            gx, gp = eng.second_order(ctx.ws, x, (gy * ggx).contiguous(), want_theta=need_p)
+        if need_gy:
+            _, J = eng.forward_grad(ctx.ws, x, want_y=False)
+            ggy = (J * ggx).sum(-1, keepdim=True)
+        return None, None, (gx if need_x else None), gp, ggy

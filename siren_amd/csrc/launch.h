@@ -1,0 +1,45 @@
+// launch.h — host-side launchers of the kernel families (one translation unit each, compiled in parallel).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace siren {
+
+struct FusedArgs {
+    const float* ws;
+    const float* x;
+    int64_t n;
+    const float* gy;
+    float* y;
+    float* gx;
+    int d, o, lh;
+    float w0, w;
+    int final_sine;
+    float* abuf;
+    float* dbuf;
+    int64_t n_pad;
+};
+
+// tu_legacy.hip
+void launch_pack(const float* p, float* ws, int d, int o, int lh, int64_t spad, int64_t total, hipStream_t st);
+void launch_legacy_fwd(dim3 grid, hipStream_t st, const FusedArgs& a);
+void launch_legacy_grad(bool store, dim3 grid, hipStream_t st, const FusedArgs& a);
+// tu_w1.hip: mode 0 = W1, 1 = STORE (W2 stage 1); tu_w0.hip: forward only
+void launch_w1(int mode, dim3 grid, hipStream_t st, const FusedArgs& a);
+void launch_w0(dim3 grid, hipStream_t st, const FusedArgs& a);
+// tu_w3.hip
+void launch_w3(bool theta, dim3 grid, hipStream_t st, const float* ws, const float* x, const float* v, int64_t n,
+               float* gx, float* spill, float* A, float* At, float* D, float* Dt, int64_t n_pad, int d, int lh,
+               float w0, float w);
+void launch_small_w3(dim3 grid, hipStream_t st, const float* At, const float* D, const float* Dt, const float* x,
+                     const float* v, int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d, int o,
+                     int lh);
+// tu_train.hip
+void launch_wgrad(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, int64_t n_pad, int64_t tps,
+                  float* partial, int64_t P, int d, int o, int lh, int with_bias);
+void launch_small(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* gy,
+                  int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d, int o, int lh);
+void launch_reduce(dim3 grid, hipStream_t st, const float* partial, int64_t S, int64_t P, float* gp, int64_t S2,
+                   int64_t lo, int64_t hi);
+
+}  // namespace siren

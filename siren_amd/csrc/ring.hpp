@@ -1,0 +1,32 @@
+// ring.hpp — 3-slot LDS weight-slice ring shared by the runtime-loop kernels (fused_kernels.hpp, w3_kernel.hpp).
+#pragma once
+#include "siren_common.h"
+
+namespace siren {
+
+// ------------------------------------------------------------------------------------------------------
+// Weight-slice ring: wave w copies 4 KiB (4 x 1 KiB global_load_lds_dwordx4) of every 16 KiB slice.
+// ------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void ring_issue(const float* __restrict__ stream, float* ring, int s, int nslices,
+                                           int wave, int lane) {
+    if (s < nslices) {
+        const float* src = stream + (int64_t)s * SLICE + wave * 1024 + lane * 4;
+        float* dst = ring + (s % NBUF) * SLICE + wave * 1024;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            __builtin_amdgcn_global_load_lds((const void*)(src + q * 256),
+                                             (__attribute__((address_space(3))) void*)(dst + q * 256), 16, 0, 0);
+    }
+}
+
+// Wait until this wave's part of slice s has landed (slice s+1 may stay in flight), then barrier so
+// every wave's part has landed and every wave has finished reading the slot that is refilled next.
+__device__ __forceinline__ void ring_wait(int s, int nslices) {
+    if (s + 1 < nslices)
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+}
+
+}  // namespace siren

@@ -1,12 +1,13 @@
 // siren_capi.hip — the C ABI of libsiren_amd.so (include/siren_amd.h): validation, workspace sizing and
-// kernel launches. Single translation unit over the kernel headers.
-#include "fused_kernels.hpp"
-#include "train_kernels.hpp"
-#include "w1_kernel.hpp"
+// dispatch to the kernel launchers (launch.h; one translation unit per kernel family).
+#include "launch.h"
+#include "siren_common.h"
+#include "siren_params.h"
 // ==========================================================================================================
 // C ABI
 // ==========================================================================================================
 #include "../../include/siren_amd.h"
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <string>
@@ -93,11 +94,8 @@ int32_t siren_workspace_floats(const siren_cfg* cfg, int64_t* count) {
 int32_t siren_pack(const siren_cfg* cfg, const float* params, float* ws, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (params == nullptr || ws == nullptr) return fail(SIREN_EINVAL, "params/ws is NULL");
-    const int64_t total = ws_floats(cfg);
-    const int threads = 256;
-    const int64_t blocks = std::min<int64_t>((total + threads - 1) / threads, 8192);
-    hipLaunchKernelGGL(siren::pack_kernel, dim3((unsigned)blocks), dim3(threads), 0, (hipStream_t)stream, params,
-                       ws, cfg->d_in, cfg->d_out, cfg->n_hidden, siren::small_pad(cfg->n_hidden), total);
+    siren::launch_pack(params, ws, cfg->d_in, cfg->d_out, cfg->n_hidden, siren::small_pad(cfg->n_hidden),
+                       ws_floats(cfg), (hipStream_t)stream);
     return hip_status("siren_pack");
 }
 
@@ -108,25 +106,13 @@ int32_t siren_forward(const siren_cfg* cfg, const float* ws, const float* x, int
     if (ws == nullptr || x == nullptr || y == nullptr) return fail(SIREN_EINVAL, "ws/x/y is NULL");
     const int64_t blocks = (n + siren::TILE - 1) / siren::TILE;
     if (blocks > 0x7fffffffll) return fail(SIREN_EINVAL, "n too large");
-    const dim3 grid((unsigned)blocks), block(siren::THREADS);
-    if (cfg->outermost_linear && cfg->n_hidden <= 5 && (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0) {
-#define SIREN_LAUNCH_FWD(LHV)                                                                                    \
-    hipLaunchKernelGGL((siren::w1_kernel<LHV, siren::MODE_FWD>), grid, block, 0, (hipStream_t)stream, ws, x, n,      \
-                       (const float*)nullptr, y, (float*)nullptr, cfg->d_in, cfg->d_out, cfg->omega_first,         \
-                       cfg->omega_hidden, (float*)nullptr, (float*)nullptr, (int64_t)0)
-        switch (cfg->n_hidden) {
-            case 1: SIREN_LAUNCH_FWD(1); break;
-            case 2: SIREN_LAUNCH_FWD(2); break;
-            case 3: SIREN_LAUNCH_FWD(3); break;
-            case 4: SIREN_LAUNCH_FWD(4); break;
-            default: SIREN_LAUNCH_FWD(5); break;
-        }
-#undef SIREN_LAUNCH_FWD
-        return hip_status("siren_forward");
-    }
-    hipLaunchKernelGGL((siren::fused_kernel<0, false>), grid, block, 0,
-                       (hipStream_t)stream, ws, x, n, nullptr, y, nullptr, cfg->d_in, cfg->d_out, cfg->n_hidden,
-                       cfg->omega_first, cfg->omega_hidden, cfg->outermost_linear ? 0 : 1);
+    const dim3 grid((unsigned)blocks);
+    siren::FusedArgs fa{ws, x, n, nullptr, y, nullptr, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first,
+                        cfg->omega_hidden, cfg->outermost_linear ? 0 : 1, nullptr, nullptr, 0};
+    if (cfg->outermost_linear && cfg->n_hidden <= 5 && (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0)
+        siren::launch_w0(grid, (hipStream_t)stream, fa);
+    else
+        siren::launch_legacy_fwd(grid, (hipStream_t)stream, fa);
     return hip_status("siren_forward");
 }
 
@@ -140,31 +126,14 @@ int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x
     if (ws == nullptr || x == nullptr || gx == nullptr) return fail(SIREN_EINVAL, "ws/x/gx is NULL");
     const int64_t blocks = (n + siren::TILE - 1) / siren::TILE;
     if (blocks > 0x7fffffffll) return fail(SIREN_EINVAL, "n too large");
-    const dim3 grid((unsigned)blocks), block(siren::THREADS);
+    const dim3 grid((unsigned)blocks);
     const int fs = cfg->outermost_linear ? 0 : 1;
-    const bool legacy = (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) != 0 || fs;
-    if (!legacy) {
-#define SIREN_LAUNCH_W1(LHV)                                                                                    \
-    hipLaunchKernelGGL((siren::w1_kernel<LHV, siren::MODE_W1>), grid, block, 0, (hipStream_t)stream, ws, x, n, gy, y, gx, \
-                       cfg->d_in, cfg->d_out, cfg->omega_first, cfg->omega_hidden, (float*)nullptr, (float*)nullptr, \
-                       (int64_t)0)
-        switch (cfg->n_hidden) {
-            case 1: SIREN_LAUNCH_W1(1); break;
-            case 2: SIREN_LAUNCH_W1(2); break;
-            default: SIREN_LAUNCH_W1(3); break;
-        }
-#undef SIREN_LAUNCH_W1
-        return hip_status("siren_forward_grad");
-    }
-#define SIREN_LAUNCH_GRAD(LHV)                                                                                   \
-    hipLaunchKernelGGL((siren::fused_kernel<LHV, true>), grid, block, 0, (hipStream_t)stream, ws, x, n, gy, y, gx, \
-                       cfg->d_in, cfg->d_out, LHV, cfg->omega_first, cfg->omega_hidden, fs)
-    switch (cfg->n_hidden) {
-        case 1: SIREN_LAUNCH_GRAD(1); break;
-        case 2: SIREN_LAUNCH_GRAD(2); break;
-        default: SIREN_LAUNCH_GRAD(3); break;
-    }
-#undef SIREN_LAUNCH_GRAD
+    siren::FusedArgs fa{ws, x, n, gy, y, gx, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first,
+                        cfg->omega_hidden, fs, nullptr, nullptr, 0};
+    if ((cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) != 0 || fs)
+        siren::launch_legacy_grad(false, grid, (hipStream_t)stream, fa);
+    else
+        siren::launch_w1(siren::MODE_W1, grid, (hipStream_t)stream, fa);
     return hip_status("siren_forward_grad");
 }
 
@@ -197,38 +166,91 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
     float* partial = tws + 2 * plan.act_floats;
     const dim3 grid((unsigned)(plan.n_pad / siren::TILE)), block(siren::THREADS);
     const int fs = cfg->outermost_linear ? 0 : 1;
-    if ((cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0 && !fs) {
-#define SIREN_LAUNCH_W1S(LHV)                                                                               \
-    hipLaunchKernelGGL((siren::w1_kernel<LHV, siren::MODE_STORE>), grid, block, 0, st, ws, x, n, gy, (float*)nullptr, gx, \
-                       cfg->d_in, cfg->d_out, cfg->omega_first, cfg->omega_hidden, abuf, dbuf, plan.n_pad)
-        switch (cfg->n_hidden) {
-            case 1: SIREN_LAUNCH_W1S(1); break;
-            case 2: SIREN_LAUNCH_W1S(2); break;
-            default: SIREN_LAUNCH_W1S(3); break;
-        }
-#undef SIREN_LAUNCH_W1S
-    } else {
-#define SIREN_LAUNCH_STORE(LHV)                                                                                    \
-    hipLaunchKernelGGL((siren::fused_kernel<LHV, true, true>), grid, block, 0, st, ws, x, n, gy, (float*)nullptr, gx, \
-                       cfg->d_in, cfg->d_out, LHV, cfg->omega_first, cfg->omega_hidden, fs, abuf, dbuf, plan.n_pad)
-    switch (cfg->n_hidden) {
-        case 1: SIREN_LAUNCH_STORE(1); break;
-        case 2: SIREN_LAUNCH_STORE(2); break;
-        default: SIREN_LAUNCH_STORE(3); break;
-    }
-#undef SIREN_LAUNCH_STORE
-    }
+    siren::FusedArgs fa{ws, x, n, gy, nullptr, gx, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first,
+                        cfg->omega_hidden, fs, abuf, dbuf, plan.n_pad};
+    if ((cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0 && !fs)
+        siren::launch_w1(siren::MODE_STORE, grid, st, fa);
+    else
+        siren::launch_legacy_grad(true, grid, st, fa);
     if (int rc = hip_status("siren_backward (fused store)")) return rc;
-    hipLaunchKernelGGL(siren::wgrad_kernel, dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden), block, 0, st, abuf,
-                       dbuf, plan.n_pad, plan.tps, partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden);
+    siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden), st, abuf, dbuf, plan.n_pad, plan.tps,
+                        partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1);
     if (int rc = hip_status("siren_backward (wgrad)")) return rc;
-    hipLaunchKernelGGL(siren::small_kernel, dim3((unsigned)plan.splits), block, 0, st, abuf, dbuf, x, gy, n, plan.n_pad,
-                       plan.tps, partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden);
+    siren::launch_small(dim3((unsigned)plan.splits), st, abuf, dbuf, x, gy, n, plan.n_pad, plan.tps, partial, P,
+                        cfg->d_in, cfg->d_out, cfg->n_hidden);
     if (int rc = hip_status("siren_backward (small)")) return rc;
     const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 4096);
-    hipLaunchKernelGGL(siren::reduce_kernel, dim3((unsigned)rblocks), dim3(256), 0, st, partial, plan.splits, P,
-                       gparams);
+    siren::launch_reduce(dim3((unsigned)rblocks), st, partial, plan.splits, P, gparams, 0, 0, 0);
     return hip_status("siren_backward (reduce)");
+}
+
+// ---- W3: second-order adjoint (Hessian-vector product + mixed theta gradient), d_out == 1 ---------------
+namespace {
+struct W3Plan {
+    int64_t n_pad, tiles, splits, tps, spill_floats, buf_floats, partial_floats, total;
+    W3Plan(const siren_cfg* cfg, int64_t n, bool theta) {
+        const TrainPlan tp(cfg, n);
+        n_pad = tp.n_pad;
+        tiles = tp.tiles;
+        splits = tp.splits;
+        tps = tp.tps;
+        spill_floats = n_pad * (int64_t)(cfg->n_hidden + 1) * 3 * siren::H;
+        buf_floats = theta ? (int64_t)(cfg->n_hidden + 1) * n_pad * siren::H : 0;
+        partial_floats = theta ? 2 * splits * param_count(cfg) : 0;
+        total = spill_floats + 4 * buf_floats + partial_floats;
+    }
+};
+}  // namespace
+
+int32_t siren_second_order_ws_floats(const siren_cfg* cfg, int64_t n, int32_t want_theta, int64_t* count) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
+    *count = W3Plan(cfg, n, want_theta != 0).total;
+    return SIREN_OK;
+}
+
+int32_t siren_second_order(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
+                           float* tws, float* gx, float* gparams, void* stream) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (cfg->n_hidden > siren::MAX_LH_GRAD)
+        return fail(SIREN_EUNSUPPORTED, "siren_second_order needs 1 <= num_hidden_layers <= 3");
+    if (cfg->d_out != 1 || !cfg->outermost_linear)
+        return fail(SIREN_EUNSUPPORTED, "siren_second_order covers d_out == 1 with a linear output layer");
+    if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    if (ws == nullptr || tws == nullptr || gx == nullptr || (n > 0 && (x == nullptr || v == nullptr)))
+        return fail(SIREN_EINVAL, "ws/x/v/tws/gx is NULL");
+    const bool theta = gparams != nullptr;
+    const W3Plan plan(cfg, n, theta);
+    const hipStream_t st = (hipStream_t)stream;
+    const int64_t P = param_count(cfg);
+    if (n == 0) {
+        if (theta) (void)hipMemsetAsync(gparams, 0, P * sizeof(float), st);
+        return hip_status("siren_second_order");
+    }
+    float* spill = tws;
+    float* A = spill + plan.spill_floats;
+    float* At = A + plan.buf_floats;
+    float* D = At + plan.buf_floats;
+    float* Dt = D + plan.buf_floats;
+    float* partial = Dt + plan.buf_floats;
+    const dim3 grid((unsigned)(plan.n_pad / siren::TILE));
+    siren::launch_w3(theta, grid, st, ws, x, v, n, gx, spill, A, At, D, Dt, plan.n_pad, cfg->d_in, cfg->n_hidden,
+                     cfg->omega_first, cfg->omega_hidden);
+    if (int rc = hip_status("siren_second_order (w3)")) return rc;
+    if (!theta) return SIREN_OK;
+    const dim3 wgrid((unsigned)plan.splits, (unsigned)cfg->n_hidden);
+    siren::launch_wgrad(wgrid, st, A, D, plan.n_pad, plan.tps, partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1);
+    siren::launch_wgrad(wgrid, st, At, Dt, plan.n_pad, plan.tps, partial + plan.splits * P, P, cfg->d_in, cfg->d_out,
+                        cfg->n_hidden, 0);
+    if (int rc = hip_status("siren_second_order (wgrad)")) return rc;
+    siren::launch_small_w3(dim3((unsigned)plan.splits), st, At, D, Dt, x, v, n, plan.n_pad, plan.tps, partial, P,
+                           cfg->d_in, cfg->d_out, cfg->n_hidden);
+    if (int rc = hip_status("siren_second_order (small)")) return rc;
+    const siren::ParamOffsets off(cfg->d_in, cfg->d_out, cfg->n_hidden);
+    const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 4096);
+    siren::launch_reduce(dim3((unsigned)rblocks), st, partial, plan.splits, P, gparams, plan.splits, off.hidden0,
+                         off.wout);
+    return hip_status("siren_second_order (reduce)");
 }
 
 }  // extern "C"

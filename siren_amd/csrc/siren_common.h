@@ -29,6 +29,10 @@ constexpr int MAXO = 4;           // max out_features of the fused kernels
 constexpr int MAX_LH_FWD = 8;     // max hidden layers of the forward-only kernel
 constexpr int MAX_LH_GRAD = 3;    // max hidden layers of the forward+grad kernel (cos kept in VGPRs)
 
+// w1_kernel modes: W1 (forward + vjp_x), STORE (W2 backward stage 1: also writes a_l, delta_l), FWD (W0: forward
+// only, sin epilogues without cos, output layer folded into a final serial epilogue).
+enum { MODE_W1 = 0, MODE_STORE = 1, MODE_FWD = 2 };
+
 // Small-parameter block (head of the workspace, copied to LDS by every workgroup):
 //   [SM_W0,  +4H)  W0T[k][n] = W_0[n][k]  (k < d_in, zero padded to 4 rows)
 //   [SM_WO,  +4H)  WoT[j][n] = W_out[j][n] (j < d_out, zero padded)

@@ -37,7 +37,7 @@ __device__ __forceinline__ void wg_issue(const float* __restrict__ dsrc, const f
 __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restrict__ abuf,
                                                           const float* __restrict__ dbuf, int64_t n_pad,
                                                           int64_t tps, float* __restrict__ partial, int64_t P,
-                                                          int d, int o, int lh) {
+                                                          int d, int o, int lh, int with_bias = 1) {
     __shared__ __attribute__((aligned(16))) float ring[WG_NBUF * WG_SLOT];
     const ParamOffsets off(d, o, lh);
     const int s = blockIdx.x, l = blockIdx.y + 1;
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 dW[(int64_t)(128 * wr + 16 * rb + 4 * g + q) * H + 128 * wc + 16 * cb + i] = acc[rb][cb][q];
-    out[off.b(l) + threadIdx.x] = bsum;
+    out[off.b(l) + threadIdx.x] = with_bias ? bsum : 0.f;
 }
 
 // grid (S): first-layer weight/bias grads from (delta_0, x) and output-layer grads from (gy, a_LH).
@@ -146,10 +146,14 @@ __global__ __launch_bounds__(THREADS) void small_kernel(const float* __restrict_
     if (t < o) out[off.bout + t] = gbo;
 }
 
-__global__ void reduce_kernel(const float* __restrict__ partial, int64_t S, int64_t P, float* __restrict__ gp) {
+// gp[i] = sum over the partial slabs; indices in [lo, hi) (the hidden layers' W/b) sum S + S2 slabs, the others
+// (first and output layer, written by the small kernels into the first S slabs only) sum S.
+__global__ void reduce_kernel(const float* __restrict__ partial, int64_t S, int64_t P, float* __restrict__ gp,
+                              int64_t S2 = 0, int64_t lo = 0, int64_t hi = 0) {
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < P; idx += (int64_t)gridDim.x * blockDim.x) {
         float acc = 0.f;
-        for (int64_t s = 0; s < S; ++s) acc += partial[s * P + idx];
+        const int64_t ns = (idx >= lo && idx < hi) ? S + S2 : S;
+        for (int64_t s = 0; s < ns; ++s) acc += partial[s * P + idx];
         gp[idx] = acc;
     }
 }

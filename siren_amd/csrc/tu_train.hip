@@ -1,0 +1,24 @@
+// tu_train.hip — split-K weight-gradient, first/last-layer and slab-reduction kernels.
+#include "launch.h"
+#include "train_kernels.hpp"
+
+namespace siren {
+
+void launch_wgrad(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, int64_t n_pad, int64_t tps,
+                  float* partial, int64_t P, int d, int o, int lh, int with_bias) {
+    hipLaunchKernelGGL(wgrad_kernel, grid, dim3(THREADS), 0, st, abuf, dbuf, n_pad, tps, partial, P, d, o, lh,
+                       with_bias);
+}
+
+void launch_small(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* gy,
+                  int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d, int o, int lh) {
+    hipLaunchKernelGGL(small_kernel, grid, dim3(THREADS), 0, st, abuf, dbuf, x, gy, n, n_pad, tps, partial, P, d, o,
+                       lh);
+}
+
+void launch_reduce(dim3 grid, hipStream_t st, const float* partial, int64_t S, int64_t P, float* gp, int64_t S2,
+                   int64_t lo, int64_t hi) {
+    hipLaunchKernelGGL(reduce_kernel, grid, dim3(256), 0, st, partial, S, P, gp, S2, lo, hi);
+}
+
+}  // namespace siren

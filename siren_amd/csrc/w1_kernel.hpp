@@ -36,9 +36,6 @@ constexpr int W1_NBUF = 4;  // ring slots of this kernel (64 KiB)
 
 enum { EPI_FIRST = 0, EPI_SINCOS = 1, EPI_SEED = 2, EPI_DELTA = 3 };
 
-// Kernel modes: W1 (forward + vjp_x), W1 STORE (W2 backward stage 1), FWD (W0: forward only, sin epilogues
-// without cos, output layer folded into a final serial epilogue).
-enum { MODE_W1 = 0, MODE_STORE = 1, MODE_FWD = 2 };
 
 template <int G, int LH>
 constexpr int epi_kind() {

@@ -1,0 +1,258 @@
+// w3_kernel.hpp — second-order adjoint of the SIREN (work unit W3), d_out == 1, for gfx950.
+//
+// What autograd asks of the graph node J(x; theta) = dPhi/dx when a loss depends on the gradient
+// (loss_functions.py:84-89 gradients_mse, :214-238 sdf; and every divergence() call inside laplace,
+// diff_operators.py:27-36): given a per-coordinate cotangent v = gJ (n, d), return
+//     gx     = d/dx     sum_c <v_c, J(x_c)>  = H(x_c) v_c        (Hessian-vector product)
+//     gtheta = d/dtheta sum_c <v_c, J(x_c)>                       (mixed second derivative; optional)
+// Reverse-over-forward: F = sum_c ydot_c where ydot is the forward-mode tangent of y along v_c.
+//   forward (per layer, primal + tangent share every weight A operand: 2 MFMAs per ds_read):
+//       z_l = W_l a_{l-1} + b_l,   zd_l = W_l ad_{l-1}      (z_0 = W0 x + b0, zd_0 = W0 v on VALU)
+//       a_l = sin(w z_l), c_l = cos(w z_l), ad_l = w c_l zd_l
+//   reverse (adjoints ab of a and adb of ad; adb_L = Wout^T, ab_L = 0):
+//       zdb_l = w c_l adb_l
+//       zb_l  = w c_l ab_l - w^2 a_l zd_l adb_l
+//       adb_{l-1} = W_l^T zdb_l,  ab_{l-1} = W_l^T zb_l,  gx = W0^T zb_0
+//   weight gradients (THETA): dW_l = zdb_l ad_{l-1}^T + zb_l a_{l-1}^T (the split-K wgrad kernel, K = 2N),
+//       db_l = sum zb_l, dW0 = zdb_0 v^T + zb_0 x^T, dWout = sum ad_L, dbout = 0.
+// (c_l, zd_l, a_l) of every layer go to a per-wave spill area in HBM in the forward sweep and come back in the
+// reverse sweep (coalesced 1 KiB per block; a WG's 768 KiB usually still sits in the 256 MiB Infinity Cache).
+// Same weight stream (packed forward + transposed slices) and 3-slot LDS ring as the W1 kernels.
+#pragma once
+#include "ring.hpp"
+#include "siren_common.h"
+#include "siren_params.h"
+
+namespace siren {
+
+// A-operand pass over one slice for the primal (bp) and tangent (bt) column tiles.
+__device__ __forceinline__ void slice_mma2(const float* sl, const f32x4& bp, const f32x4& bt, f32x4 (&accp)[NB],
+                                           f32x4 (&acct)[NB]) {
+    f32x4 a = *(const f32x4*)(sl);
+#pragma unroll
+    for (int ob = 0; ob < NB; ++ob) {
+        f32x4 nx;
+        if (ob + 1 < NB) nx = *(const f32x4*)(sl + (ob + 1) * 256);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            accp[ob] = mfma4(a[r], bp[r], accp[ob]);
+            acct[ob] = mfma4(a[r], bt[r], acct[ob]);
+        }
+        if (ob + 1 < NB) a = nx;
+    }
+}
+
+__device__ __forceinline__ void layer_mma2(const float* __restrict__ stream, float* ring, int& s, int nslices,
+                                           int wave, int lane, const f32x4 (&bp)[NB], const f32x4 (&bt)[NB],
+                                           f32x4 (&accp)[NB], f32x4 (&acct)[NB]) {
+#pragma unroll
+    for (int ob = 0; ob < NB; ++ob) {
+        accp[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
+        acct[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) {
+        ring_wait(s, nslices);
+        ring_issue(stream, ring, s + 2, nslices, wave, lane);
+        slice_mma2(ring + (s % NBUF) * SLICE + lane * 4, bp[kb], bt[kb], accp, acct);
+        ++s;
+    }
+}
+
+// spill slot of (layer l, quantity q in {c, zd, a}, block b) for this lane: 1 KiB per block, lane-contiguous
+__device__ __forceinline__ f32x4* spill_at(float* wave_spill, int l, int q, int b, int lane) {
+    return (f32x4*)(wave_spill + ((int64_t)(l * 3 + q) * NB + b) * 256 + lane * 4);
+}
+
+template <int LH, bool THETA>
+__global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict__ ws, const float* __restrict__ x,
+                                                        const float* __restrict__ v, int64_t n, float* __restrict__ gx,
+                                                        float* __restrict__ spill, float* __restrict__ A,
+                                                        float* __restrict__ At, float* __restrict__ D,
+                                                        float* __restrict__ Dt, int64_t n_pad, int d, float w0,
+                                                        float w) {
+    __shared__ __attribute__((aligned(16))) float lds[NBUF * SLICE + SMALL_MAX];
+    float* ring = lds;
+    float* sm = lds + NBUF * SLICE;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane >> 4, c = lane & 15;
+    const int nslices = 2 * LH * NB;
+    const float* stream = ws + small_pad(LH);
+    const int64_t tile = (int64_t)blockIdx.x * WAVES + wave;
+    float* wsp = spill + tile * (int64_t)(LH + 1) * 3 * NB * 256;
+    const int64_t lstride = n_pad * H;
+    const int64_t toff = tile * (H * 16) + 4 * g * 16 + c;
+
+    {
+        const int nf4 = (small_floats(LH) + 3) / 4;
+        for (int e = threadIdx.x; e < nf4; e += THREADS) ((f32x4*)sm)[e] = ((const f32x4*)ws)[e];
+    }
+    const int64_t coord = (int64_t)blockIdx.x * TILE + wave * 16 + c;
+    const bool valid = coord < n;
+    float xv[MAXD], vv[MAXD];
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k) {
+        xv[k] = (valid && k < d) ? x[coord * d + k] : 0.f;
+        vv[k] = (valid && k < d) ? v[coord * d + k] : 0.f;
+    }
+    __syncthreads();
+    ring_issue(stream, ring, 0, nslices, wave, lane);
+    ring_issue(stream, ring, 1, nslices, wave, lane);
+
+    f32x4 actp[NB], actt[NB], accp[NB], acct[NB];
+    // ---- layer 0 (VALU): z0 = W0 x + b0, zd0 = W0 v ----------------------------------------------------
+#pragma unroll
+    for (int rb = 0; rb < NB; ++rb) {
+        const int nb = 16 * rb + 4 * g;
+        f32x4 z = *(const f32x4*)(sm + SM_BIAS + nb);
+        f32x4 zd = {0.f, 0.f, 0.f, 0.f};
+        f32x4 zx = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < MAXD; ++k) {
+            if (k < d) {
+                const f32x4 wk = *(const f32x4*)(sm + SM_W0 + k * H + nb);
+                zx = k == 0 ? xv[0] * wk : zx + xv[k] * wk;
+                zd = zd + vv[k] * wk;
+            }
+        }
+        z = zx + z;
+        f32x4 sn, cs;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float a_, c_;
+            sincos_fast(w0 * z[r], a_, c_);
+            sn[r] = a_;
+            cs[r] = c_;
+        }
+        actp[rb] = sn;
+        actt[rb] = (w0 * cs) * zd;
+        *spill_at(wsp, 0, 0, rb, lane) = cs;
+        *spill_at(wsp, 0, 1, rb, lane) = zd;
+        *spill_at(wsp, 0, 2, rb, lane) = sn;
+        if (THETA) {
+            store_block(A + toff, rb, actp[rb]);
+            store_block(At + toff, rb, actt[rb]);
+        }
+    }
+
+    // ---- hidden layers: primal + tangent GEMMs ------------------------------------------------------------
+    int s = 0;
+#pragma unroll 1
+    for (int l = 1; l <= LH; ++l) {
+        layer_mma2(stream, ring, s, nslices, wave, lane, actp, actt, accp, acct);
+        const float* bl = sm + SM_BIAS + l * H + 4 * g;
+#pragma unroll
+        for (int rb = 0; rb < NB; ++rb) {
+            const f32x4 z = accp[rb] + *(const f32x4*)(bl + 16 * rb);
+            const f32x4 zd = acct[rb];
+            f32x4 sn, cs;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float a_, c_;
+                sincos_fast(w * z[r], a_, c_);
+                sn[r] = a_;
+                cs[r] = c_;
+            }
+            actp[rb] = sn;
+            actt[rb] = (w * cs) * zd;
+            *spill_at(wsp, l, 0, rb, lane) = cs;
+            *spill_at(wsp, l, 1, rb, lane) = zd;
+            *spill_at(wsp, l, 2, rb, lane) = sn;
+            if (THETA) {
+                store_block(A + l * lstride + toff, rb, actp[rb]);
+                store_block(At + l * lstride + toff, rb, actt[rb]);
+            }
+        }
+    }
+
+    // ---- reverse: seed at layer L (adb_L = Wout^T, ab_L = 0) -------------------------------------------------
+#pragma unroll
+    for (int rb = 0; rb < NB; ++rb) {
+        const f32x4 adb = *(const f32x4*)(sm + SM_SEED + 16 * rb + 4 * g);
+        const f32x4 cs = *spill_at(wsp, LH, 0, rb, lane);
+        const f32x4 zd = *spill_at(wsp, LH, 1, rb, lane);
+        const f32x4 sn = *spill_at(wsp, LH, 2, rb, lane);
+        actt[rb] = (w * cs) * adb;
+        actp[rb] = -(w * w) * sn * zd * adb;
+        if (THETA) {
+            store_block(D + LH * lstride + toff, rb, actp[rb]);
+            store_block(Dt + LH * lstride + toff, rb, actt[rb]);
+        }
+    }
+#pragma unroll 1
+    for (int l = LH; l >= 1; --l) {
+        layer_mma2(stream, ring, s, nslices, wave, lane, actp, actt, accp, acct);  // accp = ab, acct = adb (l-1)
+        const float wl = (l == 1) ? w0 : w;
+#pragma unroll
+        for (int rb = 0; rb < NB; ++rb) {
+            const f32x4 cs = *spill_at(wsp, l - 1, 0, rb, lane);
+            const f32x4 zd = *spill_at(wsp, l - 1, 1, rb, lane);
+            const f32x4 sn = *spill_at(wsp, l - 1, 2, rb, lane);
+            const f32x4 wc = wl * cs;
+            actt[rb] = wc * acct[rb];
+            actp[rb] = wc * accp[rb] - (wl * wl) * sn * zd * acct[rb];
+            if (THETA) {
+                store_block(D + (l - 1) * lstride + toff, rb, actp[rb]);
+                store_block(Dt + (l - 1) * lstride + toff, rb, actt[rb]);
+            }
+        }
+    }
+    // ---- gx = W0^T zb_0 ------------------------------------------------------------------------------------
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k) {
+        if (k < d) {
+            float p = 0.f;
+#pragma unroll
+            for (int rb = 0; rb < NB; ++rb) {
+                const f32x4 wk = *(const f32x4*)(sm + SM_W0 + k * H + 16 * rb + 4 * g);
+                p += wk[0] * actp[rb][0] + wk[1] * actp[rb][1] + wk[2] * actp[rb][2] + wk[3] * actp[rb][3];
+            }
+            p = sum_groups(p);
+            if (valid && g == 0) gx[coord * d + k] = p;
+        }
+    }
+}
+
+// First/last-layer gradients of the W3 objective: dW0 = zdb_0 v^T + zb_0 x^T, db0 = sum zb_0,
+// dWout[0] = sum ad_L, dbout = 0. Grid (S): block s reduces tiles [s*tps, (s+1)*tps).
+__global__ __launch_bounds__(THREADS) void small_w3_kernel(const float* __restrict__ At, const float* __restrict__ D,
+                                                           const float* __restrict__ Dt, const float* __restrict__ x,
+                                                           const float* __restrict__ v, int64_t n, int64_t n_pad,
+                                                           int64_t tps, float* __restrict__ partial, int64_t P, int d,
+                                                           int o, int lh) {
+    const ParamOffsets off(d, o, lh);
+    const int s = blockIdx.x, t = threadIdx.x;
+    const int64_t T = n_pad / 16;
+    const int64_t t0 = (int64_t)s * tps, t1 = t0 + tps < T ? t0 + tps : T;
+    const float* atL = At + (int64_t)lh * n_pad * H;
+    float gw0[MAXD] = {0.f, 0.f, 0.f, 0.f}, gb0 = 0.f, gwo = 0.f;
+    for (int64_t tile = t0; tile < t1; ++tile) {
+        const f32x4* drow = (const f32x4*)(D + tile * (H * 16) + t * 16);
+        const f32x4* dtrow = (const f32x4*)(Dt + tile * (H * 16) + t * 16);
+        const f32x4* arow = (const f32x4*)(atL + tile * (H * 16) + t * 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const f32x4 dv = drow[q], dtv = dtrow[q], av = arow[q];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t cc = tile * 16 + 4 * q + r;
+                if (cc < n) {
+                    gb0 += dv[r];
+                    gwo += av[r];
+#pragma unroll
+                    for (int k = 0; k < MAXD; ++k)
+                        if (k < d) gw0[k] += dtv[r] * v[cc * d + k] + dv[r] * x[cc * d + k];
+                }
+            }
+        }
+    }
+    float* out = partial + (int64_t)s * P;
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k)
+        if (k < d) out[off.w0 + (int64_t)t * d + k] = gw0[k];
+    out[off.b0 + t] = gb0;
+    out[off.wout + t] = gwo;
+    if (t == 0) out[off.bout] = 0.f;
+}
+
+}  // namespace siren

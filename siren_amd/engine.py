@@ -133,3 +133,24 @@ class SirenEngine:
                                            ctypes.c_void_p(0), _ptr(gx), _ptr(gp), _stream(x.device)),
                    'siren_backward')
         return gx, gp
+
+    def second_order(self, ws, x, v, want_theta=True):
+        """W3: (H v, d/dtheta sum <v, dPhi/dx>) for d_out == 1 — the backward of the dPhi/dx graph node
+        (gradients_mse / sdf / divergence). Returns (gx, gparams or None)."""
+        self._require()
+        if not self.grad_supported or self.cfg.d_out != 1 or not self.cfg.outermost_linear:
+            raise _lib.SirenUnsupported('siren_second_order covers d_out == 1, linear output, 1..3 hidden layers')
+        x = self._check_x(x)
+        n = x.shape[0]
+        v = v.contiguous()
+        if v.shape != x.shape or v.dtype != torch.float32 or v.device != x.device:
+            raise ValueError('v must be fp32 %s on %s' % (tuple(x.shape), x.device))
+        cnt = ctypes.c_int64()
+        _lib.check(self.lib.siren_second_order_ws_floats(ctypes.byref(self.cfg), n, 1 if want_theta else 0,
+                                                         ctypes.byref(cnt)), 'siren_second_order_ws_floats')
+        tws = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
+        gx = torch.empty(n, self.cfg.d_in, dtype=torch.float32, device=x.device)
+        gp = torch.empty(self.param_count, dtype=torch.float32, device=x.device) if want_theta else None
+        _lib.check(self.lib.siren_second_order(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(v), _ptr(tws),
+                                               _ptr(gx), _ptr(gp), _stream(x.device)), 'siren_second_order')
+        return gx, gp

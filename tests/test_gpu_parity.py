@@ -335,3 +335,64 @@ def test_g5_psnr_trajectory(cuda, manifest):
     assert abs(p - manifest['G5_psnr_final']) < 0.05, (p, manifest['G5_psnr_final'])
     for i in range(0, 300, 10):
         assert abs(losses[i] - ref[i]) <= 0.02 * ref[i] + 1e-6, (i, losses[i], ref[i])
+
+
+# ---------------------------------------------------------------------------------------------------------
+# W3: second-order adjoint (Hessian-vector product + mixed theta gradient)
+# ---------------------------------------------------------------------------------------------------------
+def torch_second_order_ref(x, layers, v, **kw):
+    xt = torch.tensor(np.asarray(x), dtype=torch.float64, requires_grad=True)
+    params = [torch.tensor(np.asarray(t), dtype=torch.float64, requires_grad=True) for W, b in layers for t in (W, b)]
+    y = O.torch_forward(xt, params, **kw)
+    J = torch.autograd.grad(y, xt, torch.ones_like(y), create_graph=True)[0]
+    F = (J * torch.tensor(np.asarray(v), dtype=torch.float64)).sum()
+    grads = torch.autograd.grad(F, [xt] + params, allow_unused=True)
+    gp = torch.cat([(torch.zeros_like(p) if g is None else g).reshape(-1) for g, p in zip(grads[1:], params)])
+    return grads[0].numpy(), gp.numpy()
+
+
+@pytest.mark.parametrize('n,d,L', [(1, 2, 3), (1000, 2, 3), (4097, 3, 3), (300, 1, 1), (777, 4, 2)])
+def test_w3_second_order_vs_fp64(cuda, n, d, L):
+    layers = random_layers(d, L, 1, seed=n + d)
+    eng = engine(d, L, 1)
+    ws = eng.pack(to_dev(O.flatten(layers), cuda))
+    rng = np.random.default_rng(n)
+    x = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    v = rng.normal(size=(n, d)).astype(np.float32)
+    hv, gp = eng.second_order(ws, to_dev(x, cuda), to_dev(v, cuda), want_theta=True)
+    hv2, none = eng.second_order(ws, to_dev(x, cuda), to_dev(v, cuda), want_theta=False)
+    rhv, rgp = torch_second_order_ref(x, layers, v)
+    assert none is None and torch.equal(hv, hv2)
+    assert np.max(np.abs(hv.cpu().numpy() - rhv)) <= tol_rel(rhv)
+    assert np.max(np.abs(gp.cpu().numpy() - rgp)) <= 1e-4 * np.max(np.abs(rgp))
+
+
+def test_w3_trained_regime(cuda, g2, g1):
+    """Large-derivative regime (G2 weights: |grad| ~ 150, |lap| ~ 1e5)."""
+    flat, layers = weights_of(g2)
+    eng = engine()
+    ws = eng.pack(to_dev(flat, cuda))
+    x = g1['coords'][0][:2048]
+    v = np.random.default_rng(0).normal(size=x.shape).astype(np.float32)
+    hv, gp = eng.second_order(ws, to_dev(x, cuda), to_dev(v, cuda))
+    rhv, rgp = torch_second_order_ref(x, layers, v)
+    assert np.max(np.abs(hv.cpu().numpy() - rhv)) <= tol_rel(rhv)
+    assert np.max(np.abs(gp.cpu().numpy() - rgp)) <= 1e-4 * np.max(np.abs(rgp))
+
+
+@pytest.mark.parametrize('jet', [True, False])
+def test_second_order_losses_use_hip_kernel(cuda, g1, jet, monkeypatch):
+    """gradients_mse training runs the W3 kernel, not the device torch recompute."""
+    from siren_amd import _torch_path, loss_functions as Lf
+    def boom(*a, **k):
+        raise AssertionError('torch fallback used on a first/second-order path')
+    monkeypatch.setattr(_torch_path, 'jacobian_vjp', boom)
+    monkeypatch.setattr(_torch_path, 'vjp_vjp', boom)
+    m = load_model(g1, cuda, jet=jet)
+    out = m({'coords': to_dev(g1['coords'], cuda)})
+    losses = Lf.gradients_mse(out, {'gradients': to_dev(g1['gt_gradients'], cuda)})
+    m.zero_grad()
+    sum(v.mean() for v in losses.values()).backward()
+    for k, p in m.named_parameters():
+        ref = g1['G1_gradients_mse_grad_' + k]
+        assert np.max(np.abs(p.grad.cpu().numpy() - ref)) <= 1e-4 * max(np.max(np.abs(ref)), 1e-30) + 1e-12, k
