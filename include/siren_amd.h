@@ -56,7 +56,7 @@ enum {
  * hidden_features, hidden_layers, out_features, outermost_linear, first_omega_0, hidden_omega_0). */
 typedef struct siren_cfg {
     int32_t d_in;             /* in_features, 1..4                                         */
-    int32_t hidden;           /* hidden_features (256 in the fused kernels)                */
+    int32_t hidden;           /* hidden_features: 256 or 512 in the fused kernels          */
     int32_t n_hidden;         /* num_hidden_layers: H->H layers between first and last    */
     int32_t d_out;            /* out_features, 1..4                                        */
     float omega_first;        /* w of the first sine layer (30; Sine hard-codes 30)        */
@@ -87,7 +87,8 @@ int32_t siren_forward(const siren_cfg* cfg, const float* ws, const float* x, int
 /* W1 (forward + coordinate vector-Jacobian product) in ONE launch:
  *   y  = Phi(x)                       (skipped when y == NULL)
  *   gx = sum_j gy_j * dPhi_j/dx       (gy == NULL means gy = ones: diff_operators.gradient, d.o.py:39-43)
- * n_hidden must be 1..3 (cos(w z_l) of every layer stays in registers). */
+ * hidden 256: n_hidden must be 1..3 (cos(w z_l) of every layer stays in registers); hidden 512: 1..8 (cos is
+ * spilled to a stream-ordered scratch allocation, hipMallocAsync/hipFreeAsync on `stream`). */
 int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x, int64_t n,
                            const float* gy, float* y, float* gx, void* stream);
 
@@ -108,7 +109,7 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
  * primal activations and adjoints of every layer plus 2*S partial slabs). */
 int32_t siren_second_order_ws_floats(const siren_cfg* cfg, int64_t n, int32_t want_theta, int64_t* count);
 
-/* W3, second-order adjoint for d_out == 1 (the backward of the dPhi/dx graph node that gradients_mse / sdf /
+/* W3, second-order adjoint for hidden 256, d_out == 1 (the backward of the dPhi/dx graph node that gradients_mse / sdf /
  * divergence differentiate, diff_operators.py:27-43, loss_functions.py:84-89, 214-238): with v (n, d_in) the
  * cotangent of J = dPhi/dx,
  *   gx (n, d_in)          = H(x) v                      (Hessian-vector product)

@@ -1,5 +1,6 @@
 """Device-side torch restatement of the SIREN op sequence, used ONLY for the higher-order adjoints that have no
-HIP kernel yet (second/third derivatives w.r.t. theta: gradients_mse/sdf/laplace_mse training, W3/W4s).
+HIP kernel yet: third derivatives (the backward of a Hessian-vector product node: laplace_mse training, W4s),
+second derivatives of hidden-512 networks, and vector outputs (d_out > 1) under create_graph.
 
 It runs on the same ROCm device as the kernels (never on the CPU) and re-records the reference's op order
 (modules.py:23-24 matmul + bias, :34 sin(w z)) so autograd can differentiate it to any order. The first-order

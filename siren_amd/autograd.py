@@ -15,9 +15,10 @@ model_in, ones, create_graph=True) (diff_operators.py:42, :35) and training call
 Which gradients autograd actually wants is read from the engine (torch._C._will_engine_execute_node on the
 next nodes), because ctx.needs_input_grad is static: autograd.grad(y, [x]) must not pay for weight gradients.
 
-Second- and third-order adjoints (SirenJacobian/SirenVJP.backward: the gradients_mse/sdf/laplace_mse training
-steps) are, in this round, recomputed through siren_amd._torch_path on the device — the
-HIP W3/W4 kernels are the next rows.
+Second-order adjoints (SirenJacobian/SirenVJP.backward: gradients_mse / sdf training, the Laplacian's
+Hessian-vector products) run on the W3 kernel (siren_second_order) for hidden 256 and d_out == 1.
+Third-order adjoints (SirenHVP.backward: laplace_mse training, W4s), second order at hidden 512 and vector
+outputs under create_graph are recomputed through siren_amd._torch_path on the device.
 """
 import torch
 
@@ -116,6 +117,9 @@ class SirenJacobian(torch.autograd.Function):
         need_x = ctx.needs_input_grad[2] and _will_execute(ctx, 0)
         need_p = ctx.needs_input_grad[3] and _will_execute(ctx, 1)
         gJ = gJ.contiguous()
+        if not ctx.engine.second_order_supported:  # hidden 512: no W3 kernel yet
+            gx, gp = _torch_path.jacobian_vjp(ctx.engine.cfg, x, flat, gJ, create_graph=torch.is_grad_enabled())
+            return None, None, (gx if need_x else None), (gp if need_p else None), None
         if not torch.is_grad_enabled():
             gx, gp = ctx.engine.second_order(ctx.ws, x, gJ, want_theta=need_p)
             return None, None, (gx if need_x else None), gp, None
@@ -159,7 +163,7 @@ class SirenVJP(torch.autograd.Function):
     def backward(ctx, ggx):
         x, flat, gy = ctx.saved_tensors
         eng = ctx.engine
-        w3_ok = eng.cfg.d_out == 1 and eng.cfg.outermost_linear and eng.grad_supported
+        w3_ok = eng.second_order_supported
         if torch.is_grad_enabled() or not w3_ok:
             gx, gp, ggy = _torch_path.vjp_vjp(eng.cfg, x, flat, gy, ggx, create_graph=torch.is_grad_enabled())
             return None, None, gx, gp, ggy

@@ -25,43 +25,47 @@ namespace siren {
 // kernel consumes them, so its ring loader walks the workspace linearly.
 // ------------------------------------------------------------------------------------------------------
 __global__ void pack_kernel(const float* __restrict__ p, float* __restrict__ ws, int d, int o, int lh,
-                            int64_t spad, int64_t total) {
-    const ParamOffsets off(d, o, lh);
+                            int64_t spad, int64_t total, int h) {
+    // h = hidden width (256: the H kernels, 512: wide_kernel.hpp); a slice is 16 K-rows x h out-neurons
+    const ParamOffsets off(d, o, lh, h);
+    const SmallLayout sl(h);
+    const int nb = h / 16;
+    const int64_t slice_floats = 16 * (int64_t)h;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
          idx += (int64_t)gridDim.x * blockDim.x) {
         float v = 0.f;
         if (idx < spad) {
             const int e = (int)idx;
-            if (e < SM_WO) {
-                const int k = e / H, n = e % H;
+            if (e < sl.wo) {
+                const int k = e / h, n = e % h;
                 v = k < d ? p[off.w0 + (int64_t)n * d + k] : 0.f;
-            } else if (e < SM_SEED) {
-                const int j = (e - SM_WO) / H, n = (e - SM_WO) % H;
-                v = j < o ? p[off.wout + (int64_t)j * H + n] : 0.f;
-            } else if (e < SM_BOUT) {
-                const int n = e - SM_SEED;
+            } else if (e < sl.seed) {
+                const int j = (e - sl.wo) / h, n = (e - sl.wo) % h;
+                v = j < o ? p[off.wout + (int64_t)j * h + n] : 0.f;
+            } else if (e < sl.bout) {
+                const int n = e - sl.seed;
                 float s = 0.f;
-                for (int j = 0; j < o; ++j) s += p[off.wout + (int64_t)j * H + n];
+                for (int j = 0; j < o; ++j) s += p[off.wout + (int64_t)j * h + n];
                 v = s;
-            } else if (e < SM_BIAS) {
-                const int j = e - SM_BOUT;
+            } else if (e < sl.bias) {
+                const int j = e - sl.bout;
                 v = j < o ? p[off.bout + j] : 0.f;
-            } else if (e < small_floats(lh)) {
-                const int l = (e - SM_BIAS) / H, n = (e - SM_BIAS) % H;
+            } else if (e < sl.floats(lh)) {
+                const int l = (e - sl.bias) / h, n = (e - sl.bias) % h;
                 v = p[off.b(l) + n];
             }
         } else {
             const int64_t e = idx - spad;
-            const int64_t slice = e / SLICE;
-            const int w = (int)(e % SLICE);
+            const int64_t slice = e / slice_floats;
+            const int w = (int)(e % slice_floats);
             const int r = w & 3, i = (w >> 2) & 15, g = (w >> 6) & 3, blk = w >> 8;
-            if (slice < (int64_t)lh * NB) {
-                const int l = (int)(slice / NB) + 1, kb = (int)(slice % NB);
-                v = p[off.w(l) + (int64_t)(16 * blk + i) * H + 16 * kb + 4 * g + r];
+            if (slice < (int64_t)lh * nb) {
+                const int l = (int)(slice / nb) + 1, kb = (int)(slice % nb);
+                v = p[off.w(l) + (int64_t)(16 * blk + i) * h + 16 * kb + 4 * g + r];
             } else {
-                const int64_t s2 = slice - (int64_t)lh * NB;
-                const int l = lh - (int)(s2 / NB), kb = (int)(s2 % NB);
-                v = p[off.w(l) + (int64_t)(16 * kb + 4 * g + r) * H + 16 * blk + i];
+                const int64_t s2 = slice - (int64_t)lh * nb;
+                const int l = lh - (int)(s2 / nb), kb = (int)(s2 % nb);
+                v = p[off.w(l) + (int64_t)(16 * kb + 4 * g + r) * h + 16 * blk + i];
             }
         }
         ws[idx] = v;

@@ -21,12 +21,14 @@ struct FusedArgs {
 };
 
 // tu_legacy.hip
-void launch_pack(const float* p, float* ws, int d, int o, int lh, int64_t spad, int64_t total, hipStream_t st);
+void launch_pack(const float* p, float* ws, int d, int o, int lh, int h, int64_t spad, int64_t total, hipStream_t st);
 void launch_legacy_fwd(dim3 grid, hipStream_t st, const FusedArgs& a);
 void launch_legacy_grad(bool store, dim3 grid, hipStream_t st, const FusedArgs& a);
 // tu_w1.hip: mode 0 = W1, 1 = STORE (W2 stage 1); tu_w0.hip: forward only
 void launch_w1(int mode, dim3 grid, hipStream_t st, const FusedArgs& a);
 void launch_w0(dim3 grid, hipStream_t st, const FusedArgs& a);
+// tu_wide.hip: hidden width 512 (mode as siren_common.h MODE_*); spill = cos scratch for MODE_W1 / MODE_STORE
+void launch_wide(int mode, dim3 grid, hipStream_t st, const FusedArgs& a, float* spill);
 // tu_w3.hip
 void launch_w3(bool theta, dim3 grid, hipStream_t st, const float* ws, const float* x, const float* v, int64_t n,
                float* gx, float* spill, float* A, float* At, float* D, float* Dt, int64_t n_pad, int d, int lh,
@@ -36,9 +38,9 @@ void launch_small_w3(dim3 grid, hipStream_t st, const float* At, const float* D,
                      int lh);
 // tu_train.hip
 void launch_wgrad(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, int64_t n_pad, int64_t tps,
-                  float* partial, int64_t P, int d, int o, int lh, int with_bias);
+                  float* partial, int64_t P, int d, int o, int lh, int with_bias, int h);
 void launch_small(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* gy,
-                  int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d, int o, int lh);
+                  int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d, int o, int lh, int h);
 void launch_reduce(dim3 grid, hipStream_t st, const float* partial, int64_t S, int64_t P, float* gp, int64_t S2,
                    int64_t lo, int64_t hi);
 

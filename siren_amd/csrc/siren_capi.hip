@@ -27,7 +27,8 @@ int check_cfg(const siren_cfg* cfg, bool fused) {
     if (!std::isfinite(cfg->omega_first) || !std::isfinite(cfg->omega_hidden))
         return fail(SIREN_EINVAL, "omega values must be finite");
     if (fused) {
-        if (cfg->hidden != siren::H) return fail(SIREN_EUNSUPPORTED, "fused kernels need hidden_features == 256");
+        if (cfg->hidden != siren::H && cfg->hidden != 512)
+            return fail(SIREN_EUNSUPPORTED, "fused kernels need hidden_features 256 or 512");
         if (cfg->d_in > siren::MAXD) return fail(SIREN_EUNSUPPORTED, "fused kernels need in_features <= 4");
         if (cfg->d_out > siren::MAXO) return fail(SIREN_EUNSUPPORTED, "fused kernels need out_features <= 4");
         if (cfg->n_hidden < 1 || cfg->n_hidden > siren::MAX_LH_FWD)
@@ -42,8 +43,13 @@ int hip_status(const char* what) {
     return SIREN_OK;
 }
 
+bool wide(const siren_cfg* cfg) { return cfg->hidden == 512; }
+
+// packed workspace: small block + forward slices + transposed slices (16 x hidden floats each)
+int64_t small_pad(const siren_cfg* cfg) { return siren::SmallLayout(cfg->hidden).pad(cfg->n_hidden); }
 int64_t ws_floats(const siren_cfg* cfg) {
-    return siren::small_pad(cfg->n_hidden) + 2ll * cfg->n_hidden * siren::NB * siren::SLICE;
+    const int64_t h = cfg->hidden;
+    return small_pad(cfg) + 2ll * cfg->n_hidden * (h / 16) * (16 * h);
 }
 
 int64_t param_count(const siren_cfg* cfg) {
@@ -51,10 +57,11 @@ int64_t param_count(const siren_cfg* cfg) {
     return H * cfg->d_in + H + (int64_t)cfg->n_hidden * (H * H + H) + (int64_t)cfg->d_out * H + cfg->d_out;
 }
 
-// W2 backward workspace: sin activations and deltas of every sine layer in 16-coordinate tiles, plus S
-// param-shaped partial slabs of the split-K weight-gradient reduction.
+// W2 backward workspace: sin activations and deltas of every sine layer in 16-coordinate tiles, S
+// param-shaped partial slabs of the split-K weight-gradient reduction and, for hidden 512, the cos scratch
+// of the wide kernel (layers 0..L-1).
 struct TrainPlan {
-    int64_t n_pad, tiles, splits, tps, act_floats, partial_floats, total;
+    int64_t n_pad, tiles, splits, tps, act_floats, partial_floats, spill_floats, total;
     TrainPlan(const siren_cfg* cfg, int64_t n) {
         n_pad = (n + siren::TILE - 1) / siren::TILE * siren::TILE;
         tiles = n_pad / 16;
@@ -64,9 +71,10 @@ struct TrainPlan {
         tps = (tiles + splits - 1) / splits;
         splits = (tiles + tps - 1) / tps;
         if (splits < 1) splits = 1;
-        act_floats = (int64_t)(cfg->n_hidden + 1) * n_pad * siren::H;
+        act_floats = (int64_t)(cfg->n_hidden + 1) * n_pad * cfg->hidden;
         partial_floats = splits * param_count(cfg);
-        total = 2 * act_floats + partial_floats;
+        spill_floats = wide(cfg) ? (int64_t)cfg->n_hidden * n_pad * cfg->hidden : 0;
+        total = 2 * act_floats + partial_floats + spill_floats;
     }
 };
 }  // namespace
@@ -94,8 +102,8 @@ int32_t siren_workspace_floats(const siren_cfg* cfg, int64_t* count) {
 int32_t siren_pack(const siren_cfg* cfg, const float* params, float* ws, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (params == nullptr || ws == nullptr) return fail(SIREN_EINVAL, "params/ws is NULL");
-    siren::launch_pack(params, ws, cfg->d_in, cfg->d_out, cfg->n_hidden, siren::small_pad(cfg->n_hidden),
-                       ws_floats(cfg), (hipStream_t)stream);
+    siren::launch_pack(params, ws, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden, small_pad(cfg), ws_floats(cfg),
+                       (hipStream_t)stream);
     return hip_status("siren_pack");
 }
 
@@ -109,7 +117,9 @@ int32_t siren_forward(const siren_cfg* cfg, const float* ws, const float* x, int
     const dim3 grid((unsigned)blocks);
     siren::FusedArgs fa{ws, x, n, nullptr, y, nullptr, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first,
                         cfg->omega_hidden, cfg->outermost_linear ? 0 : 1, nullptr, nullptr, 0};
-    if (cfg->outermost_linear && cfg->n_hidden <= 5 && (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0)
+    if (wide(cfg))
+        siren::launch_wide(siren::MODE_FWD, grid, (hipStream_t)stream, fa, nullptr);
+    else if (cfg->outermost_linear && cfg->n_hidden <= 5 && (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0)
         siren::launch_w0(grid, (hipStream_t)stream, fa);
     else
         siren::launch_legacy_fwd(grid, (hipStream_t)stream, fa);
@@ -119,8 +129,8 @@ int32_t siren_forward(const siren_cfg* cfg, const float* ws, const float* x, int
 int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* gy,
                            float* y, float* gx, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
-    if (cfg->n_hidden > siren::MAX_LH_GRAD)
-        return fail(SIREN_EUNSUPPORTED, "siren_forward_grad needs 1 <= num_hidden_layers <= 3");
+    if (cfg->n_hidden > siren::MAX_LH_GRAD && !wide(cfg))
+        return fail(SIREN_EUNSUPPORTED, "siren_forward_grad needs 1 <= num_hidden_layers <= 3 at hidden 256");
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
     if (n == 0) return SIREN_OK;
     if (ws == nullptr || x == nullptr || gx == nullptr) return fail(SIREN_EINVAL, "ws/x/gx is NULL");
@@ -130,7 +140,17 @@ int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x
     const int fs = cfg->outermost_linear ? 0 : 1;
     siren::FusedArgs fa{ws, x, n, gy, y, gx, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first,
                         cfg->omega_hidden, fs, nullptr, nullptr, 0};
-    if ((cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) != 0 || fs)
+    if (wide(cfg)) {
+        // cos scratch of layers 0..L-1 from the stream-ordered pool (this entry point has no workspace argument)
+        const int64_t n_pad = blocks * siren::TILE;
+        float* spill = nullptr;
+        const size_t bytes = (size_t)cfg->n_hidden * n_pad * cfg->hidden * sizeof(float);
+        if (hipMallocAsync((void**)&spill, bytes, (hipStream_t)stream) != hipSuccess)
+            return fail(SIREN_EHIP, "siren_forward_grad: hipMallocAsync of the hidden-512 cos scratch failed");
+        fa.n_pad = n_pad;  // per-layer scratch stride
+        siren::launch_wide(siren::MODE_W1, grid, (hipStream_t)stream, fa, spill);
+        (void)hipFreeAsync(spill, (hipStream_t)stream);
+    } else if ((cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) != 0 || fs)
         siren::launch_legacy_grad(false, grid, (hipStream_t)stream, fa);
     else
         siren::launch_w1(siren::MODE_W1, grid, (hipStream_t)stream, fa);
@@ -148,8 +168,8 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
                        float* tws, void* reserved, float* gx, float* gparams, void* stream) {
     (void)reserved;
     if (int rc = check_cfg(cfg, true)) return rc;
-    if (cfg->n_hidden > siren::MAX_LH_GRAD)
-        return fail(SIREN_EUNSUPPORTED, "siren_backward needs 1 <= num_hidden_layers <= 3");
+    if (cfg->n_hidden > siren::MAX_LH_GRAD && !wide(cfg))
+        return fail(SIREN_EUNSUPPORTED, "siren_backward needs 1 <= num_hidden_layers <= 3 at hidden 256");
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
     if (ws == nullptr || gy == nullptr || tws == nullptr || gx == nullptr || gparams == nullptr ||
         (n > 0 && x == nullptr))
@@ -164,20 +184,24 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
     float* abuf = tws;
     float* dbuf = tws + plan.act_floats;
     float* partial = tws + 2 * plan.act_floats;
+    float* spill = partial + plan.partial_floats;
     const dim3 grid((unsigned)(plan.n_pad / siren::TILE)), block(siren::THREADS);
     const int fs = cfg->outermost_linear ? 0 : 1;
     siren::FusedArgs fa{ws, x, n, gy, nullptr, gx, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first,
                         cfg->omega_hidden, fs, abuf, dbuf, plan.n_pad};
-    if ((cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0 && !fs)
+    if (wide(cfg))
+        siren::launch_wide(siren::MODE_STORE, grid, st, fa, spill);
+    else if ((cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0 && !fs)
         siren::launch_w1(siren::MODE_STORE, grid, st, fa);
     else
         siren::launch_legacy_grad(true, grid, st, fa);
     if (int rc = hip_status("siren_backward (fused store)")) return rc;
-    siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden), st, abuf, dbuf, plan.n_pad, plan.tps,
-                        partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1);
+    const unsigned quads = (unsigned)((cfg->hidden / 256) * (cfg->hidden / 256));
+    siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden, quads), st, abuf, dbuf, plan.n_pad,
+                        plan.tps, partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1, cfg->hidden);
     if (int rc = hip_status("siren_backward (wgrad)")) return rc;
     siren::launch_small(dim3((unsigned)plan.splits), st, abuf, dbuf, x, gy, n, plan.n_pad, plan.tps, partial, P,
-                        cfg->d_in, cfg->d_out, cfg->n_hidden);
+                        cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden);
     if (int rc = hip_status("siren_backward (small)")) return rc;
     const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 4096);
     siren::launch_reduce(dim3((unsigned)rblocks), st, partial, plan.splits, P, gparams, 0, 0, 0);
@@ -204,6 +228,7 @@ struct W3Plan {
 
 int32_t siren_second_order_ws_floats(const siren_cfg* cfg, int64_t n, int32_t want_theta, int64_t* count) {
     if (int rc = check_cfg(cfg, true)) return rc;
+    if (wide(cfg)) return fail(SIREN_EUNSUPPORTED, "siren_second_order covers hidden_features == 256");
     if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
     *count = W3Plan(cfg, n, want_theta != 0).total;
     return SIREN_OK;
@@ -214,8 +239,9 @@ int32_t siren_second_order(const siren_cfg* cfg, const float* ws, const float* x
     if (int rc = check_cfg(cfg, true)) return rc;
     if (cfg->n_hidden > siren::MAX_LH_GRAD)
         return fail(SIREN_EUNSUPPORTED, "siren_second_order needs 1 <= num_hidden_layers <= 3");
-    if (cfg->d_out != 1 || !cfg->outermost_linear)
-        return fail(SIREN_EUNSUPPORTED, "siren_second_order covers d_out == 1 with a linear output layer");
+    if (cfg->d_out != 1 || !cfg->outermost_linear || wide(cfg))
+        return fail(SIREN_EUNSUPPORTED,
+                    "siren_second_order covers hidden 256, d_out == 1 with a linear output layer");
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
     if (ws == nullptr || tws == nullptr || gx == nullptr || (n > 0 && (x == nullptr || v == nullptr)))
         return fail(SIREN_EINVAL, "ws/x/v/tws/gx is NULL");
@@ -239,9 +265,10 @@ int32_t siren_second_order(const siren_cfg* cfg, const float* ws, const float* x
     if (int rc = hip_status("siren_second_order (w3)")) return rc;
     if (!theta) return SIREN_OK;
     const dim3 wgrid((unsigned)plan.splits, (unsigned)cfg->n_hidden);
-    siren::launch_wgrad(wgrid, st, A, D, plan.n_pad, plan.tps, partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1);
+    siren::launch_wgrad(wgrid, st, A, D, plan.n_pad, plan.tps, partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1,
+                        siren::H);
     siren::launch_wgrad(wgrid, st, At, Dt, plan.n_pad, plan.tps, partial + plan.splits * P, P, cfg->d_in, cfg->d_out,
-                        cfg->n_hidden, 0);
+                        cfg->n_hidden, 0, siren::H);
     if (int rc = hip_status("siren_second_order (wgrad)")) return rc;
     siren::launch_small_w3(dim3((unsigned)plan.splits), st, At, D, Dt, x, v, n, plan.n_pad, plan.tps, partial, P,
                            cfg->d_in, cfg->d_out, cfg->n_hidden);

@@ -49,6 +49,15 @@ constexpr int SMALL_MAX = SM_BIAS + (MAX_LH_FWD + 1) * H;
 __host__ __device__ inline int small_floats(int lh) { return SM_BIAS + (lh + 1) * H; }
 __host__ __device__ inline int64_t small_pad(int lh) { return ((int64_t)small_floats(lh) + 1023) / 1024 * 1024; }
 
+// The same block for a hidden width hw (the H = 512 kernels of wide_kernel.hpp): offsets scale with hw.
+struct SmallLayout {
+    int w0, wo, seed, bout, bias, h;
+    __host__ __device__ explicit SmallLayout(int hw) : w0(0), wo(4 * hw), seed(8 * hw), bout(9 * hw),
+                                                       bias(9 * hw + 4), h(hw) {}
+    __host__ __device__ int floats(int lh) const { return bias + (lh + 1) * h; }
+    __host__ __device__ int64_t pad(int lh) const { return ((int64_t)floats(lh) + 1023) / 1024 * 1024; }
+};
+
 // sin/cos of a fp32 phase t = w*z, to ~1 ulp of the true values (what torch.sin/torch.cos return on the
 // reference's CPU path). Cody-Waite reduction by pi/2 with a 3-part constant (exact products for
 // |quadrant| < 2^16), then minimax polynomials on [-pi/4, pi/4]. Phases beyond 1e5 rad (never produced

@@ -8,17 +8,18 @@ namespace siren {
 // Parameter offsets inside the flat buffer (nn.Linear / state_dict order, see include/siren_amd.h).
 // ------------------------------------------------------------------------------------------------------
 struct ParamOffsets {
-    int64_t w0, b0, hidden0, wout, bout, total;
-    __host__ __device__ ParamOffsets(int d, int o, int lh) {
+    int64_t w0, b0, hidden0, wout, bout, total, h;
+    __host__ __device__ ParamOffsets(int d, int o, int lh, int hw = H) {
+        h = hw;
         w0 = 0;
-        b0 = (int64_t)H * d;
-        hidden0 = b0 + H;
-        wout = hidden0 + (int64_t)lh * (H * H + H);
-        bout = wout + (int64_t)o * H;
+        b0 = h * d;
+        hidden0 = b0 + h;
+        wout = hidden0 + (int64_t)lh * (h * h + h);
+        bout = wout + (int64_t)o * h;
         total = bout + o;
     }
-    __host__ __device__ int64_t w(int l) const { return hidden0 + (int64_t)(l - 1) * (H * H + H); }
-    __host__ __device__ int64_t b(int l) const { return l == 0 ? b0 : w(l) + (int64_t)H * H; }
+    __host__ __device__ int64_t w(int l) const { return hidden0 + (int64_t)(l - 1) * (h * h + h); }
+    __host__ __device__ int64_t b(int l) const { return l == 0 ? b0 : w(l) + h * h; }
 };
 
 

@@ -13,41 +13,45 @@
 
 namespace siren {
 
-constexpr int WG_TILE_FLOATS = H * 16;          // one 16-coordinate tile of one layer (16 KiB)
-constexpr int WG_SLOT = 2 * WG_TILE_FLOATS;     // delta tile + activation tile
+constexpr int WG_TILE_FLOATS = H * 16;          // 256 neurons of one 16-coordinate tile (16 KiB)
+constexpr int WG_SLOT = 2 * WG_TILE_FLOATS;     // delta (half-)tile + activation (half-)tile
 constexpr int WG_NBUF = 3;
 
 __device__ __forceinline__ void wg_issue(const float* __restrict__ dsrc, const float* __restrict__ asrc, float* ring,
-                                         int64_t t, int64_t t1, int k, int wave, int lane) {
+                                         int64_t t, int64_t t1, int k, int wave, int lane, int64_t tstride) {
     if (t < t1) {
         float* slot = ring + (k % WG_NBUF) * WG_SLOT;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const int chunk = wave * 8 + q;  // 32 chunks of 1 KiB: 0..15 delta tile, 16..31 activation tile
-            const float* src = (chunk < 16 ? dsrc + t * WG_TILE_FLOATS + chunk * 256
-                                           : asrc + t * WG_TILE_FLOATS + (chunk - 16) * 256) + lane * 4;
+            const float* src = (chunk < 16 ? dsrc + t * tstride + chunk * 256
+                                           : asrc + t * tstride + (chunk - 16) * 256) + lane * 4;
             __builtin_amdgcn_global_load_lds((const void*)src,
                                              (__attribute__((address_space(3))) void*)(slot + chunk * 256), 16, 0, 0);
         }
     }
 }
 
-// grid (S, LH): block (s, l-1) reduces coordinate tiles [s*tps, min(T, (s+1)*tps)) of layer l.
-// Wave w owns the 128x128 quadrant (rows 128*(w>>1), cols 128*(w&1)) of the 256x256 dW_l.
+// grid (S, LH, (h/256)^2): block (s, l-1, q) reduces coordinate tiles [s*tps, min(T, (s+1)*tps)) of layer l
+// into the 256x256 block q = (qr, qc) of dW_l (the whole dW_l for h = 256; a quadrant for h = 512, staging
+// only the 256-neuron halves of the delta and activation tiles it needs).
+// Wave w owns the 128x128 sub-block (rows 128*(w>>1), cols 128*(w&1)).
 __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restrict__ abuf,
                                                           const float* __restrict__ dbuf, int64_t n_pad,
                                                           int64_t tps, float* __restrict__ partial, int64_t P,
-                                                          int d, int o, int lh, int with_bias = 1) {
+                                                          int d, int o, int lh, int with_bias, int h) {
     __shared__ __attribute__((aligned(16))) float ring[WG_NBUF * WG_SLOT];
-    const ParamOffsets off(d, o, lh);
+    const ParamOffsets off(d, o, lh, h);
     const int s = blockIdx.x, l = blockIdx.y + 1;
+    const int qn = h / 256, qr = blockIdx.z / qn, qc = blockIdx.z % qn;
+    const int64_t tstride = (int64_t)h * 16;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane >> 4, i = lane & 15;
     const int wr = wave >> 1, wc = wave & 1;
     const int64_t T = n_pad / 16;
     const int64_t t0 = (int64_t)s * tps, t1 = t0 + tps < T ? t0 + tps : T;
-    const float* dsrc = dbuf + (int64_t)l * n_pad * H;
-    const float* asrc = abuf + (int64_t)(l - 1) * n_pad * H;
+    const float* dsrc = dbuf + (int64_t)l * n_pad * h + qr * WG_TILE_FLOATS;
+    const float* asrc = abuf + (int64_t)(l - 1) * n_pad * h + qc * WG_TILE_FLOATS;
 
     f32x4 acc[8][8];
 #pragma unroll
@@ -56,8 +60,8 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
         for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
     float bsum = 0.f;
 
-    wg_issue(dsrc, asrc, ring, t0, t1, 0, wave, lane);
-    wg_issue(dsrc, asrc, ring, t0 + 1, t1, 1, wave, lane);
+    wg_issue(dsrc, asrc, ring, t0, t1, 0, wave, lane, tstride);
+    wg_issue(dsrc, asrc, ring, t0 + 1, t1, 1, wave, lane, tstride);
     int k = 0;
     for (int64_t t = t0; t < t1; ++t, ++k) {
         if (t + 1 < t1)
@@ -65,7 +69,7 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        wg_issue(dsrc, asrc, ring, t + 2, t1, k + 2, wave, lane);
+        wg_issue(dsrc, asrc, ring, t + 2, t1, k + 2, wave, lane, tstride);
         const float* sd = ring + (k % WG_NBUF) * WG_SLOT;
         const float* sa = sd + WG_TILE_FLOATS;
         // bias gradient: thread t owns neuron t
@@ -95,55 +99,60 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
         for (int cb = 0; cb < 8; ++cb)
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                dW[(int64_t)(128 * wr + 16 * rb + 4 * g + q) * H + 128 * wc + 16 * cb + i] = acc[rb][cb][q];
-    out[off.b(l) + threadIdx.x] = with_bias ? bsum : 0.f;
+                dW[(int64_t)(256 * qr + 128 * wr + 16 * rb + 4 * g + q) * h + 256 * qc + 128 * wc + 16 * cb + i] =
+                    acc[rb][cb][q];
+    if (qc == 0) out[off.b(l) + 256 * qr + threadIdx.x] = with_bias ? bsum : 0.f;
 }
 
 // grid (S): first-layer weight/bias grads from (delta_0, x) and output-layer grads from (gy, a_LH).
+// Thread t owns neurons t, t + 256, ... (< h).
 __global__ __launch_bounds__(THREADS) void small_kernel(const float* __restrict__ abuf, const float* __restrict__ dbuf,
                                                         const float* __restrict__ x, const float* __restrict__ gy,
                                                         int64_t n, int64_t n_pad, int64_t tps,
                                                         float* __restrict__ partial, int64_t P, int d, int o,
-                                                        int lh) {
-    const ParamOffsets off(d, o, lh);
-    const int s = blockIdx.x, t = threadIdx.x;  // thread t owns neuron t
+                                                        int lh, int h) {
+    const ParamOffsets off(d, o, lh, h);
+    const int s = blockIdx.x;
     const int64_t T = n_pad / 16;
     const int64_t t0 = (int64_t)s * tps, t1 = t0 + tps < T ? t0 + tps : T;
+    const int64_t tstride = (int64_t)h * 16;
     const float* d0 = dbuf;                               // delta_0
-    const float* aL = abuf + (int64_t)lh * n_pad * H;     // a_LH
-    float gw0[MAXD] = {0.f, 0.f, 0.f, 0.f}, gb0 = 0.f;
-    float gwo[MAXO] = {0.f, 0.f, 0.f, 0.f}, gbo = 0.f;
-    for (int64_t tile = t0; tile < t1; ++tile) {
-        const f32x4* drow = (const f32x4*)(d0 + tile * WG_TILE_FLOATS + t * 16);
-        const f32x4* arow = (const f32x4*)(aL + tile * WG_TILE_FLOATS + t * 16);
+    const float* aL = abuf + (int64_t)lh * n_pad * h;     // a_LH
+    float* out = partial + (int64_t)s * P;
+    for (int t = threadIdx.x; t < h; t += THREADS) {
+        float gw0[MAXD] = {0.f, 0.f, 0.f, 0.f}, gb0 = 0.f;
+        float gwo[MAXO] = {0.f, 0.f, 0.f, 0.f}, gbo = 0.f;
+        for (int64_t tile = t0; tile < t1; ++tile) {
+            const f32x4* drow = (const f32x4*)(d0 + tile * tstride + t * 16);
+            const f32x4* arow = (const f32x4*)(aL + tile * tstride + t * 16);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const f32x4 dv = drow[q], av = arow[q];
+            for (int q = 0; q < 4; ++q) {
+                const f32x4 dv = drow[q], av = arow[q];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t c = tile * 16 + 4 * q + r;
-                if (c < n) {
-                    gb0 += dv[r];
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t c = tile * 16 + 4 * q + r;
+                    if (c < n) {
+                        gb0 += dv[r];
 #pragma unroll
-                    for (int k = 0; k < MAXD; ++k)
-                        if (k < d) gw0[k] += dv[r] * x[c * d + k];
+                        for (int k = 0; k < MAXD; ++k)
+                            if (k < d) gw0[k] += dv[r] * x[c * d + k];
 #pragma unroll
-                    for (int j = 0; j < MAXO; ++j)
-                        if (j < o) gwo[j] += gy[c * o + j] * av[r];
-                    if (t < o) gbo += gy[c * o + t];
+                        for (int j = 0; j < MAXO; ++j)
+                            if (j < o) gwo[j] += gy[c * o + j] * av[r];
+                        if (t < o) gbo += gy[c * o + t];
+                    }
                 }
             }
         }
+#pragma unroll
+        for (int k = 0; k < MAXD; ++k)
+            if (k < d) out[off.w0 + (int64_t)t * d + k] = gw0[k];
+        out[off.b0 + t] = gb0;
+#pragma unroll
+        for (int j = 0; j < MAXO; ++j)
+            if (j < o) out[off.wout + (int64_t)j * h + t] = gwo[j];
+        if (t < o) out[off.bout + t] = gbo;
     }
-    float* out = partial + (int64_t)s * P;
-#pragma unroll
-    for (int k = 0; k < MAXD; ++k)
-        if (k < d) out[off.w0 + (int64_t)t * d + k] = gw0[k];
-    out[off.b0 + t] = gb0;
-#pragma unroll
-    for (int j = 0; j < MAXO; ++j)
-        if (j < o) out[off.wout + (int64_t)j * H + t] = gwo[j];
-    if (t < o) out[off.bout + t] = gbo;
 }
 
 // gp[i] = sum over the partial slabs; indices in [lo, hi) (the hidden layers' W/b) sum S + S2 slabs, the others

@@ -5,15 +5,16 @@
 namespace siren {
 
 void launch_wgrad(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, int64_t n_pad, int64_t tps,
-                  float* partial, int64_t P, int d, int o, int lh, int with_bias) {
+                  float* partial, int64_t P, int d, int o, int lh, int with_bias, int h) {
     hipLaunchKernelGGL(wgrad_kernel, grid, dim3(THREADS), 0, st, abuf, dbuf, n_pad, tps, partial, P, d, o, lh,
-                       with_bias);
+                       with_bias, h);
 }
 
 void launch_small(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* gy,
-                  int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d, int o, int lh) {
+                  int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d, int o, int lh,
+                  int h) {
     hipLaunchKernelGGL(small_kernel, grid, dim3(THREADS), 0, st, abuf, dbuf, x, gy, n, n_pad, tps, partial, P, d, o,
-                       lh);
+                       lh, h);
 }
 
 void launch_reduce(dim3 grid, hipStream_t st, const float* partial, int64_t S, int64_t P, float* gp, int64_t S2,

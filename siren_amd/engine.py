@@ -40,7 +40,11 @@ class SirenEngine:
         self.supported = rc == _lib.SIREN_OK
         self.unsupported_reason = None if self.supported else self.lib.siren_last_error().decode()
         self.ws_floats = cnt.value if self.supported else 0
-        self.grad_supported = self.supported and 1 <= n_hidden <= 3
+        # hidden 256 keeps cos(w z_l) of every layer in registers (1..3 hidden layers); hidden 512 spills it
+        self.grad_supported = self.supported and (1 <= n_hidden <= 3 or int(hidden) == 512)
+        # the W3 second-order kernel: hidden 256, scalar output, linear output layer
+        self.second_order_supported = (self.supported and int(hidden) == 256 and 1 <= n_hidden <= 3
+                                       and int(d_out) == 1 and bool(outermost_linear))
 
     # ------------------------------------------------------------------------------------------------------
     def _require(self):
@@ -95,7 +99,7 @@ class SirenEngine:
         diff_operators.gradient returns, diff_operators.py:39-43)."""
         self._require()
         if not self.grad_supported:
-            raise _lib.SirenUnsupported('siren_forward_grad needs 1 <= num_hidden_layers <= 3')
+            raise _lib.SirenUnsupported('siren_forward_grad needs 1 <= num_hidden_layers <= 3 at hidden 256')
         x = self._check_x(x)
         n = x.shape[0]
         if gy is not None:
@@ -119,7 +123,7 @@ class SirenEngine:
         """
         self._require()
         if not self.grad_supported:
-            raise _lib.SirenUnsupported('siren_backward needs 1 <= num_hidden_layers <= 3')
+            raise _lib.SirenUnsupported('siren_backward needs 1 <= num_hidden_layers <= 3 at hidden 256')
         x = self._check_x(x)
         n = x.shape[0]
         gy = gy.contiguous()
@@ -138,8 +142,9 @@ class SirenEngine:
         """W3: (H v, d/dtheta sum <v, dPhi/dx>) for d_out == 1 — the backward of the dPhi/dx graph node
         (gradients_mse / sdf / divergence). Returns (gx, gparams or None)."""
         self._require()
-        if not self.grad_supported or self.cfg.d_out != 1 or not self.cfg.outermost_linear:
-            raise _lib.SirenUnsupported('siren_second_order covers d_out == 1, linear output, 1..3 hidden layers')
+        if not self.second_order_supported:
+            raise _lib.SirenUnsupported('siren_second_order covers hidden 256, d_out == 1, linear output, '
+                                        '1..3 hidden layers')
         x = self._check_x(x)
         n = x.shape[0]
         v = v.contiguous()

@@ -13,8 +13,8 @@ State-dict keys (net.net.{i}.0.weight|bias for SingleBVPNet, net.{i}.linear.* fo
 consumption order of initialisation are the reference's, so torch.manual_seed(s) gives identical weights and
 checkpoints load either way.
 
-The fused path covers type='sine', mode='mlp', hidden_features=256, in/out_features <= 4, 1..8 hidden layers
-(first-order derivatives: 1..3), unbatched fp32 weights on a ROCm device. A sine network outside that raises
+The fused path covers type='sine', mode='mlp', hidden_features 256 or 512, in/out_features <= 4, 1..8 hidden
+layers (first-order derivatives at hidden 256: 1..3), unbatched fp32 weights on a ROCm device. A sine network outside that raises
 SirenUnsupported; there is no silent torch or CPU fallback. Non-sine baselines (relu, tanh, ...) keep the
 reference's plain torch layers: they are not the SIREN hot path.
 """

@@ -1,0 +1,139 @@
+"""Parity of the hidden-512 kernels (wide_kernel.hpp + the h = 512 wgrad/small kernels) against the reference's
+G4 golden vectors (SingleBVPNet(in 3, out 3, hidden 512, 3 hidden layers), BASELINE config 4) and the fp64
+oracle. Needs an MI355X. Tolerances as test_gpu_parity.py (1e-4 abs / relative to max|ref|).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import siren_oracle as O
+from conftest import weights_of
+
+pytestmark = pytest.mark.gpu
+
+H = 512
+
+
+def tol_rel(ref, rel=1e-4):
+    return rel * max(1., float(np.max(np.abs(ref))))
+
+
+def wide_engine(d=3, L=3, o=3, w0=30., w=30., lin=True):
+    from siren_amd.engine import SirenEngine
+    return SirenEngine(d, H, L, o, w0, w, lin)
+
+
+def random_layers(d, L, o, seed=0, w=30.):
+    rng = np.random.default_rng(seed)
+    dims = [d] + [H] * (L + 1) + [o]
+    layers = []
+    for i, (fi, fo) in enumerate(zip(dims[:-1], dims[1:])):
+        bound = 1. / fi if i == 0 else np.sqrt(6. / fi) / w
+        layers.append((rng.uniform(-bound, bound, (fo, fi)).astype(np.float32),
+                       (rng.uniform(-1, 1, fo) / np.sqrt(fi)).astype(np.float32)))
+    return layers
+
+
+def to_dev(a, dev):
+    return torch.tensor(np.asarray(a, np.float32), device=dev)
+
+
+def test_g4_forward_gradient_vs_reference_golden(cuda, g4):
+    flat, _ = weights_of(g4)
+    eng = wide_engine()
+    ws = eng.pack(to_dev(flat, cuda))
+    x = to_dev(g4['coords'][0], cuda)
+    y0 = eng.forward(ws, x).cpu().numpy()
+    y1, gx = eng.forward_grad(ws, x)
+    ry, rg = g4['G4_model_out_f64'][0], g4['G4_gradient_f64'][0]
+    assert np.max(np.abs(y0 - ry)) <= 1e-4
+    assert np.max(np.abs(y1.cpu().numpy() - ry)) <= 1e-4
+    assert np.max(np.abs(gx.cpu().numpy() - rg)) <= tol_rel(rg)
+
+
+def test_g4_image_mse_theta_grads_vs_reference_golden(cuda, g4):
+    flat, layers = weights_of(g4)
+    eng = wide_engine()
+    ws = eng.pack(to_dev(flat, cuda))
+    x = to_dev(g4['coords'][0], cuda)
+    y = eng.forward(ws, x)
+    gt = to_dev(g4['gt_img'][0], cuda)
+    gy = 2. * (y - gt) / y.numel()
+    gx, gp = eng.backward_params(ws, x, gy)
+    keys = ['net.net.%d.0.%s' % (i, k) for i in range(5) for k in ('weight', 'bias')]
+    ref = np.concatenate([g4['G4_image_mse_grad_' + k].reshape(-1) for k in keys])
+    assert np.max(np.abs(gp.cpu().numpy() - ref)) <= 1e-4 * np.max(np.abs(ref))
+    _, rgx = O.forward_grad(g4['coords'][0], layers, gy.cpu().numpy())
+    assert np.max(np.abs(gx.cpu().numpy() - rgx)) <= 1e-4 * np.max(np.abs(rgx))
+
+
+@pytest.mark.parametrize('n,d,L,o', [(1, 2, 1, 1), (100, 3, 2, 3), (5000, 2, 3, 1), (3000, 1, 5, 2)])
+def test_wide_shapes_vs_oracle(cuda, n, d, L, o):
+    layers = random_layers(d, L, o, seed=n + L)
+    eng = wide_engine(d, L, o)
+    ws = eng.pack(to_dev(O.flatten(layers), cuda))
+    rng = np.random.default_rng(n)
+    x = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    gy = rng.normal(size=(n, o)).astype(np.float32)
+    xd, gyd = to_dev(x, cuda), to_dev(gy, cuda)
+    y = eng.forward(ws, xd)
+    y1, gx = eng.forward_grad(ws, xd, gyd)
+    ry, rg = O.forward_grad(x, layers, gy)
+    assert np.max(np.abs(y.cpu().numpy() - ry)) <= 1e-4
+    assert np.max(np.abs(y1.cpu().numpy() - ry)) <= 1e-4
+    assert np.max(np.abs(gx.cpu().numpy() - rg)) <= tol_rel(rg)
+    gyn = gy / n
+    gx2, gp = eng.backward_params(ws, xd, to_dev(gyn, cuda))
+    xt = torch.tensor(x, dtype=torch.float64)
+    params = [torch.tensor(np.asarray(t), dtype=torch.float64, requires_grad=True) for W, b in layers for t in (W, b)]
+    yt = O.torch_forward(xt, params)
+    ref = torch.cat([g.reshape(-1) for g in torch.autograd.grad(yt, params, torch.tensor(gyn, dtype=torch.float64))])
+    ref = ref.numpy()
+    assert np.max(np.abs(gp.cpu().numpy() - ref)) <= 1e-4 * np.max(np.abs(ref))
+    assert np.max(np.abs(gx2.cpu().numpy() - rg / n)) <= tol_rel(rg / n)
+
+
+def test_wide_final_sine_vs_oracle(cuda):
+    """notebook Siren(outermost_linear=False) at hidden 512: sin on the output layer too."""
+    layers = random_layers(2, 2, 1, seed=7)
+    eng = wide_engine(2, 2, 1, lin=False)
+    ws = eng.pack(to_dev(O.flatten(layers), cuda))
+    x = np.random.default_rng(7).uniform(-1, 1, (777, 2)).astype(np.float32)
+    y, gx = eng.forward_grad(ws, to_dev(x, cuda))
+    ry, rg = O.forward_grad(x, layers, None, outermost_linear=False)
+    assert np.max(np.abs(y.cpu().numpy() - ry)) <= 1e-4
+    assert np.max(np.abs(gx.cpu().numpy() - rg)) <= tol_rel(rg)
+
+
+def test_wide_deterministic_and_linear(cuda):
+    layers = random_layers(3, 3, 3, seed=5)
+    eng = wide_engine()
+    ws = eng.pack(to_dev(O.flatten(layers), cuda))
+    n = 1 << 17
+    x = torch.rand(n, 3, device=cuda) * 2 - 1
+    gy = torch.randn(n, 3, device=cuda)
+    a = eng.backward_params(ws, x, gy)
+    b = eng.backward_params(ws, x, gy)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    _, g1 = eng.forward_grad(ws, x, gy, want_y=False)
+    _, g2 = eng.forward_grad(ws, x, 2. * gy, want_y=False)
+    assert torch.allclose(g2, 2. * g1, rtol=0, atol=1e-6 * float(g1.abs().max()))
+    # subset against the oracle
+    idx = torch.randperm(n, generator=torch.Generator().manual_seed(0))[:512]
+    _, rg = O.forward_grad(x[idx].cpu().numpy(), layers, gy[idx].cpu().numpy())
+    assert np.max(np.abs(g1[idx].cpu().numpy() - rg)) <= tol_rel(rg)
+
+
+def test_module_image_fit_step_wide(cuda, g4):
+    """Drop-in: SingleBVPNet(hidden_features=512) + loss_functions.image_mse + backward == reference golden."""
+    from siren_amd.modules import SingleBVPNet
+    from siren_amd import loss_functions as LF
+    torch.manual_seed(0)
+    m = SingleBVPNet(out_features=3, in_features=3, hidden_features=512, num_hidden_layers=3, verbose=False).to(cuda)
+    out = m({'coords': to_dev(g4['coords'], cuda)})
+    loss = LF.image_mse(None, out, {'img': to_dev(g4['gt_img'], cuda)})['img_loss']
+    assert abs(float(loss) - 0.3987086920864164) <= 1e-5
+    loss.backward()
+    for name, p in m.named_parameters():
+        ref = g4['G4_image_mse_grad_' + name]
+        assert np.max(np.abs(p.grad.cpu().numpy() - ref)) <= 1e-4 * max(1e-6, np.max(np.abs(ref))) + 1e-9, name

@@ -55,6 +55,9 @@ def test_param_count_and_workspace(lib):
     assert lib.siren_param_count(None, ctypes.byref(c)) == _lib.SIREN_EINVAL
     wide = _lib.SirenCfg(3, 512, 3, 3, 30., 30., 1, 0)
     assert lib.siren_param_count(ctypes.byref(wide), ctypes.byref(c)) == 0 and c.value == 791555
+    assert lib.siren_workspace_floats(ctypes.byref(wide), ctypes.byref(c)) == 0
+    assert c.value == 7168 + 2 * 3 * 32 * 8192          # small block padded to 1 KiB + 32 KiB slices
+    assert lib.siren_second_order_ws_floats(ctypes.byref(wide), 10, 1, ctypes.byref(c)) == _lib.SIREN_EUNSUPPORTED
 
 
 def test_zero_coords_is_a_noop(lib):

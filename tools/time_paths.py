@@ -1,0 +1,53 @@
+"""Times the engine entry points (HIP events on the launch stream) for one architecture:
+python tools/time_paths.py [--hidden 512] [--layers 3] [--d 3] [--o 3] [--n 262144]"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timed(fn, reps=5):
+    st = torch.cuda.current_stream()
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(st)
+    for _ in range(reps):
+        fn()
+    b.record(st)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--hidden', type=int, default=512)
+    ap.add_argument('--layers', type=int, default=3)
+    ap.add_argument('--d', type=int, default=3)
+    ap.add_argument('--o', type=int, default=3)
+    ap.add_argument('--n', type=int, default=1 << 18)
+    a = ap.parse_args()
+    from siren_amd.engine import SirenEngine
+    from siren_amd.modules import FCBlock
+    torch.manual_seed(0)
+    net = FCBlock(a.d, a.o, a.layers, a.hidden, outermost_linear=True, nonlinearity='sine')
+    flat = torch.cat([p.detach().reshape(-1) for p in net.parameters()]).cuda()
+    eng = SirenEngine(a.d, a.hidden, a.layers, a.o)
+    ws = eng.pack(flat)
+    x = torch.rand(a.n, a.d, device='cuda') * 2 - 1
+    gy = torch.randn(a.n, a.o, device='cuda')
+    H, L, d, o = a.hidden, a.layers, a.d, a.o
+    F = 2 * (d * H + L * H * H + H * o)
+    for name, fn, work in (('W0 forward', lambda: eng.forward(ws, x), F),
+                           ('W1 forward+vjp_x', lambda: eng.forward_grad(ws, x, gy), 2 * F),
+                           ('W2 backward (store+wgrad+small+reduce)', lambda: eng.backward_params(ws, x, gy), 3 * F)):
+        ms = timed(fn)
+        print('%-42s %8.3f ms  %8.2f Mcoords/s  %6.1f TFLOP/s (%.1f%% of 157.3)'
+              % (name, ms, a.n / ms / 1e3, work * a.n / ms / 1e9, work * a.n / ms / 1e9 / 157.3 * 100), flush=True)
+
+
+if __name__ == '__main__':
+    main()
