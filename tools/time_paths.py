@@ -44,9 +44,17 @@ def main():
     for name, fn, work in (('W0 forward', lambda: eng.forward(ws, x), F),
                            ('W1 forward+vjp_x', lambda: eng.forward_grad(ws, x, gy), 2 * F),
                            ('W2 backward (store+wgrad+small+reduce)', lambda: eng.backward_params(ws, x, gy), 3 * F)):
-        ms = timed(fn)
-        print('%-42s %8.3f ms  %8.2f Mcoords/s  %6.1f TFLOP/s (%.1f%% of 157.3)'
-              % (name, ms, a.n / ms / 1e3, work * a.n / ms / 1e9, work * a.n / ms / 1e9 / 157.3 * 100), flush=True)
+        report(name, timed(fn), work, a.n)
+    if eng.second_order_supported:
+        v = torch.randn(a.n, a.d, device='cuda')
+        for name, fn, work in (('W3 H v (x only)', lambda: eng.second_order(ws, x, v, want_theta=False), 4 * F),
+                               ('W3 H v + theta-grad', lambda: eng.second_order(ws, x, v, want_theta=True), 6 * F)):
+            report(name, timed(fn), work, a.n)
+
+
+def report(name, ms, work, n):
+    print('%-42s %8.3f ms  %8.2f Mcoords/s  %6.1f TFLOP/s (%.1f%% of 157.3)'
+          % (name, ms, n / ms / 1e3, work * n / ms / 1e9, work * n / ms / 1e9 / 157.3 * 100), flush=True)
 
 
 if __name__ == '__main__':
