@@ -92,6 +92,15 @@ int32_t siren_forward(const siren_cfg* cfg, const float* ws, const float* x, int
 int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x, int64_t n,
                            const float* gy, float* y, float* gx, void* stream);
 
+/* W4 (the fused Laplacian) in ONE launch, forward-mode Taylor jet:
+ *   y   (n, d_out)  = Phi(x)                       (skipped when y == NULL)
+ *   gx  (n, d_in)   = sum_j dPhi_j/dx              (diff_operators.gradient; skipped when gx == NULL)
+ *   lap (n)         = sum_j sum_i d2Phi_j/dx_i2    (diff_operators.laplace, diff_operators.py:27-36)
+ * hidden 256, d_in <= 2, linear output layer, n_hidden 1..5. Replaces the d + 1 autograd sweeps that
+ * laplace() records (gradient, then one create_graph grad per input dimension). */
+int32_t siren_forward_laplace(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y,
+                              float* gx, float* lap, void* stream);
+
 /* fp32 values of backward workspace siren_backward() needs for n coordinates (sin activations and deltas of
  * every sine layer, plus the split-K partial gradient slabs). */
 int32_t siren_train_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count);
@@ -104,6 +113,20 @@ int32_t siren_train_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count);
  * Replaces autograd's MmBackward/SinBackward/MulBackward chain of train_loss.backward() (training.py:95-96). */
 int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* gy,
                        float* tws, void* reserved, float* gx, float* gparams, void* stream);
+
+/* fp32 values of workspace siren_laplace_backward() needs for n coordinates (a-, z- and cotangent jets of every
+ * sine layer as 16-column tiles, plus the split-K partial slabs). */
+int32_t siren_laplace_backward_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count);
+
+/* W4s, the backward of the fused Laplacian (laplace_mse training, loss_functions.py:104-109): with glap (n) the
+ * cotangent of lap = siren_forward_laplace's output,
+ *   gx (n, d_in)          = d/dx sum_c glap_c lap(x_c)
+ *   gparams (param_count) = d/dtheta sum_c glap_c lap(x_c)
+ * The reverse of the forward-mode jet (same 4 coordinates x 4 streams MFMA columns), then the split-K MFMA
+ * weight-gradient kernel over K = 4n columns and a deterministic slab reduction. Same coverage as
+ * siren_forward_laplace. Replaces autograd's third-order sweep through laplace()'s graph (training.py:95-96). */
+int32_t siren_laplace_backward(const siren_cfg* cfg, const float* ws, const float* x, int64_t n,
+                               const float* glap, float* tws, float* gx, float* gparams, void* stream);
 
 /* fp32 values of workspace siren_second_order() needs (per-layer spill, and with want_theta the tangent /
  * primal activations and adjoints of every layer plus 2*S partial slabs). */

@@ -39,8 +39,11 @@ _SIGS = {
     'siren_pack': [_CFG, _P, _P, _P],
     'siren_forward': [_CFG, _P, _P, _I64, _P, _P],
     'siren_forward_grad': [_CFG, _P, _P, _I64, _P, _P, _P, _P],
+    'siren_forward_laplace': [_CFG, _P, _P, _I64, _P, _P, _P, _P],
     'siren_train_ws_floats': [_CFG, _I64, ctypes.POINTER(_I64)],
     'siren_backward': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P, _P],
+    'siren_laplace_backward_ws_floats': [_CFG, _I64, ctypes.POINTER(_I64)],
+    'siren_laplace_backward': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P],
     'siren_second_order_ws_floats': [_CFG, _I64, ctypes.c_int32, ctypes.POINTER(_I64)],
     'siren_second_order': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P],
 }

@@ -85,3 +85,21 @@ def hvp_vjp(cfg, x, flat, v, g, create_graph):
     if not v.requires_grad:
         rv = None
     return rx, rp, rv
+
+
+def laplacian(cfg, x, flat):
+    """sum_j sum_i d2 Phi_j / dx_i2 as a differentiable graph (diff_operators.laplace's op sequence)."""
+    y = forward(cfg, x, flat)
+    g = torch.autograd.grad(y, x, torch.ones_like(y), create_graph=True)[0]
+    lap = 0.
+    for i in range(x.shape[-1]):
+        lap = lap + torch.autograd.grad(g[:, i], x, torch.ones_like(g[:, i]), create_graph=True)[0][:, i:i + 1]
+    return lap
+
+
+def laplace_vjp(cfg, x, flat, glap, create_graph):
+    """d/d(x, theta) of <glap, Laplacian(x; theta)> (the backward of the fused Laplacian node)."""
+    with torch.enable_grad():
+        lap = laplacian(cfg, x, flat)
+        gx, gp = _grads(lap, [x, flat], glap, create_graph)
+    return gx, gp

@@ -179,3 +179,70 @@ class SirenVJP(torch.autograd.Function):
             _, J = eng.forward_grad(ctx.ws, x, want_y=False)
             ggy = (J * ggx).sum(-1, keepdim=True)
         return None, None, (gx if need_x else None), gp, ggy
+
+
+class SirenLaplace(torch.autograd.Function):
+    """Laplacian sum_j sum_i d2 Phi_j/dx_i2 (n, 1) as ONE graph node: forward = the W4 jet kernel
+    (siren_forward_laplace: y, grad and Laplacian in one forward-mode sweep). diff_operators.laplace routes here
+    when its y comes straight from a SirenFunction node of x. Backward (laplace_mse training, a third derivative)
+    = the W4s kernels (siren_laplace_backward: reverse of the jet + MFMA wgrad over 4N columns); only a
+    differentiable backward (create_graph over it, a fourth derivative) recomputes with device torch ops."""
+
+    @staticmethod
+    def forward(ctx, engine, ws, x, flat):
+        _, _, lap = engine.forward_laplace(ws, x)
+        ctx.engine, ctx.ws = engine, ws
+        ctx.save_for_backward(x, flat)
+        return lap
+
+    @staticmethod
+    def backward(ctx, glap):
+        x, flat = ctx.saved_tensors
+        # tensor inputs in order: ws (0), x (1), flat (2)
+        need_x = ctx.needs_input_grad[2] and _will_execute(ctx, 1)
+        need_p = ctx.needs_input_grad[3] and _will_execute(ctx, 2)
+        if not (need_x or need_p):
+            return None, None, None, None
+        if not torch.is_grad_enabled():
+            gx, gp = ctx.engine.laplace_backward(ctx.ws, x, glap)
+            return None, None, (gx if need_x else None), (gp if need_p else None)
+        gx, gp = _torch_path.laplace_vjp(ctx.engine.cfg, x, flat, glap.contiguous(),
+                                         create_graph=torch.is_grad_enabled())
+        return None, None, (gx if need_x else None), (gp if need_p else None)
+
+
+_VIEW_NODES = ('ViewBackward0', 'ReshapeAliasBackward0', 'UnsafeViewBackward0')
+
+
+def siren_node_of(y, x):
+    """The SirenFunction node that produced y (through views only) from a view of x, else None."""
+    node = getattr(y, 'grad_fn', None)
+    for _ in range(4):
+        if node is None:
+            return None
+        name = type(node).__name__
+        if name == 'SirenFunctionBackward':
+            break
+        if name not in _VIEW_NODES:
+            return None
+        node = node.next_functions[0][0]
+    else:
+        return None
+    if not hasattr(node, 'engine') or not hasattr(node, 'ws'):
+        return None
+    xs = node.saved_tensors[0]
+    if xs.data_ptr() != x.data_ptr() or xs.numel() != x.numel() or x.shape[-1] != xs.shape[-1]:
+        return None
+    if not (xs is x or xs._base is x or (x._base is not None and xs._base is x._base)):
+        return None
+    return node
+
+
+def fused_laplace(y, x):
+    """diff_operators.laplace(y, x) in one W4 launch when y = SingleBVPNet/FCBlock output of x; else None."""
+    node = siren_node_of(y, x)
+    if node is None or not node.engine.laplace_supported:
+        return None
+    xs, flat = node.saved_tensors
+    lap = SirenLaplace.apply(node.engine, node.ws, xs, flat)
+    return lap.view(*y.shape[:-1], 1)

@@ -1,0 +1,188 @@
+#pragma once
+// jet_kernel.hpp — W4s: the backward of the fused Laplacian (laplace_mse training, loss_functions.py:104-109).
+//
+// The forward is the W4 jet (w1_kernel MODE_JET): per coordinate, 4 jet streams (value, d/dx_1, d/dx_2,
+// sum_i d2/dx_i2) of every layer, packed as 4 coordinates x 4 streams into the 16 MFMA columns of a wave. Its
+// reverse is again a 16-column MFMA sweep: the cotangent of a layer's output jet goes back through W_l^T for all
+// streams at once, and the elementwise coupling between the streams (jet_sin_adjoint, siren_common.h) runs in
+// the epilogue with the quad's values exchanged by DPP. The weight gradient of layer l is then
+//   dW_l = sum over all 16 columns of zb_l (jet of the layer-l pre-activation cotangent) x a_{l-1} (jet)
+// i.e. wgrad_kernel over K = 4 N columns (bias: value columns only), and the first / output layers are reduced
+// by small_jet_kernel:
+//   dW_0[:, k] = sum zb_0,value x_k + zb_0,tangent k     db_0 = sum zb_0,value     (z_0 = W0 x + b0, dz_0/dx_k = W0[:, k])
+//   dWout[j]   = sum glap a_L,second                                               (lap = sum_j Wout_j a_L,second)
+//   gx         = W0^T zb_0,value
+//
+// jet_store_kernel: forward jet (stores a-jets to abuf and z-jets to a lane-major scratch), seed
+// u_L,second = (sum_j Wout_j) glap, then the reverse sweep storing zb-jets to dbuf; one layer body for all 2L
+// GEMM passes (runtime loop), 3-slot ring of 16 KiB slices (ring.hpp). Tiles are 16 columns = 4 coordinates.
+#include "ring.hpp"
+#include "siren_common.h"
+#include "siren_params.h"
+
+namespace siren {
+
+__global__ __launch_bounds__(THREADS, 1) void jet_store_kernel(
+    const float* __restrict__ ws, const float* __restrict__ x, int64_t n, const float* __restrict__ glap,
+    float* __restrict__ gx, int d, int o, int lh, float w0, float w, float* __restrict__ spill,
+    float* __restrict__ abuf, float* __restrict__ dbuf, int64_t n_pad) {
+    __shared__ __attribute__((aligned(16))) float lds[NBUF * SLICE + SMALL_MAX];
+    float* ring = lds;
+    float* sm = lds + NBUF * SLICE;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane >> 4, c = lane & 15, js = c & 3;
+    const int nslices = 2 * lh * NB;
+    const float* stream = ws + small_pad(lh);
+    {
+        const int nf4 = (small_floats(lh) + 3) / 4;
+        for (int e = threadIdx.x; e < nf4; e += THREADS) ((f32x4*)sm)[e] = ((const f32x4*)ws)[e];
+    }
+    const int64_t coord = (int64_t)blockIdx.x * 16 + wave * 4 + (c >> 2);
+    const bool valid = coord < n;
+    const int64_t wt = (int64_t)blockIdx.x * WAVES + wave;      // 16-column tile (4 coordinates)
+    const int64_t lstride = 4 * n_pad * H;                      // floats per layer (n_pad coordinates)
+    const int64_t toff = wt * (H * 16) + 4 * g * 16 + c;
+    float* sp = spill + wt * (H * 16) + lane * 4;
+    float xv[MAXD];
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k) xv[k] = (valid && k < d) ? x[coord * d + k] : 0.f;
+    const float val = js == 0 ? 1.f : 0.f;
+    float jcf[MAXD];
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k) jcf[k] = val * xv[k] + (js == k + 1 ? 1.f : 0.f);
+    const float kb0 = js == 0 ? 0.f : w0, kg0 = js == 3 ? w0 * w0 : 0.f;
+    const float kb = js == 0 ? 0.f : w, kg = js == 3 ? w * w : 0.f;
+    const float m12 = (js == 1 || js == 2) ? 1.f : 0.f;
+    const float gl = (valid && js == 3) ? glap[coord] : 0.f;
+    __syncthreads();
+    ring_issue(stream, ring, 0, nslices, wave, lane);
+    ring_issue(stream, ring, 1, nslices, wave, lane);
+
+    // ---- first layer: z_0 jet (VALU, K = d_in) ---------------------------------------------------------------
+    f32x4 act[NB], acc[NB];
+#pragma unroll
+    for (int rb = 0; rb < NB; ++rb) {
+        const int nb = 16 * rb + 4 * g;
+        f32x4 z = val * *(const f32x4*)(sm + SM_BIAS + nb);
+#pragma unroll
+        for (int k = 0; k < MAXD; ++k)
+            if (k < d) z += jcf[k] * *(const f32x4*)(sm + SM_W0 + k * H + nb);
+        *(f32x4*)(sp + rb * 256) = z;
+        act[rb] = jet_sin(z, w0, val, kb0, kg0);
+    }
+    store_tile(abuf + toff, act);
+
+    int s = 0;
+#pragma unroll 1
+    for (int p = 0; p < 2 * lh; ++p) {
+#pragma unroll
+        for (int ob = 0; ob < NB; ++ob) acc[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb2 = 0; kb2 < NB; ++kb2) {
+            ring_wait(s, nslices);
+            ring_issue(stream, ring, s + 2, nslices, wave, lane);
+            const float* sl = ring + (s % NBUF) * SLICE + lane * 4;
+            const f32x4 bop = act[kb2];
+#pragma unroll
+            for (int ob = 0; ob < NB; ob += 2) {
+                const f32x4 a0 = *(const f32x4*)(sl + ob * 256);
+                const f32x4 a1 = *(const f32x4*)(sl + (ob + 1) * 256);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    acc[ob] = mfma4(a0[r], bop[r], acc[ob]);
+                    acc[ob + 1] = mfma4(a1[r], bop[r], acc[ob + 1]);
+                }
+            }
+            ++s;
+        }
+        if (p < lh) {
+            // forward layer l = p + 1: z_l jet -> scratch, a_l jet -> abuf
+            const int l = p + 1;
+            const float* bl = sm + SM_BIAS + l * H + 4 * g;
+            float* zp = sp + (int64_t)l * lstride;
+#pragma unroll
+            for (int rb = 0; rb < NB; ++rb) {
+                const f32x4 z = acc[rb] + val * *(const f32x4*)(bl + 16 * rb);
+                *(f32x4*)(zp + rb * 256) = z;
+                act[rb] = jet_sin(z, w, val, kb, kg);
+            }
+            store_tile(abuf + (int64_t)l * lstride + toff, act);
+            if (l == lh) {
+                // seed: u_L (cotangent of the a_L jet) = (sum_j Wout_j) glap on the second-order stream only,
+                // then zb_L = adjoint of the last sine layer
+#pragma unroll
+                for (int rb = 0; rb < NB; ++rb) {
+                    const f32x4 u = gl * *(const f32x4*)(sm + SM_SEED + 16 * rb + 4 * g);
+                    const f32x4 z = *(const f32x4*)(zp + rb * 256);
+                    act[rb] = jet_sin_adjoint(u, z, w, val, m12);
+                }
+                store_tile(dbuf + (int64_t)lh * lstride + toff, act);
+            }
+        } else {
+            // reverse through W_l (l = 2L - p): acc = u_{l-1}, zb_{l-1} = adjoint of sine layer l-1
+            const int lm = 2 * lh - p - 1;
+            const float* zp = sp + (int64_t)lm * lstride;
+            const float wl = lm == 0 ? w0 : w;
+#pragma unroll
+            for (int rb = 0; rb < NB; ++rb) act[rb] = jet_sin_adjoint(acc[rb], *(const f32x4*)(zp + rb * 256), wl, val, m12);
+            store_tile(dbuf + (int64_t)lm * lstride + toff, act);
+        }
+    }
+
+    // ---- gx = W0^T zb_0 (value stream) -----------------------------------------------------------------------
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k) {
+        if (k < d) {
+            float q = 0.f;
+#pragma unroll
+            for (int rb = 0; rb < NB; ++rb) {
+                const f32x4 wk = *(const f32x4*)(sm + SM_W0 + k * H + 16 * rb + 4 * g);
+                q += wk[0] * act[rb][0] + wk[1] * act[rb][1] + wk[2] * act[rb][2] + wk[3] * act[rb][3];
+            }
+            q = sum_groups(q);
+            if (valid && g == 0 && js == 0) gx[coord * d + k] = q;
+        }
+    }
+}
+
+// grid (S): first- and output-layer gradients of the jet backward; thread t owns neuron t. Tiles are 16 columns
+// (4 coordinates x 4 streams), T = n_pad / 4 of them.
+__global__ __launch_bounds__(THREADS) void small_jet_kernel(const float* __restrict__ abuf,
+                                                            const float* __restrict__ dbuf,
+                                                            const float* __restrict__ x,
+                                                            const float* __restrict__ glap, int64_t n,
+                                                            int64_t n_pad, int64_t tps, float* __restrict__ partial,
+                                                            int64_t P, int d, int o, int lh) {
+    const ParamOffsets off(d, o, lh);
+    const int s = blockIdx.x, t = threadIdx.x;
+    const int64_t T = n_pad / 4;
+    const int64_t t0 = (int64_t)s * tps, t1 = t0 + tps < T ? t0 + tps : T;
+    const float* z0 = dbuf;                                    // zb_0 jet
+    const float* aL = abuf + (int64_t)lh * 4 * n_pad * H;      // a_L jet
+    float gw0[MAXD] = {0.f, 0.f, 0.f, 0.f}, gb0 = 0.f, gwo = 0.f;
+    for (int64_t tile = t0; tile < t1; ++tile) {
+        const f32x4* zrow = (const f32x4*)(z0 + tile * (H * 16) + t * 16);
+        const f32x4* arow = (const f32x4*)(aL + tile * (H * 16) + t * 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {  // column group q = coordinate tile*4 + q, streams in the f32x4
+            const int64_t cd = tile * 4 + q;
+            if (cd < n) {
+                const f32x4 zv = zrow[q], av = arow[q];
+                gb0 += zv[0];
+#pragma unroll
+                for (int k = 0; k < MAXD; ++k)
+                    if (k < d) gw0[k] += zv[0] * x[cd * d + k] + (k < 2 ? zv[k + 1] : 0.f);
+                gwo += glap[cd] * av[3];
+            }
+        }
+    }
+    float* out = partial + (int64_t)s * P;
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k)
+        if (k < d) out[off.w0 + (int64_t)t * d + k] = gw0[k];
+    out[off.b0 + t] = gb0;
+    for (int j = 0; j < o; ++j) out[off.wout + (int64_t)j * H + t] = gwo;
+    if (t < o) out[off.bout + t] = 0.f;
+}
+
+}  // namespace siren

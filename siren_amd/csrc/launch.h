@@ -27,6 +27,16 @@ void launch_legacy_grad(bool store, dim3 grid, hipStream_t st, const FusedArgs& 
 // tu_w1.hip: mode 0 = W1, 1 = STORE (W2 stage 1); tu_w0.hip: forward only
 void launch_w1(int mode, dim3 grid, hipStream_t st, const FusedArgs& a);
 void launch_w0(dim3 grid, hipStream_t st, const FusedArgs& a);
+// tu_w4.hip: JET mode (16 coordinates per workgroup); lap (n) = sum_j Laplacian(y_j), gx (n, d) = sum_j grad y_j
+void launch_w4(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, float* y, float* gx, float* lap,
+               int d, int o, int lh, float w0, float w);
+// tu_jet.hip: W4s (backward of the fused Laplacian), tiles of 16 columns = 4 coordinates x 4 jet streams
+void launch_jet_store(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* glap,
+                      float* gx, int d, int o, int lh, float w0, float w, float* spill, float* abuf, float* dbuf,
+                      int64_t n_pad);
+void launch_small_jet(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x,
+                      const float* glap, int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d,
+                      int o, int lh);
 // tu_wide.hip: hidden width 512 (mode as siren_common.h MODE_*); spill = cos scratch for MODE_W1 / MODE_STORE
 void launch_wide(int mode, dim3 grid, hipStream_t st, const FusedArgs& a, float* spill);
 // tu_w3.hip
@@ -38,7 +48,7 @@ void launch_small_w3(dim3 grid, hipStream_t st, const float* At, const float* D,
                      int lh);
 // tu_train.hip
 void launch_wgrad(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, int64_t n_pad, int64_t tps,
-                  float* partial, int64_t P, int d, int o, int lh, int with_bias, int h);
+                  float* partial, int64_t P, int d, int o, int lh, int with_bias, int h, int jet_bias = 0);
 void launch_small(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* gy,
                   int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d, int o, int lh, int h);
 void launch_reduce(dim3 grid, hipStream_t st, const float* partial, int64_t S, int64_t P, float* gp, int64_t S2,

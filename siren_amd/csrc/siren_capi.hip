@@ -157,6 +157,22 @@ int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x
     return hip_status("siren_forward_grad");
 }
 
+int32_t siren_forward_laplace(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y, float* gx,
+                              float* lap, void* stream) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (wide(cfg) || cfg->d_in > 2 || !cfg->outermost_linear || cfg->n_hidden > 5)
+        return fail(SIREN_EUNSUPPORTED,
+                    "siren_forward_laplace covers hidden 256, in_features <= 2, linear output, 1..5 hidden layers");
+    if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    if (n == 0) return SIREN_OK;
+    if (ws == nullptr || x == nullptr || lap == nullptr) return fail(SIREN_EINVAL, "ws/x/lap is NULL");
+    const int64_t blocks = (n + 15) / 16;  // 4 coordinates x 4 jet streams per wave
+    if (blocks > 0x7fffffffll) return fail(SIREN_EINVAL, "n too large");
+    siren::launch_w4(dim3((unsigned)blocks), (hipStream_t)stream, ws, x, n, y, gx, lap, cfg->d_in, cfg->d_out,
+                     cfg->n_hidden, cfg->omega_first, cfg->omega_hidden);
+    return hip_status("siren_forward_laplace");
+}
+
 int32_t siren_train_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
@@ -206,6 +222,75 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
     const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 4096);
     siren::launch_reduce(dim3((unsigned)rblocks), st, partial, plan.splits, P, gparams, 0, 0, 0);
     return hip_status("siren_backward (reduce)");
+}
+
+// ---- W4s: backward of the fused Laplacian (laplace_mse training) ------------------------------------------
+namespace {
+int check_jet(const siren_cfg* cfg) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (wide(cfg) || cfg->d_in > 2 || !cfg->outermost_linear || cfg->n_hidden > 5)
+        return fail(SIREN_EUNSUPPORTED,
+                    "the fused Laplacian covers hidden 256, in_features <= 2, linear output, 1..5 hidden layers");
+    return SIREN_OK;
+}
+
+// jet tiles are 16 columns = 4 coordinates x 4 streams: a-jets, zb-jets and z-jets of every layer + S slabs
+struct JetPlan {
+    int64_t n_pad, cols, tiles, splits, tps, buf_floats, partial_floats, total;
+    JetPlan(const siren_cfg* cfg, int64_t n) {
+        n_pad = (n + 15) / 16 * 16;
+        cols = 4 * n_pad;
+        tiles = cols / 16;
+        const int64_t want = (512 + cfg->n_hidden - 1) / cfg->n_hidden;
+        splits = tiles < want ? tiles : want;
+        if (splits < 1) splits = 1;
+        tps = (tiles + splits - 1) / splits;
+        splits = (tiles + tps - 1) / tps;
+        if (splits < 1) splits = 1;
+        buf_floats = (int64_t)(cfg->n_hidden + 1) * cols * siren::H;
+        partial_floats = splits * param_count(cfg);
+        total = 3 * buf_floats + partial_floats;
+    }
+};
+}  // namespace
+
+int32_t siren_laplace_backward_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count) {
+    if (int rc = check_jet(cfg)) return rc;
+    if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
+    *count = JetPlan(cfg, n).total;
+    return SIREN_OK;
+}
+
+int32_t siren_laplace_backward(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* glap,
+                               float* tws, float* gx, float* gparams, void* stream) {
+    if (int rc = check_jet(cfg)) return rc;
+    if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    if (ws == nullptr || tws == nullptr || gx == nullptr || gparams == nullptr ||
+        (n > 0 && (x == nullptr || glap == nullptr)))
+        return fail(SIREN_EINVAL, "ws/x/glap/tws/gx/gparams is NULL");
+    const JetPlan plan(cfg, n);
+    const hipStream_t st = (hipStream_t)stream;
+    const int64_t P = param_count(cfg);
+    if (n == 0) {
+        (void)hipMemsetAsync(gparams, 0, P * sizeof(float), st);
+        return hip_status("siren_laplace_backward");
+    }
+    float* abuf = tws;
+    float* dbuf = abuf + plan.buf_floats;
+    float* spill = dbuf + plan.buf_floats;
+    float* partial = spill + plan.buf_floats;
+    siren::launch_jet_store(dim3((unsigned)(plan.n_pad / 16)), st, ws, x, n, glap, gx, cfg->d_in, cfg->d_out,
+                            cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, spill, abuf, dbuf, plan.n_pad);
+    if (int rc = hip_status("siren_laplace_backward (jet store)")) return rc;
+    siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden), st, abuf, dbuf, plan.cols, plan.tps,
+                        partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1, siren::H, 1);
+    if (int rc = hip_status("siren_laplace_backward (wgrad)")) return rc;
+    siren::launch_small_jet(dim3((unsigned)plan.splits), st, abuf, dbuf, x, glap, n, plan.n_pad, plan.tps, partial,
+                            P, cfg->d_in, cfg->d_out, cfg->n_hidden);
+    if (int rc = hip_status("siren_laplace_backward (small)")) return rc;
+    const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 4096);
+    siren::launch_reduce(dim3((unsigned)rblocks), st, partial, plan.splits, P, gparams, 0, 0, 0);
+    return hip_status("siren_laplace_backward (reduce)");
 }
 
 // ---- W3: second-order adjoint (Hessian-vector product + mixed theta gradient), d_out == 1 ---------------

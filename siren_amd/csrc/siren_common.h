@@ -31,7 +31,10 @@ constexpr int MAX_LH_GRAD = 3;    // max hidden layers of the forward+grad kerne
 
 // w1_kernel modes: W1 (forward + vjp_x), STORE (W2 backward stage 1: also writes a_l, delta_l), FWD (W0: forward
 // only, sin epilogues without cos, output layer folded into a final serial epilogue).
-enum { MODE_W1 = 0, MODE_STORE = 1, MODE_FWD = 2 };
+// MODE_JET (W4): forward-mode Taylor jet for the Laplacian — 4 coordinates x 4 jet streams (value, d/dx_1,
+// d/dx_2, sum_i d2/dx_i2) in the 16 MFMA columns, y / grad / Laplacian in one forward sweep.
+enum { MODE_W1 = 0, MODE_STORE = 1, MODE_FWD = 2, MODE_JET = 3 };
+__host__ __device__ constexpr bool forward_only(int mode) { return mode == MODE_FWD || mode == MODE_JET; }
 
 // Small-parameter block (head of the workspace, copied to LDS by every workgroup):
 //   [SM_W0,  +4H)  W0T[k][n] = W_0[n][k]  (k < d_in, zero padded to 4 rows)
@@ -108,6 +111,53 @@ __device__ __forceinline__ void sincos_fast(float t, float& sn, float& cs) {
     const int cv = (si & odd) | (ci & ~odd);
     sn = __int_as_float(sv ^ ((qi & 2) << 30));
     cs = __int_as_float(cv ^ (((qi + 1) & 2) << 30));
+}
+
+// ---- forward-mode Taylor jets (MODE_JET, jet_kernel.hpp) ---------------------------------------------------
+// A wave's 16 MFMA columns are 4 coordinates x 4 jet streams (column 4q + s): s = 0 value, s = 1, 2 the tangents
+// d/dx_1, d/dx_2, s = 3 the second-order sum sum_i d2/dx_i2. A coordinate's streams sit in one DPP quad.
+template <int SEL>
+__device__ __forceinline__ float quad_bcast(float v) {  // value of quad lane SEL
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), SEL * 0x55, 0xf, 0xf, false));
+}
+
+// the jet of z (this lane's stream) -> the jet of sin(w z):
+//   a = sin(w z0), a_i = w cos(w z0) z_i, a_3 = w cos(w z0) z_3 - w^2 sin(w z0) (z_1^2 + z_2^2)
+// with per-lane coefficients ka = [s == 0], kb = w [s != 0], kg = w^2 [s == 3].
+__device__ __forceinline__ f32x4 jet_sin(const f32x4& z, float w, float ka, float kb, float kg) {
+    f32x4 out;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float z0 = quad_bcast<0>(z[r]), t1 = quad_bcast<1>(z[r]), t2 = quad_bcast<2>(z[r]);
+        float sn, cs;
+        sincos_fast(w * z0, sn, cs);
+        const float q2 = __builtin_fmaf(t1, t1, t2 * t2);
+        out[r] = __builtin_fmaf(ka, sn, __builtin_fmaf(kb * cs, z[r], -(kg * sn) * q2));
+    }
+    return out;
+}
+
+// Adjoint of jet_sin: given this lane's stream of the cotangent u of the output jet and of the input jet z,
+// the cotangent of z (m0 = [s == 0], m12 = [s == 1 or 2]):
+//   zb_3 = w c u_3
+//   zb_i = w c u_i - 2 w^2 s z_i u_3
+//   zb_0 = w c u_0 - w^2 s (u_1 z_1 + u_2 z_2) - u_3 (w^2 s z_3 + w^3 c (z_1^2 + z_2^2))
+__device__ __forceinline__ f32x4 jet_sin_adjoint(const f32x4& u, const f32x4& z, float w, float m0, float m12) {
+    f32x4 out;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float z0 = quad_bcast<0>(z[r]), z1 = quad_bcast<1>(z[r]), z2 = quad_bcast<2>(z[r]);
+        const float z3 = quad_bcast<3>(z[r]);
+        const float u1 = quad_bcast<1>(u[r]), u2 = quad_bcast<2>(u[r]), u3 = quad_bcast<3>(u[r]);
+        float sn, cs;
+        sincos_fast(w * z0, sn, cs);
+        const float wc = w * cs, w2s = w * w * sn;
+        const float t12 = (2.f * w2s) * (z[r] * u3);
+        const float t0 = __builtin_fmaf(w2s, __builtin_fmaf(u1, z1, u2 * z2),
+                                        u3 * __builtin_fmaf(w2s, z3, (w * w * wc) * __builtin_fmaf(z1, z1, z2 * z2)));
+        out[r] = __builtin_fmaf(wc, u[r], -__builtin_fmaf(m12, t12, m0 * t0));
+    }
+    return out;
 }
 
 __device__ __forceinline__ float sin_phase(float t) {

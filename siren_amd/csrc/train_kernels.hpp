@@ -39,7 +39,8 @@ __device__ __forceinline__ void wg_issue(const float* __restrict__ dsrc, const f
 __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restrict__ abuf,
                                                           const float* __restrict__ dbuf, int64_t n_pad,
                                                           int64_t tps, float* __restrict__ partial, int64_t P,
-                                                          int d, int o, int lh, int with_bias, int h) {
+                                                          int d, int o, int lh, int with_bias, int h,
+                                                          int jet_bias = 0) {
     __shared__ __attribute__((aligned(16))) float ring[WG_NBUF * WG_SLOT];
     const ParamOffsets off(d, o, lh, h);
     const int s = blockIdx.x, l = blockIdx.y + 1;
@@ -72,11 +73,15 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
         wg_issue(dsrc, asrc, ring, t + 2, t1, k + 2, wave, lane, tstride);
         const float* sd = ring + (k % WG_NBUF) * WG_SLOT;
         const float* sa = sd + WG_TILE_FLOATS;
-        // bias gradient: thread t owns neuron t
+        // bias gradient: thread t owns neuron t (jet tiles: the bias only enters the value columns 0, 4, 8, 12)
         {
             const f32x4* row = (const f32x4*)(sd + threadIdx.x * 16);
-            const f32x4 v = row[0] + row[1] + row[2] + row[3];
-            bsum += (v[0] + v[1]) + (v[2] + v[3]);
+            if (jet_bias) {
+                bsum += (row[0][0] + row[1][0]) + (row[2][0] + row[3][0]);
+            } else {
+                const f32x4 v = row[0] + row[1] + row[2] + row[3];
+                bsum += (v[0] + v[1]) + (v[2] + v[3]);
+            }
         }
         f32x4 av[8], bv[8];
 #pragma unroll

@@ -5,9 +5,9 @@
 namespace siren {
 
 void launch_wgrad(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, int64_t n_pad, int64_t tps,
-                  float* partial, int64_t P, int d, int o, int lh, int with_bias, int h) {
+                  float* partial, int64_t P, int d, int o, int lh, int with_bias, int h, int jet_bias) {
     hipLaunchKernelGGL(wgrad_kernel, grid, dim3(THREADS), 0, st, abuf, dbuf, n_pad, tps, partial, P, d, o, lh,
-                       with_bias, h);
+                       with_bias, h, jet_bias);
 }
 
 void launch_small(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* gy,

@@ -24,6 +24,12 @@
 //   * sincos_fast (siren_common.h) is branch-free: fma Cody-Waite with a full-precision pi/2, valid for
 //     |w z| < 1e6 rad (|z| < 3.3e4 at w = 30), <= 1.1e-7 absolute error.
 //   * STORE (W2 backward stage 1) additionally writes a_l and delta_l in 16-coordinate tiles.
+//   * JET (W4, the fused Laplacian): forward sweep only, but the 16 MFMA columns of a wave are 4 coordinates x
+//     4 jet streams s (column 4q + s): s = 0 the value z, s = 1, 2 the tangents dz/dx_s, s = 3 the second-order
+//     sum sum_i d2z/dx_i2. Weights act on every stream (bias only on s = 0), and the epilogue maps the jet of z
+//     to the jet of a = sin(w z) with the quad's stream-0/1/2 values broadcast by DPP quad_perm:
+//       a = sin(w z), da_i = w cos(w z) dz_i, d2a = w cos(w z) d2z - w^2 sin(w z) sum_i dz_i^2.
+//     The output layer turns the streams into y, grad y and the Laplacian (diff_operators.py:27-43).
 // Requires outermost_linear (SingleBVPNet); the notebook Siren's final sine uses fused_kernel.
 #pragma once
 #include <type_traits>
@@ -87,11 +93,14 @@ __device__ __forceinline__ void lgkm_wait(f32x4& a, f32x4& b) {
     asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N));
 }
 
+template <int MODE>
+constexpr int npasses() { return forward_only(MODE) ? 1 : 2; }
+
 template <int LH, int MODE>
 struct W1State {
     f32x4 act[NB];     // B operand of the current GEMM (filled one block ahead)
     f32x4 acc[2][NB];  // ping-pong accumulators
-    f32x4 C[MODE == MODE_FWD ? 1 : LH][NB];  // cos(w z_l), l = 0 .. LH-1 (unused in FWD mode)
+    f32x4 C[forward_only(MODE) ? 1 : LH][NB];  // cos(w z_l), l = 0 .. LH-1 (unused in forward-only modes)
     f32x4 pa0, pa1;    // prefetched first operand pair of the next slice
     float xv[MAXD];    // this lane's coordinate
     float gyv[MAXO];   // this lane's output cotangent
@@ -110,6 +119,10 @@ struct W1Ctx {
     int64_t lstride;
     unsigned ring_vaddr;  // LDS byte address of this lane's 16 B in slot 0 of the ring
     unsigned sm_vaddr;    // LDS byte address of the small-parameter block + this lane's 4*g neuron offset
+    // JET: per-lane stream coefficients (stream s = lane & 3)
+    float jcf[MAXD];      // first layer: z = sum_k jcf[k] W0[:, k] + jcb b0  (value: x_k; tangent s: e_{s-1})
+    float jcb;            // 1 on the value stream (bias), else 0
+    float ja, jb0, jg0, jb, jg;  // a = ja sin + jb cos dz - jg sin |dz|^2  (jb0/jg0 with w0, jb/jg with w)
 };
 
 __device__ __forceinline__ void ring_issue4(const float* __restrict__ stream, float* ring, int s, int wave, int lane) {
@@ -157,8 +170,18 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
                                             const EpiParams<epi_kind<G, LH>(), G, LH>& ep) {
     constexpr int KIND = epi_kind<G, LH>();
     constexpr bool STORE = MODE == MODE_STORE;
-    constexpr bool FWD = MODE == MODE_FWD;
-    if constexpr (KIND == EPI_FIRST) {
+    constexpr bool FWD = forward_only(MODE);
+    if constexpr (MODE == MODE_JET && KIND == EPI_FIRST) {
+        f32x4 z = cx.jcf[0] * ep.v[0];
+#pragma unroll
+        for (int k = 1; k < MAXD; ++k)
+            if (k < cx.d) z += cx.jcf[k] * ep.v[k];
+        z += cx.jcb * ep.v[4];
+        st.act[b] = jet_sin(z, cx.w0, cx.ja, cx.jb0, cx.jg0);
+    } else if constexpr (MODE == MODE_JET && KIND == EPI_SINCOS) {
+        const f32x4 z = st.acc[(G + 1) & 1][b] + cx.jcb * ep.v[0];
+        st.act[b] = jet_sin(z, cx.w, cx.ja, cx.jb, cx.jg);
+    } else if constexpr (KIND == EPI_FIRST) {
         f32x4 z = st.xv[0] * ep.v[0];
 #pragma unroll
         for (int k = 1; k < MAXD; ++k)
@@ -220,7 +243,7 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
 // slice's first pair prefetched during pair 7, and epilogue block KB+1 of GEMM G-1 in the MFMA shadow.
 template <int G, int KB, int LH, int MODE>
 __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx) {
-    constexpr int NS = (MODE == MODE_FWD ? 1 : 2) * LH * NB;
+    constexpr int NS = npasses<MODE>() * LH * NB;
     constexpr int S = G * NB + KB;
     constexpr int SLOT = (S % W1_NBUF) * SLICE * 4;
     constexpr int NSLOT = ((S + 1) % W1_NBUF) * SLICE * 4;
@@ -297,7 +320,7 @@ __device__ __forceinline__ void w1_gemm(W1State<LH, MODE>& st, const W1Ctx& cx) 
 
 template <int G, int LH, int MODE>
 __device__ __forceinline__ void w1_run(W1State<LH, MODE>& st, const W1Ctx& cx) {
-    if constexpr (G < (MODE == MODE_FWD ? 1 : 2) * LH) {
+    if constexpr (G < npasses<MODE>() * LH) {
         w1_gemm<G, LH, MODE>(st, cx);
         w1_run<G + 1, LH, MODE>(st, cx);
     }
@@ -305,14 +328,17 @@ __device__ __forceinline__ void w1_run(W1State<LH, MODE>& st, const W1Ctx& cx) {
 
 constexpr int small_floats_ct(int lh) { return SM_BIAS + (lh + 1) * H; }
 
+// JET mode: 16 coordinates per workgroup (4 per wave); lap (n) receives sum_j Laplacian(y_j), gx (n, d) sum_j
+// grad y_j (the quantities diff_operators.laplace / gradient return); abuf is reused as the lap pointer.
 template <int LH, int MODE>
-__global__ __launch_bounds__(THREADS, MODE == MODE_FWD ? 2 : 1) void w1_kernel(const float* __restrict__ ws, const float* __restrict__ x,
+__global__ __launch_bounds__(THREADS, forward_only(MODE) ? 2 : 1) void w1_kernel(const float* __restrict__ ws, const float* __restrict__ x,
                                                         int64_t n, const float* __restrict__ gy, float* __restrict__ y,
                                                         float* __restrict__ gx, int d, int o, float w0, float w,
                                                         float* __restrict__ abuf, float* __restrict__ dbuf,
                                                         int64_t n_pad) {
     constexpr bool STORE = MODE == MODE_STORE;
-    constexpr int NS = (MODE == MODE_FWD ? 1 : 2) * LH * NB;
+    constexpr bool JET = MODE == MODE_JET;
+    constexpr int NS = npasses<MODE>() * LH * NB;
     __shared__ __attribute__((aligned(16))) float lds[W1_NBUF * SLICE + small_floats_ct(LH)];
     W1Ctx cx;
     W1State<LH, MODE> st;
@@ -341,10 +367,23 @@ __global__ __launch_bounds__(THREADS, MODE == MODE_FWD ? 2 : 1) void w1_kernel(c
         const int nf4 = (small_floats(LH) + 3) / 4;
         for (int e = threadIdx.x; e < nf4; e += THREADS) ((f32x4*)sm)[e] = ((const f32x4*)ws)[e];
     }
-    const int64_t coord = (int64_t)blockIdx.x * TILE + cx.wave * 16 + c;
+    const int js = c & 3;  // JET stream of this lane
+    const int64_t coord = JET ? (int64_t)blockIdx.x * 16 + cx.wave * 4 + (c >> 2)
+                              : (int64_t)blockIdx.x * TILE + cx.wave * 16 + c;
     const bool valid = coord < n;
 #pragma unroll
     for (int k = 0; k < MAXD; ++k) st.xv[k] = (valid && k < d) ? x[coord * d + k] : 0.f;
+    if constexpr (JET) {
+        const float val = js == 0 ? 1.f : 0.f;
+#pragma unroll
+        for (int k = 0; k < MAXD; ++k) cx.jcf[k] = val * st.xv[k] + (js == k + 1 ? 1.f : 0.f);
+        cx.jcb = val;
+        cx.ja = val;
+        cx.jb0 = js == 0 ? 0.f : w0;
+        cx.jg0 = js == 3 ? w0 * w0 : 0.f;
+        cx.jb = js == 0 ? 0.f : w;
+        cx.jg = js == 3 ? w * w : 0.f;
+    }
 #pragma unroll
     for (int j = 0; j < MAXO; ++j) {
         st.yp[j] = 0.f;
@@ -363,6 +402,37 @@ __global__ __launch_bounds__(THREADS, MODE == MODE_FWD ? 2 : 1) void w1_kernel(c
 
     w1_run<0, LH, MODE>(st, cx);
 
+    if constexpr (JET) {
+        // last hidden layer's jet, output layer per stream, then y / grad / Laplacian from the quad's lanes
+        constexpr int GL = (LH - 1) & 1;
+#pragma unroll
+        for (int rb = 0; rb < NB; ++rb) {
+            const int nb = 16 * rb + 4 * cx.g;
+            const f32x4 z = st.acc[GL][rb] + cx.jcb * *(const f32x4*)(sm + SM_BIAS + LH * H + nb);
+            const f32x4 a = jet_sin(z, w, cx.ja, cx.jb, cx.jg);
+#pragma unroll
+            for (int j = 0; j < MAXO; ++j) {
+                if (j < o) {
+                    const f32x4 wj = *(const f32x4*)(sm + SM_WO + j * H + nb);
+                    st.yp[j] += wj[0] * a[0] + wj[1] * a[1] + wj[2] * a[2] + wj[3] * a[3];
+                }
+            }
+        }
+        float tot = 0.f;
+#pragma unroll
+        for (int j = 0; j < MAXO; ++j) {
+            if (j < o) {
+                const float vj = sum_groups(st.yp[j]) + cx.jcb * sm[SM_BOUT + j];
+                if (y != nullptr && valid && cx.g == 0 && js == 0) y[coord * o + j] = vj;
+                tot += vj;
+            }
+        }
+        if (valid && cx.g == 0) {
+            if (js == 3) abuf[coord] = tot;
+            else if (js >= 1 && js <= d && gx != nullptr) gx[coord * d + js - 1] = tot;
+        }
+        return;
+    }
     if constexpr (MODE == MODE_FWD) {
         // last hidden layer: z_L = acc + b_L, a_L = sin(w z_L), y = a_L Wout^T + bout (serial epilogue)
         constexpr int GL = (LH - 1) & 1;

@@ -24,6 +24,13 @@ def divergence(y, x):
 
 
 def laplace(y, x):
+    """divergence(gradient(y, x), x) (diff_operators.py:27-29). When y is a siren_amd SIREN's output of x, the whole
+    Laplacian is ONE fused forward-mode kernel launch (W4, autograd.SirenLaplace) instead of d + 1 autograd
+    sweeps; otherwise (or for networks the jet kernel does not cover) the reference's autograd recipe runs."""
+    from .autograd import fused_laplace
+    lap = fused_laplace(y, x)
+    if lap is not None:
+        return lap
     return divergence(gradient(y, x), x)
 
 

@@ -43,6 +43,9 @@ class SirenEngine:
         # hidden 256 keeps cos(w z_l) of every layer in registers (1..3 hidden layers); hidden 512 spills it
         self.grad_supported = self.supported and (1 <= n_hidden <= 3 or int(hidden) == 512)
         # the W3 second-order kernel: hidden 256, scalar output, linear output layer
+        # the W4 jet kernel (fused Laplacian): hidden 256, d_in <= 2, linear output, 1..5 hidden layers
+        self.laplace_supported = (self.supported and int(hidden) == 256 and int(d_in) <= 2 and 1 <= n_hidden <= 5
+                                  and bool(outermost_linear))
         self.second_order_supported = (self.supported and int(hidden) == 256 and 1 <= n_hidden <= 3
                                        and int(d_out) == 1 and bool(outermost_linear))
 
@@ -113,6 +116,45 @@ class SirenEngine:
         _lib.check(self.lib.siren_forward_grad(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(gy), _ptr(y),
                                                _ptr(gx), _stream(x.device)), 'siren_forward_grad')
         return y, gx
+
+    def forward_laplace(self, ws, x, want_y=False, want_gx=False):
+        """W4 in one launch: (y | None, sum_j grad y_j | None, sum_j Laplacian y_j (n, 1)) — what
+        diff_operators.gradient / laplace return (diff_operators.py:27-43)."""
+        self._require()
+        if not self.laplace_supported:
+            raise _lib.SirenUnsupported('siren_forward_laplace covers hidden 256, in_features <= 2, linear output, '
+                                        '1..5 hidden layers')
+        x = self._check_x(x)
+        n = x.shape[0]
+        y = torch.empty(n, self.cfg.d_out, dtype=torch.float32, device=x.device) if want_y else None
+        gx = torch.empty(n, self.cfg.d_in, dtype=torch.float32, device=x.device) if want_gx else None
+        lap = torch.empty(n, 1, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_forward_laplace(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(y), _ptr(gx),
+                                                  _ptr(lap), _stream(x.device)), 'siren_forward_laplace')
+        return y, gx, lap
+
+    def laplace_backward(self, ws, x, glap):
+        """W4s: (gx, gparams) = d/d(x, theta) of sum_c glap_c Laplacian(x_c) — the backward of the fused
+        Laplacian node (laplace_mse training)."""
+        self._require()
+        if not self.laplace_supported:
+            raise _lib.SirenUnsupported('siren_laplace_backward covers hidden 256, in_features <= 2, linear output, '
+                                        '1..5 hidden layers')
+        x = self._check_x(x)
+        n = x.shape[0]
+        glap = glap.reshape(-1).contiguous()
+        if glap.numel() != n or glap.dtype != torch.float32 or glap.device != x.device:
+            raise ValueError('glap must be fp32 with %d values on %s' % (n, x.device))
+        cnt = ctypes.c_int64()
+        _lib.check(self.lib.siren_laplace_backward_ws_floats(ctypes.byref(self.cfg), n, ctypes.byref(cnt)),
+                   'siren_laplace_backward_ws_floats')
+        tws = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
+        gx = torch.empty(n, self.cfg.d_in, dtype=torch.float32, device=x.device)
+        gp = torch.empty(self.param_count, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_laplace_backward(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(glap),
+                                                   _ptr(tws), _ptr(gx), _ptr(gp), _stream(x.device)),
+                   'siren_laplace_backward')
+        return gx, gp
 
     # ------------------------------------------------------------------------------------------------------
     def backward_params(self, ws, x, gy):

@@ -45,6 +45,10 @@ def main():
                            ('W1 forward+vjp_x', lambda: eng.forward_grad(ws, x, gy), 2 * F),
                            ('W2 backward (store+wgrad+small+reduce)', lambda: eng.backward_params(ws, x, gy), 3 * F)):
         report(name, timed(fn), work, a.n)
+    if eng.laplace_supported:
+        # W4 algorithmic unit: (1 + 2d) F; the jet kernel executes 4F (4 MFMA columns/coord)
+        report('W4 y+grad+Laplacian (jet, 1 launch)', timed(lambda: eng.forward_laplace(ws, x, True, True)),
+               (1 + 2 * d) * F, a.n)
     if eng.second_order_supported:
         v = torch.randn(a.n, a.d, device='cuda')
         for name, fn, work in (('W3 H v (x only)', lambda: eng.second_order(ws, x, v, want_theta=False), 4 * F),
