@@ -8,8 +8,9 @@ sharded per rank with no collective on the data path (the W1 path has no exchang
 bracketed by barrier + synchronize and the max over ranks is used.
 
 Also reported: roofline of the fused kernel (HIP events on the launch stream), the oracle's CPU restatement
-timed on the host cores (cpu_baseline), a short W2 training-step rate and the PSNR of a 300-step image fit
-against the reference's (tests/golden manifest), all on the same JSON line.
+timed on the host cores (cpu_baseline), a short W2 training-step rate, the PSNR of a 300-step image fit
+against the reference's (tests/golden manifest), and per-config training / inference rates for the other
+BASELINE configs (sdf = W3, 5x512 video = W2 at hidden 512, Poisson 512^2 = W4/W4s), all on the same JSON line.
 
 python bench.py [--gpus N] [--steps K] [--warmup W] [--n COORDS] [--no-cpu] [--no-extra]
 """
@@ -58,7 +59,7 @@ def cpu_baseline(seconds=15.):
         x = x0.clone().requires_grad_(True)
         y = O.torch_forward(x, params)
         g = O.torch_gradient(y, x)
-        _ = float(g.sum())
+        _ = float(g.detach().sum())
         done += n
         el = time.perf_counter() - t0
         if el > seconds:
@@ -124,6 +125,65 @@ def train_step_rate(device, n=1 << 18, steps=5):
         step()
     torch.cuda.synchronize()
     return n * steps / (time.perf_counter() - t0) / 1e6
+
+
+def config_rates(device, steps=5):
+    """Secondary per-config rates (BASELINE.json configs[2..4]), one GPU, drop-in API end to end (model ->
+    loss_functions -> backward -> Adam), inputs resident on the device. Mcoords/s per GPU."""
+    from siren_amd.modules import SingleBVPNet
+    from siren_amd import loss_functions as LF
+    from siren_amd import dataio
+    from siren_amd.engine import SirenEngine
+    res = {}
+
+    def rate(model, x, loss_fn, n):
+        opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+
+        def step():
+            out = model({'coords': x})
+            total = sum(v.mean() for v in loss_fn(out).values())
+            opt.zero_grad()
+            total.backward()
+            opt.step()
+        step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        return round(n * steps / (time.perf_counter() - t0) / 1e6, 3)
+
+    # configs[2]: sdf (W3 training: on/off-surface sphere batch), 5x256 d3, 2^19 coords per GPU
+    torch.manual_seed(0)
+    m = SingleBVPNet(in_features=3, verbose=False).to(device)
+    inp, gt_sdf = dataio.sphere_sdf_batch(1 << 18, device=device)  # 2^18 on + 2^18 off surface = 2^19
+    n = inp['coords'].shape[1]
+    res['sdf_5x256_d3_train_mcoords_s'] = rate(m, inp['coords'], lambda o: LF.sdf(o, gt_sdf), n)
+    # configs[3]: video fit, 5x512 d3 o3 image_mse (W2 at hidden 512), 2^18 coords per GPU
+    torch.manual_seed(0)
+    m = SingleBVPNet(in_features=3, out_features=3, hidden_features=512, verbose=False).to(device)
+    n = 1 << 18
+    x = torch.rand(1, n, 3, device=device) * 2 - 1
+    gt = 0.5 + 0.5 * torch.sin(3 * x + torch.tensor([0., 1., 2.], device=device))
+    res['video_5x512_d3o3_train_mcoords_s'] = rate(m, x, lambda o: LF.image_mse(None, o, {'img': gt}), n)
+    # configs[4]: Poisson on a 512^2 grid: laplace_mse training (W4 + W4s) and W4 inference (y, grad, Laplacian)
+    torch.manual_seed(0)
+    m = SingleBVPNet(verbose=False).to(device)
+    grid = dataio.get_mgrid(512)[None].to(device)
+    n = grid.shape[1]
+    lap_gt = torch.sin(4 * grid[..., :1])
+    res['poisson_512sq_laplace_mse_train_mcoords_s'] = rate(m, grid, lambda o: LF.laplace_mse(o, {'laplace': lap_gt}), n)
+    eng = SirenEngine(2, 256, 3, 1)
+    ws = eng.pack(seed0_params(device))
+    x2 = grid[0].contiguous()
+    eng.forward_laplace(ws, x2, True, True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.forward_laplace(ws, x2, True, True)
+    torch.cuda.synchronize()
+    res['poisson_512sq_w4_y_grad_laplacian_mcoords_s'] = round(n * steps / (time.perf_counter() - t0) / 1e6, 3)
+    return res
 
 
 def psnr_fit(device, steps=300):
@@ -203,6 +263,7 @@ def main():
     extra = {}
     if rank == 0 and not args.no_extra:
         extra['w2_image_mse_train_mcoords_s'] = round(train_step_rate(device), 3)
+        extra['configs'] = config_rates(device)
         p, secs = psnr_fit(device)
         extra['psnr_db'] = {'value': round(p, 3), 'reference_cpu': REF_PSNR_DB, 'steps': 300,
                             'fit_seconds': round(secs, 2)}

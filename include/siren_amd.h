@@ -50,6 +50,8 @@ enum {
 /* cfg.reserved flags (benchmarking only): run the round-1 kernel whose sin/cos epilogues are not
  * interleaved with the MFMA stream, for in-process A/B timing. */
 #define SIREN_FLAG_LEGACY_KERNEL 1
+/* cfg.reserved flag (benchmarking only): one workgroup per coordinate tile instead of the persistent grid. */
+#define SIREN_FLAG_NO_PERSIST 2
 
 /* Network description. Mirrors SingleBVPNet(out_features, type='sine', in_features, mode='mlp',
  * hidden_features, num_hidden_layers) (modules.py:122-123) and the notebook Siren(in_features,

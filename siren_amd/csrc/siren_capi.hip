@@ -52,6 +52,25 @@ int64_t ws_floats(const siren_cfg* cfg) {
     return small_pad(cfg) + 2ll * cfg->n_hidden * (h / 16) * (16 * h);
 }
 
+// Persistent grid for W1 / STORE (one workgroup per CU): each walks tiles blockIdx.x, + gridDim.x, ... with its
+// weight ring streaming across tile boundaries (+1 % on W1, profiles/r01_ab_w1_persist.log). The forward-only
+// modes (2 workgroups per CU) measured slower persistent and keep one workgroup per tile.
+// SIREN_FLAG_NO_PERSIST: one workgroup per tile (A/B).
+dim3 tile_grid(const siren_cfg* cfg, int64_t tiles, int per_cu) {
+    if ((cfg->reserved & SIREN_FLAG_NO_PERSIST) != 0) return dim3((unsigned)tiles);
+    static int cus[64] = {0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) dev = 0;
+    if (cus[dev] == 0) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        cus[dev] = v;
+    }
+    const int64_t g = (int64_t)cus[dev] * per_cu;
+    return dim3((unsigned)(tiles < g ? tiles : g));
+}
+
 int64_t param_count(const siren_cfg* cfg) {
     const int64_t H = cfg->hidden;
     return H * cfg->d_in + H + (int64_t)cfg->n_hidden * (H * H + H) + (int64_t)cfg->d_out * H + cfg->d_out;
@@ -120,7 +139,7 @@ int32_t siren_forward(const siren_cfg* cfg, const float* ws, const float* x, int
     if (wide(cfg))
         siren::launch_wide(siren::MODE_FWD, grid, (hipStream_t)stream, fa, nullptr);
     else if (cfg->outermost_linear && cfg->n_hidden <= 5 && (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0)
-        siren::launch_w0(grid, (hipStream_t)stream, fa);
+        siren::launch_w0(grid, (hipStream_t)stream, fa);  // 2 WGs/CU: persistence measured slower
     else
         siren::launch_legacy_fwd(grid, (hipStream_t)stream, fa);
     return hip_status("siren_forward");
@@ -153,7 +172,7 @@ int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x
     } else if ((cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) != 0 || fs)
         siren::launch_legacy_grad(false, grid, (hipStream_t)stream, fa);
     else
-        siren::launch_w1(siren::MODE_W1, grid, (hipStream_t)stream, fa);
+        siren::launch_w1(siren::MODE_W1, tile_grid(cfg, blocks, 1), (hipStream_t)stream, fa);
     return hip_status("siren_forward_grad");
 }
 
@@ -208,7 +227,7 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
     if (wide(cfg))
         siren::launch_wide(siren::MODE_STORE, grid, st, fa, spill);
     else if ((cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0 && !fs)
-        siren::launch_w1(siren::MODE_STORE, grid, st, fa);
+        siren::launch_w1(siren::MODE_STORE, tile_grid(cfg, plan.n_pad / siren::TILE, 1), st, fa);
     else
         siren::launch_legacy_grad(true, grid, st, fa);
     if (int rc = hip_status("siren_backward (fused store)")) return rc;

@@ -116,6 +116,8 @@ struct W1Ctx {
     bool seed_ones;
     float* abuf;  // STORE: lane-adjusted tile base of layer 0; layer l at + l * lstride
     float* dbuf;
+    bool more;    // persistent grid: this workgroup runs another coordinate tile after the current one, so the
+                  // ring keeps streaming (slices 0..2 of the next tile are issued during the last 3 slices)
     int64_t lstride;
     unsigned ring_vaddr;  // LDS byte address of this lane's 16 B in slot 0 of the ring
     unsigned sm_vaddr;    // LDS byte address of the small-parameter block + this lane's 4*g neuron offset
@@ -256,23 +258,29 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
     f32x4 a0 = st.pa0, a1 = st.pa1;
     static_for<0, NB / 2>([&](auto P) {
         constexpr int p = decltype(P)::value;
-        if constexpr (p == 4 && S + 1 < NS) {
+        if constexpr (p == 4) {
             // publish slice S+1 (own part landed: at most slice S+2's 4 loads still outstanding) and free the
-            // slot of slice S-1 (every wave is past its last read of it) for slice S+3
-            if constexpr (S + 2 < NS)
-                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            if constexpr (S + 3 < NS) {
-                const float* sp = cx.stream;
-                asm volatile("" : "+s"(sp));  // keep slice addresses from being hoisted into SGPRs
-                ring_issue4(sp, cx.ring, S + 3, cx.wave, cx.lane);
+            // slot of slice S-1 (every wave is past its last read of it) for slice S+3. Slices past the end of the
+            // tile are the next tile's slices 0..2 (NS is a multiple of the ring size, so the slots line up).
+            if (S + 1 < NS || cx.more) {
+                if (S + 2 < NS || cx.more)
+                    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                if (S + 3 < NS || cx.more) {
+                    const float* sp = cx.stream;
+                    asm volatile("" : "+s"(sp));  // keep slice addresses from being hoisted into SGPRs
+                    ring_issue4(sp, cx.ring, (S + 3) % NS, cx.wave, cx.lane);
+                }
             }
         }
         f32x4 n0, n1;
         constexpr bool NEXT_IN_SLICE = p + 1 < NB / 2;
         constexpr bool NEXT_SLICE = !NEXT_IN_SLICE && S + 1 < NS;
+        constexpr bool NEXT_TILE = !NEXT_IN_SLICE && S + 1 == NS;  // first pair of the next tile's slice 0
+        static_assert(NS % W1_NBUF == 0, "the ring must wrap onto slot 0 at a tile boundary");
+        bool next = NEXT_IN_SLICE || NEXT_SLICE;
         if constexpr (NEXT_IN_SLICE) {
             n0 = lds_read4<SLOT + (2 * p + 2) * 1024>(cx.ring_vaddr);
             n1 = lds_read4<SLOT + (2 * p + 3) * 1024>(cx.ring_vaddr);
@@ -280,10 +288,20 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
             n0 = lds_read4<NSLOT>(cx.ring_vaddr);
             n1 = lds_read4<NSLOT + 1024>(cx.ring_vaddr);
         }
-        if constexpr (NEXT_IN_SLICE || NEXT_SLICE)
+        if constexpr (NEXT_IN_SLICE || NEXT_SLICE) {
             lgkm_wait<2>(a0, a1);
-        else
+        } else if constexpr (NEXT_TILE) {
+            if (cx.more) {
+                n0 = lds_read4<NSLOT>(cx.ring_vaddr);
+                n1 = lds_read4<NSLOT + 1024>(cx.ring_vaddr);
+                lgkm_wait<2>(a0, a1);
+                next = true;
+            } else {
+                lgkm_wait<0>(a0, a1);
+            }
+        } else {
             lgkm_wait<0>(a0, a1);
+        }
         if constexpr (p == 0 && EPI) {
             // the epilogue parameters were issued before pair 1's reads: the wait above covered them
 #pragma unroll
@@ -294,7 +312,7 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
             acc[2 * p] = mfma4(a0[r], bop[r], acc[2 * p]);
             acc[2 * p + 1] = mfma4(a1[r], bop[r], acc[2 * p + 1]);
         }
-        if constexpr (NEXT_IN_SLICE || NEXT_SLICE) {
+        if (next) {
             a0 = n0;
             a1 = n1;
         }
@@ -354,40 +372,42 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE) ? 2 : 1) void w1_kernel
     cx.w0 = w0;
     cx.w = w;
     cx.seed_ones = gy == nullptr;
+    cx.abuf = cx.dbuf = nullptr;
+    cx.more = false;
     cx.stream = ws + small_pad(LH);
     cx.lstride = n_pad * H;
     const unsigned lds_base = (unsigned)(uintptr_t)((__attribute__((address_space(3))) float*)lds);
     cx.ring_vaddr = lds_base + cx.lane * 16;
     cx.sm_vaddr = lds_base + W1_NBUF * SLICE * 4 + 16 * cx.g;
-    const int64_t toff = ((int64_t)blockIdx.x * WAVES + cx.wave) * (H * 16) + 4 * cx.g * 16 + c;
-    cx.abuf = STORE ? abuf + toff : nullptr;
-    cx.dbuf = STORE ? dbuf + toff : nullptr;
 
     {
         const int nf4 = (small_floats(LH) + 3) / 4;
         for (int e = threadIdx.x; e < nf4; e += THREADS) ((f32x4*)sm)[e] = ((const f32x4*)ws)[e];
     }
     const int js = c & 3;  // JET stream of this lane
-    const int64_t coord = JET ? (int64_t)blockIdx.x * 16 + cx.wave * 4 + (c >> 2)
-                              : (int64_t)blockIdx.x * TILE + cx.wave * 16 + c;
-    const bool valid = coord < n;
+    const int64_t tiles = JET ? (n + 15) / 16 : (n + TILE - 1) / TILE;
+    auto coord_of = [&](int64_t tile) -> int64_t {
+        return JET ? tile * 16 + cx.wave * 4 + (c >> 2) : tile * TILE + cx.wave * 16 + c;
+    };
+    // this lane's inputs for a tile (prefetched one tile ahead so the loads never stall the MFMA stream)
+    float xn[MAXD], gn[MAXO];
+    auto load_inputs = [&](int64_t tile) {
+        const int64_t cd = coord_of(tile);
+        const bool ok = tile < tiles && cd < n;
 #pragma unroll
-    for (int k = 0; k < MAXD; ++k) st.xv[k] = (valid && k < d) ? x[coord * d + k] : 0.f;
+        for (int k = 0; k < MAXD; ++k) xn[k] = (ok && k < d) ? x[cd * d + k] : 0.f;
+#pragma unroll
+        for (int j = 0; j < MAXO; ++j) gn[j] = (gy != nullptr && ok && j < o) ? gy[cd * o + j] : 0.f;
+    };
+    load_inputs(blockIdx.x);
     if constexpr (JET) {
         const float val = js == 0 ? 1.f : 0.f;
-#pragma unroll
-        for (int k = 0; k < MAXD; ++k) cx.jcf[k] = val * st.xv[k] + (js == k + 1 ? 1.f : 0.f);
         cx.jcb = val;
         cx.ja = val;
         cx.jb0 = js == 0 ? 0.f : w0;
         cx.jg0 = js == 3 ? w0 * w0 : 0.f;
         cx.jb = js == 0 ? 0.f : w;
         cx.jg = js == 3 ? w * w : 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < MAXO; ++j) {
-        st.yp[j] = 0.f;
-        st.gyv[j] = (gy != nullptr && valid && j < o) ? gy[coord * o + j] : 0.f;
     }
     __syncthreads();
     // ring prologue: slices 0..2 in flight; slice 0 published; its first operand pair read
@@ -400,95 +420,119 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE) ? 2 : 1) void w1_kernel
     st.pa0 = lds_read4<0>(cx.ring_vaddr);
     st.pa1 = lds_read4<1024>(cx.ring_vaddr);
 
-    w1_run<0, LH, MODE>(st, cx);
-
-    if constexpr (JET) {
-        // last hidden layer's jet, output layer per stream, then y / grad / Laplacian from the quad's lanes
-        constexpr int GL = (LH - 1) & 1;
+    // ---- coordinate tiles: a persistent grid walks tile = blockIdx.x, + gridDim.x, ... (a one-tile-per-
+    // workgroup grid runs the loop once); the weight ring streams on across tile boundaries ----------------------
+#pragma unroll 1
+    for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+        cx.more = tile + gridDim.x < tiles;
+        const int64_t coord = coord_of(tile);
+        const bool valid = coord < n;
 #pragma unroll
-        for (int rb = 0; rb < NB; ++rb) {
-            const int nb = 16 * rb + 4 * cx.g;
-            const f32x4 z = st.acc[GL][rb] + cx.jcb * *(const f32x4*)(sm + SM_BIAS + LH * H + nb);
-            const f32x4 a = jet_sin(z, w, cx.ja, cx.jb, cx.jg);
-#pragma unroll
-            for (int j = 0; j < MAXO; ++j) {
-                if (j < o) {
-                    const f32x4 wj = *(const f32x4*)(sm + SM_WO + j * H + nb);
-                    st.yp[j] += wj[0] * a[0] + wj[1] * a[1] + wj[2] * a[2] + wj[3] * a[3];
-                }
-            }
-        }
-        float tot = 0.f;
+        for (int k = 0; k < MAXD; ++k) st.xv[k] = xn[k];
 #pragma unroll
         for (int j = 0; j < MAXO; ++j) {
-            if (j < o) {
-                const float vj = sum_groups(st.yp[j]) + cx.jcb * sm[SM_BOUT + j];
-                if (y != nullptr && valid && cx.g == 0 && js == 0) y[coord * o + j] = vj;
-                tot += vj;
-            }
+            st.gyv[j] = gn[j];
+            st.yp[j] = 0.f;
         }
-        if (valid && cx.g == 0) {
-            if (js == 3) abuf[coord] = tot;
-            else if (js >= 1 && js <= d && gx != nullptr) gx[coord * d + js - 1] = tot;
+        load_inputs(tile + gridDim.x);
+        if constexpr (JET) {
+#pragma unroll
+            for (int k = 0; k < MAXD; ++k) cx.jcf[k] = cx.ja * st.xv[k] + (js == k + 1 ? 1.f : 0.f);
         }
-        return;
-    }
-    if constexpr (MODE == MODE_FWD) {
-        // last hidden layer: z_L = acc + b_L, a_L = sin(w z_L), y = a_L Wout^T + bout (serial epilogue)
-        constexpr int GL = (LH - 1) & 1;
-#pragma unroll
-        for (int rb = 0; rb < NB; ++rb) {
-            const int nb = 16 * rb + 4 * cx.g;
-            const f32x4 z = st.acc[GL][rb] + *(const f32x4*)(sm + SM_BIAS + LH * H + nb);
-            f32x4 sn;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float a, cc;
-                sincos_fast(w * z[r], a, cc);
-                sn[r] = a;
-            }
-#pragma unroll
-            for (int j = 0; j < MAXO; ++j) {
-                if (j < o) {
-                    const f32x4 wj = *(const f32x4*)(sm + SM_WO + j * H + nb);
-                    st.yp[j] += wj[0] * sn[0] + wj[1] * sn[1] + wj[2] * sn[2] + wj[3] * sn[3];
-                }
-            }
+        if constexpr (STORE) {
+            const int64_t toff = (tile * WAVES + cx.wave) * (H * 16) + 4 * cx.g * 16 + c;
+            cx.abuf = abuf + toff;
+            cx.dbuf = dbuf + toff;
         }
-#pragma unroll
-        for (int j = 0; j < MAXO; ++j) {
-            if (j < o) {
-                const float yj = sum_groups(st.yp[j]) + sm[SM_BOUT + j];
-                if (valid && cx.g == 0) y[coord * o + j] = yj;
-            }
-        }
-        return;
-    }
 
-    // y (reduced over the 4 lane groups)
-#pragma unroll
-    for (int j = 0; j < MAXO; ++j) {
-        if (j < o) {
-            const float yj = sum_groups(st.yp[j]) + sm[SM_BOUT + j];
-            if (y != nullptr && valid && cx.g == 0) y[coord * o + j] = yj;
-        }
-    }
-    // delta_0 = u_0 . cos(w0 z_0) . w0 ;  gx = delta_0 W0
-    constexpr int GL = (2 * LH - 1) & 1;
-#pragma unroll
-    for (int rb = 0; rb < NB; ++rb) st.act[rb] = (st.acc[GL][rb] * st.C[0][rb]) * w0;
-    if constexpr (STORE) store_tile(cx.dbuf, st.act);
-#pragma unroll
-    for (int k = 0; k < MAXD; ++k) {
-        if (k < d) {
-            float p = 0.f;
+        w1_run<0, LH, MODE>(st, cx);
+
+        if constexpr (JET) {
+            // last hidden layer's jet, output layer per stream, then y / grad / Laplacian from the quad's lanes
+            constexpr int GL = (LH - 1) & 1;
 #pragma unroll
             for (int rb = 0; rb < NB; ++rb) {
-                const f32x4 wk = *(const f32x4*)(sm + SM_W0 + k * H + 16 * rb + 4 * cx.g);
-                p += wk[0] * st.act[rb][0] + wk[1] * st.act[rb][1] + wk[2] * st.act[rb][2] + wk[3] * st.act[rb][3];
+                const int nb = 16 * rb + 4 * cx.g;
+                const f32x4 z = st.acc[GL][rb] + cx.jcb * *(const f32x4*)(sm + SM_BIAS + LH * H + nb);
+                const f32x4 a = jet_sin(z, w, cx.ja, cx.jb, cx.jg);
+#pragma unroll
+                for (int j = 0; j < MAXO; ++j) {
+                    if (j < o) {
+                        const f32x4 wj = *(const f32x4*)(sm + SM_WO + j * H + nb);
+                        st.yp[j] += wj[0] * a[0] + wj[1] * a[1] + wj[2] * a[2] + wj[3] * a[3];
+                    }
+                }
             }
-            p = sum_groups(p);
-            if (valid && cx.g == 0) gx[coord * d + k] = p;
+            float tot = 0.f;
+#pragma unroll
+            for (int j = 0; j < MAXO; ++j) {
+                if (j < o) {
+                    const float vj = sum_groups(st.yp[j]) + cx.jcb * sm[SM_BOUT + j];
+                    if (y != nullptr && valid && cx.g == 0 && js == 0) y[coord * o + j] = vj;
+                    tot += vj;
+                }
+            }
+            if (valid && cx.g == 0) {
+                if (js == 3) abuf[coord] = tot;
+                else if (js >= 1 && js <= d && gx != nullptr) gx[coord * d + js - 1] = tot;
+            }
+        } else if constexpr (MODE == MODE_FWD) {
+            // last hidden layer: z_L = acc + b_L, a_L = sin(w z_L), y = a_L Wout^T + bout (serial epilogue)
+            constexpr int GL = (LH - 1) & 1;
+#pragma unroll
+            for (int rb = 0; rb < NB; ++rb) {
+                const int nb = 16 * rb + 4 * cx.g;
+                const f32x4 z = st.acc[GL][rb] + *(const f32x4*)(sm + SM_BIAS + LH * H + nb);
+                f32x4 sn;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float a, cc;
+                    sincos_fast(w * z[r], a, cc);
+                    sn[r] = a;
+                }
+#pragma unroll
+                for (int j = 0; j < MAXO; ++j) {
+                    if (j < o) {
+                        const f32x4 wj = *(const f32x4*)(sm + SM_WO + j * H + nb);
+                        st.yp[j] += wj[0] * sn[0] + wj[1] * sn[1] + wj[2] * sn[2] + wj[3] * sn[3];
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < MAXO; ++j) {
+                if (j < o) {
+                    const float yj = sum_groups(st.yp[j]) + sm[SM_BOUT + j];
+                    if (valid && cx.g == 0) y[coord * o + j] = yj;
+                }
+            }
+        } else {
+            // y (reduced over the 4 lane groups)
+#pragma unroll
+            for (int j = 0; j < MAXO; ++j) {
+                if (j < o) {
+                    const float yj = sum_groups(st.yp[j]) + sm[SM_BOUT + j];
+                    if (y != nullptr && valid && cx.g == 0) y[coord * o + j] = yj;
+                }
+            }
+            // delta_0 = u_0 . cos(w0 z_0) . w0 ;  gx = delta_0 W0
+            constexpr int GL = (2 * LH - 1) & 1;
+#pragma unroll
+            for (int rb = 0; rb < NB; ++rb) st.act[rb] = (st.acc[GL][rb] * st.C[0][rb]) * w0;
+            if constexpr (STORE) store_tile(cx.dbuf, st.act);
+#pragma unroll
+            for (int k = 0; k < MAXD; ++k) {
+                if (k < d) {
+                    float q = 0.f;
+#pragma unroll
+                    for (int rb = 0; rb < NB; ++rb) {
+                        const f32x4 wk = *(const f32x4*)(sm + SM_W0 + k * H + 16 * rb + 4 * cx.g);
+                        q += wk[0] * st.act[rb][0] + wk[1] * st.act[rb][1] + wk[2] * st.act[rb][2] +
+                             wk[3] * st.act[rb][3];
+                    }
+                    q = sum_groups(q);
+                    if (valid && cx.g == 0) gx[coord * d + k] = q;
+                }
+            }
         }
     }
 }
