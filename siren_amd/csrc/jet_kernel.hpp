@@ -8,7 +8,7 @@
 // the epilogue with the quad's values exchanged by DPP. The weight gradient of layer l is then
 //   dW_l = sum over all 16 columns of zb_l (jet of the layer-l pre-activation cotangent) x a_{l-1} (jet)
 // i.e. wgrad_kernel over K = 4 N columns (bias: value columns only), and the first / output layers are reduced
-// by small_jet_kernel:
+// by edge_kernel<EDGE_JET> (train_kernels.hpp):
 //   dW_0[:, k] = sum zb_0,value x_k + zb_0,tangent k     db_0 = sum zb_0,value     (z_0 = W0 x + b0, dz_0/dx_k = W0[:, k])
 //   dWout[j]   = sum glap a_L,second                                               (lap = sum_j Wout_j a_L,second)
 //   gx         = W0^T zb_0,value
@@ -143,46 +143,6 @@ __global__ __launch_bounds__(THREADS, 1) void jet_store_kernel(
             if (valid && g == 0 && js == 0) gx[coord * d + k] = q;
         }
     }
-}
-
-// grid (S): first- and output-layer gradients of the jet backward; thread t owns neuron t. Tiles are 16 columns
-// (4 coordinates x 4 streams), T = n_pad / 4 of them.
-__global__ __launch_bounds__(THREADS) void small_jet_kernel(const float* __restrict__ abuf,
-                                                            const float* __restrict__ dbuf,
-                                                            const float* __restrict__ x,
-                                                            const float* __restrict__ glap, int64_t n,
-                                                            int64_t n_pad, int64_t tps, float* __restrict__ partial,
-                                                            int64_t P, int d, int o, int lh) {
-    const ParamOffsets off(d, o, lh);
-    const int s = blockIdx.x, t = threadIdx.x;
-    const int64_t T = n_pad / 4;
-    const int64_t t0 = (int64_t)s * tps, t1 = t0 + tps < T ? t0 + tps : T;
-    const float* z0 = dbuf;                                    // zb_0 jet
-    const float* aL = abuf + (int64_t)lh * 4 * n_pad * H;      // a_L jet
-    float gw0[MAXD] = {0.f, 0.f, 0.f, 0.f}, gb0 = 0.f, gwo = 0.f;
-    for (int64_t tile = t0; tile < t1; ++tile) {
-        const f32x4* zrow = (const f32x4*)(z0 + tile * (H * 16) + t * 16);
-        const f32x4* arow = (const f32x4*)(aL + tile * (H * 16) + t * 16);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {  // column group q = coordinate tile*4 + q, streams in the f32x4
-            const int64_t cd = tile * 4 + q;
-            if (cd < n) {
-                const f32x4 zv = zrow[q], av = arow[q];
-                gb0 += zv[0];
-#pragma unroll
-                for (int k = 0; k < MAXD; ++k)
-                    if (k < d) gw0[k] += zv[0] * x[cd * d + k] + (k < 2 ? zv[k + 1] : 0.f);
-                gwo += glap[cd] * av[3];
-            }
-        }
-    }
-    float* out = partial + (int64_t)s * P;
-#pragma unroll
-    for (int k = 0; k < MAXD; ++k)
-        if (k < d) out[off.w0 + (int64_t)t * d + k] = gw0[k];
-    out[off.b0 + t] = gb0;
-    for (int j = 0; j < o; ++j) out[off.wout + (int64_t)j * H + t] = gwo;
-    if (t < o) out[off.bout + t] = 0.f;
 }
 
 }  // namespace siren

@@ -39,7 +39,7 @@ void launch_small_jet(dim3 grid, hipStream_t st, const float* abuf, const float*
                       int o, int lh);
 // tu_wide.hip: hidden width 512 (mode as siren_common.h MODE_*); spill = cos scratch for MODE_W1 / MODE_STORE
 void launch_wide(int mode, dim3 grid, hipStream_t st, const FusedArgs& a, float* spill);
-// tu_w3.hip
+// tu_w3.hip (launch_small_w3 lives in tu_train.hip with the other edge-layer reductions)
 void launch_w3(bool theta, dim3 grid, hipStream_t st, const float* ws, const float* x, const float* v, int64_t n,
                float* gx, float* spill, float* A, float* At, float* D, float* Dt, int64_t n_pad, int d, int lh,
                float w0, float w);

@@ -76,6 +76,14 @@ int64_t param_count(const siren_cfg* cfg) {
     return H * cfg->d_in + H + (int64_t)cfg->n_hidden * (H * H + H) + (int64_t)cfg->d_out * H + cfg->d_out;
 }
 
+// Split-K factor of the weight-gradient kernel: its grid is (S, L, (H/256)^2) workgroups at one per CU, so S is
+// chosen to fill two whole rounds of the 256 CUs (a grid of 513 would run a third round for one workgroup).
+int64_t wgrad_splits(const siren_cfg* cfg) {
+    const int64_t per_split = (int64_t)cfg->n_hidden * (cfg->hidden / 256) * (cfg->hidden / 256);
+    const int64_t s = 512 / per_split;
+    return s > 0 ? s : 1;
+}
+
 // W2 backward workspace: sin activations and deltas of every sine layer in 16-coordinate tiles, S
 // param-shaped partial slabs of the split-K weight-gradient reduction and, for hidden 512, the cos scratch
 // of the wide kernel (layers 0..L-1).
@@ -84,7 +92,7 @@ struct TrainPlan {
     TrainPlan(const siren_cfg* cfg, int64_t n) {
         n_pad = (n + siren::TILE - 1) / siren::TILE * siren::TILE;
         tiles = n_pad / 16;
-        const int64_t want = (512 + cfg->n_hidden - 1) / cfg->n_hidden;  // ~512 wgrad workgroups in total
+        const int64_t want = wgrad_splits(cfg);
         splits = tiles < want ? tiles : want;
         if (splits < 1) splits = 1;
         tps = (tiles + splits - 1) / splits;
@@ -260,7 +268,7 @@ struct JetPlan {
         n_pad = (n + 15) / 16 * 16;
         cols = 4 * n_pad;
         tiles = cols / 16;
-        const int64_t want = (512 + cfg->n_hidden - 1) / cfg->n_hidden;
+        const int64_t want = wgrad_splits(cfg);
         splits = tiles < want ? tiles : want;
         if (splits < 1) splits = 1;
         tps = (tiles + splits - 1) / splits;

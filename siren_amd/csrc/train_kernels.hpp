@@ -109,54 +109,108 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
     if (qc == 0) out[off.b(l) + 256 * qr + threadIdx.x] = with_bias ? bsum : 0.f;
 }
 
-// grid (S): first-layer weight/bias grads from (delta_0, x) and output-layer grads from (gy, a_LH).
-// Thread t owns neurons t, t + 256, ... (< h).
-__global__ __launch_bounds__(THREADS) void small_kernel(const float* __restrict__ abuf, const float* __restrict__ dbuf,
-                                                        const float* __restrict__ x, const float* __restrict__ gy,
-                                                        int64_t n, int64_t n_pad, int64_t tps,
-                                                        float* __restrict__ partial, int64_t P, int d, int o,
-                                                        int lh, int h) {
+// ---- first / output layer gradients ("edge" layers: K = d_in or d_out, VALU) ------------------------------------
+// grid (S): block s reduces the coordinate tiles of split s (the same split as wgrad_kernel); thread t owns
+// neurons t, t + 256, ... The per-column scalars of a chunk of 16 tiles (x, gy / v / glap) are staged in LDS and
+// read as broadcasts; the tile loop is unrolled so each thread keeps several 64 B row loads in flight (the first
+// version walked one tile at a time and was latency-bound at 7x its HBM time).
+//   EDGE_W2 : rows delta_0, a_L:            dW0 = delta_0^T x, db0 = sum delta_0, dWout = gy^T a_L, dbout = sum gy
+//   EDGE_W3 : rows zb_0, zdb_0, adot_L:     dW0 = zdb_0^T v + zb_0^T x, db0 = sum zb_0, dWout = sum adot_L, dbout = 0
+//   EDGE_JET: rows zb_0 jet, a_L jet (16 columns = 4 coordinates x 4 streams, scalars per coordinate):
+//             dW0[:, k] = sum zb_0,value x_k + zb_0,tangent k, db0 = sum zb_0,value, dWout = sum glap a_L,second
+enum { EDGE_W2 = 0, EDGE_W3 = 1, EDGE_JET = 2 };
+constexpr int EDGE_CHUNK = 16;  // tiles per LDS staging chunk
+
+template <int KIND>
+__global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__ r0, const float* __restrict__ r1,
+                                                       const float* __restrict__ r2, const float* __restrict__ x,
+                                                       const float* __restrict__ sc, int64_t n, int64_t ntiles,
+                                                       int64_t tps, float* __restrict__ partial, int64_t P, int d,
+                                                       int o, int lh, int h) {
+    // per-column scalars of one chunk: [col][0..3] = x (d_in <= 4), [col][4..7] = gy / v / glap
+    constexpr int CPT = KIND == EDGE_JET ? 4 : 16;  // coordinates per tile
+    __shared__ __attribute__((aligned(16))) float scal[EDGE_CHUNK * CPT][8];
     const ParamOffsets off(d, o, lh, h);
     const int s = blockIdx.x;
-    const int64_t T = n_pad / 16;
-    const int64_t t0 = (int64_t)s * tps, t1 = t0 + tps < T ? t0 + tps : T;
+    const int64_t t0 = (int64_t)s * tps, t1 = t0 + tps < ntiles ? t0 + tps : ntiles;
     const int64_t tstride = (int64_t)h * 16;
-    const float* d0 = dbuf;                               // delta_0
-    const float* aL = abuf + (int64_t)lh * n_pad * h;     // a_LH
+    const int ns = KIND == EDGE_W2 ? o : (KIND == EDGE_W3 ? d : 1);  // scalars per coordinate besides x
     float* out = partial + (int64_t)s * P;
-    for (int t = threadIdx.x; t < h; t += THREADS) {
+    for (int tb = 0; tb < h; tb += THREADS) {
+        const int t = tb + threadIdx.x;
         float gw0[MAXD] = {0.f, 0.f, 0.f, 0.f}, gb0 = 0.f;
         float gwo[MAXO] = {0.f, 0.f, 0.f, 0.f}, gbo = 0.f;
-        for (int64_t tile = t0; tile < t1; ++tile) {
-            const f32x4* drow = (const f32x4*)(d0 + tile * tstride + t * 16);
-            const f32x4* arow = (const f32x4*)(aL + tile * tstride + t * 16);
+        for (int64_t c0 = t0; c0 < t1; c0 += EDGE_CHUNK) {
+            const int nt = (int)(t1 - c0 < EDGE_CHUNK ? t1 - c0 : EDGE_CHUNK);
+            __syncthreads();
+            for (int e = threadIdx.x; e < EDGE_CHUNK * CPT; e += THREADS) {
+                const int64_t cd = c0 * CPT + e;
+                const bool ok = e < nt * CPT && cd < n;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const f32x4 dv = drow[q], av = arow[q];
+                for (int k = 0; k < MAXD; ++k) scal[e][k] = (ok && k < d) ? x[cd * d + k] : 0.f;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int64_t c = tile * 16 + 4 * q + r;
-                    if (c < n) {
-                        gb0 += dv[r];
+                for (int j = 0; j < 4; ++j) scal[e][4 + j] = (ok && j < ns) ? sc[cd * ns + j] : 0.f;
+            }
+            __syncthreads();
+            if (t < h) {
+#pragma unroll 2
+                for (int i = 0; i < nt; ++i) {
+                    const int64_t tile = c0 + i;
+                    const f32x4* a = (const f32x4*)(r0 + tile * tstride + t * 16);
+                    const f32x4* b = (const f32x4*)(r1 + tile * tstride + t * 16);
+                    f32x4 av[4], bv[4], cv[4];
 #pragma unroll
-                        for (int k = 0; k < MAXD; ++k)
-                            if (k < d) gw0[k] += dv[r] * x[c * d + k];
+                    for (int q = 0; q < 4; ++q) {
+                        av[q] = a[q];
+                        bv[q] = b[q];
+                        if (KIND == EDGE_W3) cv[q] = ((const f32x4*)(r2 + tile * tstride + t * 16))[q];
+                    }
 #pragma unroll
-                        for (int j = 0; j < MAXO; ++j)
-                            if (j < o) gwo[j] += gy[c * o + j] * av[r];
-                        if (t < o) gbo += gy[c * o + t];
+                    for (int q = 0; q < 4; ++q) {
+                        if constexpr (KIND == EDGE_JET) {
+                            // columns 4q..4q+3 = coordinate q of the tile, streams (value, d/dx1, d/dx2, second)
+                            const float* sv = scal[i * 4 + q];
+                            gb0 += av[q][0];
+                            gw0[0] += av[q][0] * sv[0] + av[q][1];
+                            gw0[1] += av[q][0] * sv[1] + av[q][2];
+                            gwo[0] += sv[4] * bv[q][3];
+                        } else {
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const float* sv = scal[i * 16 + 4 * q + r];
+                                gb0 += av[q][r];
+                                if constexpr (KIND == EDGE_W2) {
+#pragma unroll
+                                    for (int k = 0; k < MAXD; ++k) gw0[k] += av[q][r] * sv[k];
+#pragma unroll
+                                    for (int j = 0; j < MAXO; ++j) gwo[j] += sv[4 + j] * bv[q][r];
+                                    gbo += t < MAXO ? sv[4 + (t & 3)] : 0.f;
+                                } else {
+#pragma unroll
+                                    for (int k = 0; k < MAXD; ++k) gw0[k] += cv[q][r] * sv[4 + k] + av[q][r] * sv[k];
+                                    gwo[0] += bv[q][r];
+                                }
+                            }
+                        }
                     }
                 }
             }
         }
+        if (t < h) {
 #pragma unroll
-        for (int k = 0; k < MAXD; ++k)
-            if (k < d) out[off.w0 + (int64_t)t * d + k] = gw0[k];
-        out[off.b0 + t] = gb0;
+            for (int k = 0; k < MAXD; ++k)
+                if (k < d) out[off.w0 + (int64_t)t * d + k] = gw0[k];
+            out[off.b0 + t] = gb0;
+            if constexpr (KIND == EDGE_W2) {
 #pragma unroll
-        for (int j = 0; j < MAXO; ++j)
-            if (j < o) out[off.wout + (int64_t)j * h + t] = gwo[j];
-        if (t < o) out[off.bout + t] = gbo;
+                for (int j = 0; j < MAXO; ++j)
+                    if (j < o) out[off.wout + (int64_t)j * h + t] = gwo[j];
+                if (t < o) out[off.bout + t] = gbo;
+            } else {
+                for (int j = 0; j < o; ++j) out[off.wout + (int64_t)j * h + t] = gwo[0];
+                if (t < o) out[off.bout + t] = 0.f;
+            }
+        }
     }
 }
 

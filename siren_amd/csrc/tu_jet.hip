@@ -11,11 +11,5 @@ void launch_jet_store(dim3 grid, hipStream_t st, const float* ws, const float* x
                        dbuf, n_pad);
 }
 
-void launch_small_jet(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x,
-                      const float* glap, int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d,
-                      int o, int lh) {
-    hipLaunchKernelGGL(small_jet_kernel, grid, dim3(THREADS), 0, st, abuf, dbuf, x, glap, n, n_pad, tps, partial, P,
-                       d, o, lh);
-}
 
 }  // namespace siren

@@ -27,11 +27,5 @@ void launch_w3(bool theta, dim3 grid, hipStream_t st, const float* ws, const flo
 #undef SIREN_L
 }
 
-void launch_small_w3(dim3 grid, hipStream_t st, const float* At, const float* D, const float* Dt, const float* x,
-                     const float* v, int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d, int o,
-                     int lh) {
-    hipLaunchKernelGGL(small_w3_kernel, grid, dim3(THREADS), 0, st, At, D, Dt, x, v, n, n_pad, tps, partial, P, d, o,
-                       lh);
-}
 
 }  // namespace siren

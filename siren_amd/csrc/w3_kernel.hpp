@@ -213,46 +213,4 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
     }
 }
 
-// First/last-layer gradients of the W3 objective: dW0 = zdb_0 v^T + zb_0 x^T, db0 = sum zb_0,
-// dWout[0] = sum ad_L, dbout = 0. Grid (S): block s reduces tiles [s*tps, (s+1)*tps).
-__global__ __launch_bounds__(THREADS) void small_w3_kernel(const float* __restrict__ At, const float* __restrict__ D,
-                                                           const float* __restrict__ Dt, const float* __restrict__ x,
-                                                           const float* __restrict__ v, int64_t n, int64_t n_pad,
-                                                           int64_t tps, float* __restrict__ partial, int64_t P, int d,
-                                                           int o, int lh) {
-    const ParamOffsets off(d, o, lh);
-    const int s = blockIdx.x, t = threadIdx.x;
-    const int64_t T = n_pad / 16;
-    const int64_t t0 = (int64_t)s * tps, t1 = t0 + tps < T ? t0 + tps : T;
-    const float* atL = At + (int64_t)lh * n_pad * H;
-    float gw0[MAXD] = {0.f, 0.f, 0.f, 0.f}, gb0 = 0.f, gwo = 0.f;
-    for (int64_t tile = t0; tile < t1; ++tile) {
-        const f32x4* drow = (const f32x4*)(D + tile * (H * 16) + t * 16);
-        const f32x4* dtrow = (const f32x4*)(Dt + tile * (H * 16) + t * 16);
-        const f32x4* arow = (const f32x4*)(atL + tile * (H * 16) + t * 16);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const f32x4 dv = drow[q], dtv = dtrow[q], av = arow[q];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t cc = tile * 16 + 4 * q + r;
-                if (cc < n) {
-                    gb0 += dv[r];
-                    gwo += av[r];
-#pragma unroll
-                    for (int k = 0; k < MAXD; ++k)
-                        if (k < d) gw0[k] += dtv[r] * v[cc * d + k] + dv[r] * x[cc * d + k];
-                }
-            }
-        }
-    }
-    float* out = partial + (int64_t)s * P;
-#pragma unroll
-    for (int k = 0; k < MAXD; ++k)
-        if (k < d) out[off.w0 + (int64_t)t * d + k] = gw0[k];
-    out[off.b0 + t] = gb0;
-    out[off.wout + t] = gwo;
-    if (t == 0) out[off.bout] = 0.f;
-}
-
 }  // namespace siren
