@@ -22,7 +22,33 @@
 
 namespace siren {
 
-__global__ __launch_bounds__(THREADS, 1) void jet_store_kernel(
+// Tile / scratch accessors that step their pointer through an opaque register: the compiler would otherwise
+// hoist one 64-bit address per 16-neuron block (the offsets exceed the 12-bit immediate) and run out of VGPRs
+// at 2 waves per SIMD.
+__device__ __forceinline__ void jstore_tile(float* p, const f32x4 (&v)[NB]) {
+#pragma unroll
+    for (int rb = 0; rb < NB; ++rb) {
+        store_block(p, 0, v[rb]);
+        p += 256;
+        asm volatile("" : "+v"(p));
+    }
+}
+struct LaneBlocks {  // lane-major scratch: block rb of this lane at p + rb * 256
+    float* p;
+    __device__ __forceinline__ f32x4 next_load() {
+        const f32x4 v = *(const f32x4*)p;
+        p += 256;
+        asm volatile("" : "+v"(p));
+        return v;
+    }
+    __device__ __forceinline__ void next_store(const f32x4& v) {
+        *(f32x4*)p = v;
+        p += 256;
+        asm volatile("" : "+v"(p));
+    }
+};
+
+__global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
     const float* __restrict__ ws, const float* __restrict__ x, int64_t n, const float* __restrict__ glap,
     float* __restrict__ gx, int d, int o, int lh, float w0, float w, float* __restrict__ spill,
     float* __restrict__ abuf, float* __restrict__ dbuf, int64_t n_pad) {
@@ -60,17 +86,20 @@ __global__ __launch_bounds__(THREADS, 1) void jet_store_kernel(
 
     // ---- first layer: z_0 jet (VALU, K = d_in) ---------------------------------------------------------------
     f32x4 act[NB], acc[NB];
+    {
+        LaneBlocks zs{sp};
 #pragma unroll
-    for (int rb = 0; rb < NB; ++rb) {
-        const int nb = 16 * rb + 4 * g;
-        f32x4 z = val * *(const f32x4*)(sm + SM_BIAS + nb);
+        for (int rb = 0; rb < NB; ++rb) {
+            const int nb = 16 * rb + 4 * g;
+            f32x4 z = val * *(const f32x4*)(sm + SM_BIAS + nb);
 #pragma unroll
-        for (int k = 0; k < MAXD; ++k)
-            if (k < d) z += jcf[k] * *(const f32x4*)(sm + SM_W0 + k * H + nb);
-        *(f32x4*)(sp + rb * 256) = z;
-        act[rb] = jet_sin(z, w0, val, kb0, kg0);
+            for (int k = 0; k < MAXD; ++k)
+                if (k < d) z += jcf[k] * *(const f32x4*)(sm + SM_W0 + k * H + nb);
+            zs.next_store(z);
+            act[rb] = jet_sin(z, w0, val, kb0, kg0);
+        }
     }
-    store_tile(abuf + toff, act);
+    jstore_tile(abuf + toff, act);
 
     int s = 0;
 #pragma unroll 1
@@ -100,32 +129,35 @@ __global__ __launch_bounds__(THREADS, 1) void jet_store_kernel(
             const int l = p + 1;
             const float* bl = sm + SM_BIAS + l * H + 4 * g;
             float* zp = sp + (int64_t)l * lstride;
+            LaneBlocks zs{zp};
 #pragma unroll
             for (int rb = 0; rb < NB; ++rb) {
                 const f32x4 z = acc[rb] + val * *(const f32x4*)(bl + 16 * rb);
-                *(f32x4*)(zp + rb * 256) = z;
+                zs.next_store(z);
                 act[rb] = jet_sin(z, w, val, kb, kg);
             }
-            store_tile(abuf + (int64_t)l * lstride + toff, act);
+            jstore_tile(abuf + (int64_t)l * lstride + toff, act);
             if (l == lh) {
                 // seed: u_L (cotangent of the a_L jet) = (sum_j Wout_j) glap on the second-order stream only,
                 // then zb_L = adjoint of the last sine layer
+                LaneBlocks zl{zp};
 #pragma unroll
                 for (int rb = 0; rb < NB; ++rb) {
                     const f32x4 u = gl * *(const f32x4*)(sm + SM_SEED + 16 * rb + 4 * g);
-                    const f32x4 z = *(const f32x4*)(zp + rb * 256);
-                    act[rb] = jet_sin_adjoint(u, z, w, val, m12);
-                }
-                store_tile(dbuf + (int64_t)lh * lstride + toff, act);
+                    act[rb] = jet_sin_adjoint(u, zl.next_load(), w, val, m12);
+                    }
+                jstore_tile(dbuf + (int64_t)lh * lstride + toff, act);
             }
         } else {
             // reverse through W_l (l = 2L - p): acc = u_{l-1}, zb_{l-1} = adjoint of sine layer l-1
             const int lm = 2 * lh - p - 1;
-            const float* zp = sp + (int64_t)lm * lstride;
+            LaneBlocks zl{sp + (int64_t)lm * lstride};
             const float wl = lm == 0 ? w0 : w;
 #pragma unroll
-            for (int rb = 0; rb < NB; ++rb) act[rb] = jet_sin_adjoint(acc[rb], *(const f32x4*)(zp + rb * 256), wl, val, m12);
-            store_tile(dbuf + (int64_t)lm * lstride + toff, act);
+            for (int rb = 0; rb < NB; ++rb) {
+                act[rb] = jet_sin_adjoint(acc[rb], zl.next_load(), wl, val, m12);
+            }
+            jstore_tile(dbuf + (int64_t)lm * lstride + toff, act);
         }
     }
 
