@@ -86,7 +86,7 @@ def kernel_roofline(eng, ws, x, reps=10):
     return ms, achieved
 
 
-HEADLINE_KERNEL = 'w1_kernel<3,false>'   # kernel name as tools/pmc_summary.py shortens it
+HEADLINE_KERNEL = 'w1_kernel<3,0>'   # kernel name as tools/pmc_summary.py shortens it
 
 
 def pmc_traffic(n):
