@@ -144,6 +144,14 @@ int32_t siren_second_order_ws_floats(const siren_cfg* cfg, int64_t n, int32_t wa
 int32_t siren_second_order(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
                            float* tws, float* gx, float* gparams, void* stream);
 
+/* W3 with a first-order seed: the gradient of sum_c gy_c y_c + <v_c, J(x_c)> in ONE sweep (gy (n) nullable; NULL is
+ * siren_second_order). This is the backward autograd runs when a loss uses both the value and the gradient of the
+ * network (loss_functions.py:214-238 sdf: sdf/inter terms on model_out, normal/eikonal terms on gradient()), which
+ * the reference evaluates as two separate backward sweeps through training.py:96. Same workspace as
+ * siren_second_order. */
+int32_t siren_second_order_seeded(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
+                                  const float* gy, float* tws, float* gx, float* gparams, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

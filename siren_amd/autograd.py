@@ -4,21 +4,25 @@ The reference never calls its model's derivatives directly: losses call torch.au
 model_in, ones, create_graph=True) (diff_operators.py:42, :35) and training calls train_loss.backward()
 (training.py:96). So the fused kernels sit behind torch.autograd.Function nodes:
 
-  SirenFunction      y = Phi(x; theta)                        forward: W0 kernel, or the W1 kernel in "jet"
-                                                              mode (y and dPhi/dx in ONE launch, d_out == 1)
-    .backward(gy)    no create_graph: gx via the W1 kernel (or gy*J from jet mode), (gx, gtheta) via the
-                     W2 pipeline (fused reverse sweep + split-K MFMA weight-gradient + slab reduction)
-                     create_graph:    differentiable gx through SirenJacobian / SirenVJP nodes
-  SirenJacobian      J (jet-mode dPhi/dx, already computed by the forward launch) as a graph node
+  SirenFunction      y = Phi(x; theta)                        forward: W0 kernel
+    .backward(gy)    no create_graph: gx via the W1 kernel, (gx, gtheta) via the W2 pipeline (fused reverse
+                     sweep + split-K MFMA weight-gradient + slab reduction)
+                     create_graph:    differentiable gx through a SirenVJP node
+  SirenJetFunction   (y, J = dPhi/dx) from ONE W1 launch as ONE two-output node ("jet" mode, d_out == 1); its
+    .backward(gy, gJ) gets the value and gradient cotangents together: the seeded W3 kernel returns the gradient
+                     of sum gy*y + <gJ, J> in one sweep (sdf training); create_graph: gy*J + SirenHVP(gJ)
   SirenVJP           gx = J^T gy computed by the W1 kernel as a graph node
+  SirenLaplace       the fused Laplacian (W4 jet kernel) and its W4s backward
 
 Which gradients autograd actually wants is read from the engine (torch._C._will_engine_execute_node on the
 next nodes), because ctx.needs_input_grad is static: autograd.grad(y, [x]) must not pay for weight gradients.
 
-Second-order adjoints (SirenJacobian/SirenVJP.backward: gradients_mse / sdf training, the Laplacian's
-Hessian-vector products) run on the W3 kernel (siren_second_order) for hidden 256 and d_out == 1.
-Third-order adjoints (SirenHVP.backward: laplace_mse training, W4s), second order at hidden 512 and vector
-outputs under create_graph are recomputed through siren_amd._torch_path on the device.
+Second-order adjoints (SirenJetFunction/SirenVJP.backward: gradients_mse / sdf training, the Laplacian's
+Hessian-vector products) run on the W3 kernel (siren_second_order[_seeded]) for hidden 256 and
+d_out == 1. laplace_mse training runs the W4s kernels (SirenLaplace). Only derivatives the reference's losses never
+take through our nodes — theta-gradients under create_graph (meta-learning), third order through a SirenHVP node
+built by an unfused divergence(), second order at hidden 512 and vector outputs — are recomputed through
+siren_amd._torch_path with device torch ops.
 """
 import torch
 
@@ -55,21 +59,15 @@ class SirenFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, engine, jet, x, flat):
         ws = engine.pack(flat)
-        J = None
-        use_jet = (jet is not None and jet.active and engine.cfg.d_out == 1 and engine.grad_supported
-                   and x.requires_grad)
-        if use_jet:
-            y, J = engine.forward_grad(ws, x)
-        else:
-            y = engine.forward(ws, x)
-        ctx.engine, ctx.jet, ctx.ws, ctx.J = engine, jet, ws, J
+        y = engine.forward(ws, x)
+        ctx.engine, ctx.jet, ctx.ws = engine, jet, ws
         ctx.save_for_backward(x, flat)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, flat = ctx.saved_tensors
-        engine, ws, J = ctx.engine, ctx.ws, ctx.J
+        engine, ws = ctx.engine, ctx.ws
         need_x = ctx.needs_input_grad[2] and _will_execute(ctx, 0)
         need_p = ctx.needs_input_grad[3] and _will_execute(ctx, 1)
         gx = gp = None
@@ -80,54 +78,80 @@ class SirenFunction(torch.autograd.Function):
                 if not need_x:
                     gx = None
             elif need_x:
-                if J is not None:
-                    gx = gy * J
-                else:
-                    _, gx = engine.forward_grad(ws, x, gy, want_y=False)
+                _, gx = engine.forward_grad(ws, x, gy, want_y=False)
             return None, None, gx, gp
         # create_graph=True: results must be differentiable functions of (x, theta, gy)
         if need_x:
             if ctx.jet is not None and not need_p:
                 ctx.jet.observe_x_gradient_request()
-            if J is not None:
-                gx = gy * SirenJacobian.apply(engine, [J], x, flat, ws)
-            else:
-                gx = SirenVJP.apply(engine, ws, x, flat, gy)
+            gx = SirenVJP.apply(engine, ws, x, flat, gy)
         if need_p:
             gp = _torch_path.vjp_params(engine.cfg, x, flat, gy, create_graph=True)
         return None, None, gx, gp
 
 
-class SirenJacobian(torch.autograd.Function):
-    """J(x; theta) = dPhi/dx (d_out == 1) as a graph node; the value comes from the jet-mode forward launch.
+class SirenJetFunction(torch.autograd.Function):
+    """(y, J) = (Phi(x; theta), dPhi/dx) for d_out == 1 from ONE W1 launch, as ONE graph node with two outputs.
 
-    backward(gJ) is the second-order adjoint: (H gJ, d/dtheta <gJ, J>) from the W3 kernel
-    (siren_second_order). Under create_graph (laplace/divergence, third-order losses) the Hessian-vector product
-    becomes a SirenHVP node whose forward is the same kernel."""
+    The module returns y; J stays an output of the node and is what diff_operators.gradient's create_graph
+    backward hands out (gx = gy * J). Because y and J belong to the same node, a loss that uses both the value and
+    the gradient (sdf: loss_functions.py:214-238) reaches this node's backward ONCE with (gy, gJ), and the seeded
+    W3 kernel returns the gradient of sum gy*y + <gJ, J> in a single sweep (siren_second_order_seeded) instead of
+    the reference's two separate backward passes (a first-order one for the value terms and a second-order one
+    for the gradient terms)."""
 
     @staticmethod
-    def forward(ctx, engine, holder, x, flat, ws):
+    def forward(ctx, engine, x, flat):
+        ws = engine.pack(flat)
+        y, J = engine.forward_grad(ws, x)
         ctx.engine, ctx.ws = engine, ws
-        ctx.save_for_backward(x, flat)
-        return holder[0].clone()  # a fresh output tensor per node (J may feed several gradient() calls)
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(x, flat, J)
+        return y, J
 
     @staticmethod
-    def backward(ctx, gJ):
-        x, flat = ctx.saved_tensors
-        need_x = ctx.needs_input_grad[2] and _will_execute(ctx, 0)
-        need_p = ctx.needs_input_grad[3] and _will_execute(ctx, 1)
-        gJ = gJ.contiguous()
-        if not ctx.engine.second_order_supported:  # hidden 512: no W3 kernel yet (DESIGN.md §7)
-            gx, gp = _torch_path.jacobian_vjp(ctx.engine.cfg, x, flat, gJ, create_graph=torch.is_grad_enabled())
-            return None, None, (gx if need_x else None), (gp if need_p else None), None
+    def backward(ctx, gy, gJ):
+        x, flat, J = ctx.saved_tensors
+        engine, ws = ctx.engine, ctx.ws
+        # tensor inputs in order: x (0), flat (1)
+        need_x = ctx.needs_input_grad[1] and _will_execute(ctx, 0)
+        need_p = ctx.needs_input_grad[2] and _will_execute(ctx, 1)
+        if (gy is None and gJ is None) or not (need_x or need_p):
+            return None, None, None
+        gy = gy.contiguous() if gy is not None else None
+        gJ = gJ.contiguous() if gJ is not None else None
+        gx = gp = None
         if not torch.is_grad_enabled():
-            gx, gp = ctx.engine.second_order(ctx.ws, x, gJ, want_theta=need_p)
-            return None, None, (gx if need_x else None), gp, None
-        gx = SirenHVP.apply(ctx.engine, ctx.ws, x, flat, gJ) if need_x else None
-        gp = None
+            if gJ is None:  # first order only
+                if need_p:
+                    gx, gp = engine.backward_params(ws, x, gy)
+                else:
+                    gx = gy * J
+            elif engine.second_order_supported:
+                gx, gp = engine.second_order(ws, x, gJ, want_theta=need_p, gy=gy)
+            else:
+                gx, gp = _torch_path.jacobian_vjp(engine.cfg, x, flat, gJ, create_graph=False)
+                if gy is not None:
+                    gx = gx + gy * J
+                    if need_p:
+                        gp = gp + engine.backward_params(ws, x, gy)[1]
+            return None, (gx if need_x else None), (gp if need_p else None)
+        # create_graph=True: differentiable in (x, theta, gy, gJ); J here is this node's own output 1
+        if need_x:
+            gx = gy * J if gy is not None else None
+            if gJ is not None:
+                if engine.second_order_supported:
+                    h = SirenHVP.apply(engine, ws, x, flat, gJ)
+                else:
+                    h, _ = _torch_path.jacobian_vjp(engine.cfg, x, flat, gJ, create_graph=True)
+                gx = h if gx is None else gx + h
         if need_p:
-            _, gp = _torch_path.jacobian_vjp(ctx.engine.cfg, x, flat, gJ, create_graph=True)
-        return None, None, gx, gp, None
+            if gy is not None:
+                gp = _torch_path.vjp_params(engine.cfg, x, flat, gy, create_graph=True)
+            if gJ is not None:
+                _, gpj = _torch_path.jacobian_vjp(engine.cfg, x, flat, gJ, create_graph=True)
+                gp = gpj if gp is None else gp + gpj
+        return None, gx, gp
 
 
 class SirenHVP(torch.autograd.Function):
@@ -215,18 +239,22 @@ _VIEW_NODES = ('ViewBackward0', 'ReshapeAliasBackward0', 'UnsafeViewBackward0')
 
 
 def siren_node_of(y, x):
-    """The SirenFunction node that produced y (through views only) from a view of x, else None."""
+    """The SirenFunction / SirenJetFunction node that produced y (its value output, through views only) from a view
+    of x, else None."""
     node = getattr(y, 'grad_fn', None)
+    out_nr = getattr(y, 'output_nr', 0)
     for _ in range(4):
         if node is None:
             return None
         name = type(node).__name__
-        if name == 'SirenFunctionBackward':
+        if name in ('SirenFunctionBackward', 'SirenJetFunctionBackward'):
             break
         if name not in _VIEW_NODES:
             return None
-        node = node.next_functions[0][0]
+        node, out_nr = node.next_functions[0]
     else:
+        return None
+    if out_nr != 0:  # the jet node's second output is dPhi/dx, not the network value
         return None
     if not hasattr(node, 'engine') or not hasattr(node, 'ws'):
         return None
@@ -243,6 +271,6 @@ def fused_laplace(y, x):
     node = siren_node_of(y, x)
     if node is None or not node.engine.laplace_supported:
         return None
-    xs, flat = node.saved_tensors
+    xs, flat = node.saved_tensors[:2]
     lap = SirenLaplace.apply(node.engine, node.ws, xs, flat)
     return lap.view(*y.shape[:-1], 1)

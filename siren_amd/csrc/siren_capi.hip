@@ -348,6 +348,11 @@ int32_t siren_second_order_ws_floats(const siren_cfg* cfg, int64_t n, int32_t wa
 
 int32_t siren_second_order(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
                            float* tws, float* gx, float* gparams, void* stream) {
+    return siren_second_order_seeded(cfg, ws, x, n, v, nullptr, tws, gx, gparams, stream);
+}
+
+int32_t siren_second_order_seeded(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
+                                  const float* gy, float* tws, float* gx, float* gparams, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (cfg->n_hidden > siren::MAX_LH_GRAD)
         return fail(SIREN_EUNSUPPORTED, "siren_second_order needs 1 <= num_hidden_layers <= 3");
@@ -372,7 +377,7 @@ int32_t siren_second_order(const siren_cfg* cfg, const float* ws, const float* x
     float* Dt = D + plan.buf_floats;
     float* partial = Dt + plan.buf_floats;
     const dim3 grid((unsigned)(plan.n_pad / siren::TILE));
-    siren::launch_w3(theta, grid, st, ws, x, v, n, gx, spill, A, At, D, Dt, plan.n_pad, cfg->d_in, cfg->n_hidden,
+    siren::launch_w3(theta, grid, st, ws, x, v, gy, n, gx, spill, A, At, D, Dt, plan.n_pad, cfg->d_in, cfg->n_hidden,
                      cfg->omega_first, cfg->omega_hidden);
     if (int rc = hip_status("siren_second_order (w3)")) return rc;
     if (!theta) return SIREN_OK;
@@ -382,8 +387,9 @@ int32_t siren_second_order(const siren_cfg* cfg, const float* ws, const float* x
     siren::launch_wgrad(wgrid, st, At, Dt, plan.n_pad, plan.tps, partial + plan.splits * P, P, cfg->d_in, cfg->d_out,
                         cfg->n_hidden, 0, siren::H);
     if (int rc = hip_status("siren_second_order (wgrad)")) return rc;
-    siren::launch_small_w3(dim3((unsigned)plan.splits), st, At, D, Dt, x, v, n, plan.n_pad, plan.tps, partial, P,
-                           cfg->d_in, cfg->d_out, cfg->n_hidden);
+    const float* a_last = A + (int64_t)cfg->n_hidden * plan.n_pad * siren::H;  // a_L rows (first-order seed)
+    siren::launch_small_w3(dim3((unsigned)plan.splits), st, At, D, Dt, a_last, x, v, gy, n, plan.n_pad, plan.tps,
+                           partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden);
     if (int rc = hip_status("siren_second_order (small)")) return rc;
     const siren::ParamOffsets off(cfg->d_in, cfg->d_out, cfg->n_hidden);
     const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 4096);

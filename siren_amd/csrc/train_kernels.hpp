@@ -116,6 +116,7 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
 // version walked one tile at a time and was latency-bound at 7x its HBM time).
 //   EDGE_W2 : rows delta_0, a_L:            dW0 = delta_0^T x, db0 = sum delta_0, dWout = gy^T a_L, dbout = sum gy
 //   EDGE_W3 : rows zb_0, zdb_0, adot_L:     dW0 = zdb_0^T v + zb_0^T x, db0 = sum zb_0, dWout = sum adot_L, dbout = 0
+//             (+ with a first-order seed gy, rows a_L: dWout += gy^T a_L, dbout = sum gy)
 //   EDGE_JET: rows zb_0 jet, a_L jet (16 columns = 4 coordinates x 4 streams, scalars per coordinate):
 //             dW0[:, k] = sum zb_0,value x_k + zb_0,tangent k, db0 = sum zb_0,value, dWout = sum glap a_L,second
 enum { EDGE_W2 = 0, EDGE_W3 = 1, EDGE_JET = 2 };
@@ -123,13 +124,16 @@ constexpr int EDGE_CHUNK = 16;  // tiles per LDS staging chunk
 
 template <int KIND>
 __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__ r0, const float* __restrict__ r1,
-                                                       const float* __restrict__ r2, const float* __restrict__ x,
-                                                       const float* __restrict__ sc, int64_t n, int64_t ntiles,
+                                                       const float* __restrict__ r2, const float* __restrict__ r3,
+                                                       const float* __restrict__ x, const float* __restrict__ sc,
+                                                       const float* __restrict__ sgy, int64_t n, int64_t ntiles,
                                                        int64_t tps, float* __restrict__ partial, int64_t P, int d,
                                                        int o, int lh, int h) {
-    // per-column scalars of one chunk: [col][0..3] = x (d_in <= 4), [col][4..7] = gy / v / glap
+    // per-column scalars of one chunk: [col][0..3] = x (d_in <= 4), [col][4..7] = gy / v / glap, [col][8] = the
+    // first-order seed gy of a seeded W3 (sgy != nullptr: rows r3 = a_L add sum gy a_L to dWout, sum gy to dbout)
     constexpr int CPT = KIND == EDGE_JET ? 4 : 16;  // coordinates per tile
-    __shared__ __attribute__((aligned(16))) float scal[EDGE_CHUNK * CPT][8];
+    __shared__ __attribute__((aligned(16))) float scal[EDGE_CHUNK * CPT][9];
+    const bool seeded = KIND == EDGE_W3 && sgy != nullptr;
     const ParamOffsets off(d, o, lh, h);
     const int s = blockIdx.x;
     const int64_t t0 = (int64_t)s * tps, t1 = t0 + tps < ntiles ? t0 + tps : ntiles;
@@ -150,6 +154,7 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
                 for (int k = 0; k < MAXD; ++k) scal[e][k] = (ok && k < d) ? x[cd * d + k] : 0.f;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) scal[e][4 + j] = (ok && j < ns) ? sc[cd * ns + j] : 0.f;
+                scal[e][8] = (ok && seeded) ? sgy[cd] : 0.f;
             }
             __syncthreads();
             if (t < h) {
@@ -158,12 +163,13 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
                     const int64_t tile = c0 + i;
                     const f32x4* a = (const f32x4*)(r0 + tile * tstride + t * 16);
                     const f32x4* b = (const f32x4*)(r1 + tile * tstride + t * 16);
-                    f32x4 av[4], bv[4], cv[4];
+                    f32x4 av[4], bv[4], cv[4], ev[4];
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         av[q] = a[q];
                         bv[q] = b[q];
                         if (KIND == EDGE_W3) cv[q] = ((const f32x4*)(r2 + tile * tstride + t * 16))[q];
+                        if (KIND == EDGE_W3) ev[q] = seeded ? ((const f32x4*)(r3 + tile * tstride + t * 16))[q] : f32x4{};
                     }
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
@@ -188,7 +194,8 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
                                 } else {
 #pragma unroll
                                     for (int k = 0; k < MAXD; ++k) gw0[k] += cv[q][r] * sv[4 + k] + av[q][r] * sv[k];
-                                    gwo[0] += bv[q][r];
+                                    gwo[0] += bv[q][r] + sv[8] * ev[q][r];
+                                    gbo += sv[8];
                                 }
                             }
                         }
@@ -208,7 +215,7 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
                 if (t < o) out[off.bout + t] = gbo;
             } else {
                 for (int j = 0; j < o; ++j) out[off.wout + (int64_t)j * h + t] = gwo[0];
-                if (t < o) out[off.bout + t] = 0.f;
+                if (t < o) out[off.bout + t] = KIND == EDGE_W3 ? gbo : 0.f;
             }
         }
     }

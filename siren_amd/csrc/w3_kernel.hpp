@@ -9,12 +9,14 @@
 //   forward (per layer, primal + tangent share every weight A operand: 2 MFMAs per ds_read):
 //       z_l = W_l a_{l-1} + b_l,   zd_l = W_l ad_{l-1}      (z_0 = W0 x + b0, zd_0 = W0 v on VALU)
 //       a_l = sin(w z_l), c_l = cos(w z_l), ad_l = w c_l zd_l
-//   reverse (adjoints ab of a and adb of ad; adb_L = Wout^T, ab_L = 0):
+//   reverse (adjoints ab of a and adb of ad; adb_L = Wout^T, ab_L = gy_c Wout^T):
 //       zdb_l = w c_l adb_l
 //       zb_l  = w c_l ab_l - w^2 a_l zd_l adb_l
 //       adb_{l-1} = W_l^T zdb_l,  ab_{l-1} = W_l^T zb_l,  gx = W0^T zb_0
 //   weight gradients (THETA): dW_l = zdb_l ad_{l-1}^T + zb_l a_{l-1}^T (the split-K wgrad kernel, K = 2N),
-//       db_l = sum zb_l, dW0 = zdb_0 v^T + zb_0 x^T, dWout = sum ad_L, dbout = 0.
+//       db_l = sum zb_l, dW0 = zdb_0 v^T + zb_0 x^T, dWout = sum (ad_L + gy a_L), dbout = sum gy.
+// Optional first-order seed gy (n): the same sweep then returns the gradient of sum_c gy_c y_c + <v_c, J(x_c)>
+// (the sdf loss's value and gradient terms in ONE backward; the first-order adjoint rides in ab, which is linear).
 // (c_l, zd_l, a_l) of every layer go to a per-wave spill area in HBM in the forward sweep and come back in the
 // reverse sweep (coalesced 1 KiB per block; a WG's 768 KiB usually still sits in the 256 MiB Infinity Cache).
 // Same weight stream (packed forward + transposed slices) and 3-slot LDS ring as the W1 kernels.
@@ -66,7 +68,8 @@ __device__ __forceinline__ f32x4* spill_at(float* wave_spill, int l, int q, int 
 
 template <int LH, bool THETA>
 __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict__ ws, const float* __restrict__ x,
-                                                        const float* __restrict__ v, int64_t n, float* __restrict__ gx,
+                                                        const float* __restrict__ v, const float* __restrict__ gy,
+                                                        int64_t n, float* __restrict__ gx,
                                                         float* __restrict__ spill, float* __restrict__ A,
                                                         float* __restrict__ At, float* __restrict__ D,
                                                         float* __restrict__ Dt, int64_t n_pad, int d, float w0,
@@ -165,7 +168,8 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
         }
     }
 
-    // ---- reverse: seed at layer L (adb_L = Wout^T, ab_L = 0) -------------------------------------------------
+    // ---- reverse: seed at layer L (adb_L = Wout^T, ab_L = gy Wout^T; gy = 0 without a first-order seed) -------
+    const float gyv = (gy != nullptr && valid) ? gy[coord] : 0.f;
 #pragma unroll
     for (int rb = 0; rb < NB; ++rb) {
         const f32x4 adb = *(const f32x4*)(sm + SM_SEED + 16 * rb + 4 * g);
@@ -173,7 +177,7 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
         const f32x4 zd = *spill_at(wsp, LH, 1, rb, lane);
         const f32x4 sn = *spill_at(wsp, LH, 2, rb, lane);
         actt[rb] = (w * cs) * adb;
-        actp[rb] = -(w * w) * sn * zd * adb;
+        actp[rb] = (w * cs) * (gyv * adb) - (w * w) * sn * zd * adb;
         if (THETA) {
             store_block(D + LH * lstride + toff, rb, actp[rb]);
             store_block(Dt + LH * lstride + toff, rb, actt[rb]);

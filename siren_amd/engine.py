@@ -180,9 +180,10 @@ class SirenEngine:
                    'siren_backward')
         return gx, gp
 
-    def second_order(self, ws, x, v, want_theta=True):
+    def second_order(self, ws, x, v, want_theta=True, gy=None):
         """W3: (H v, d/dtheta sum <v, dPhi/dx>) for d_out == 1 — the backward of the dPhi/dx graph node
-        (gradients_mse / sdf / divergence). Returns (gx, gparams or None)."""
+        (gradients_mse / sdf / divergence). With a first-order seed gy (n, 1) the same sweep returns the gradient of
+        sum gy*y + <v, dPhi/dx> (siren_second_order_seeded). Returns (gx, gparams or None)."""
         self._require()
         if not self.second_order_supported:
             raise _lib.SirenUnsupported('siren_second_order covers hidden 256, d_out == 1, linear output, '
@@ -192,12 +193,17 @@ class SirenEngine:
         v = v.contiguous()
         if v.shape != x.shape or v.dtype != torch.float32 or v.device != x.device:
             raise ValueError('v must be fp32 %s on %s' % (tuple(x.shape), x.device))
+        if gy is not None:
+            gy = gy.contiguous()
+            if gy.numel() != n or gy.dtype != torch.float32 or gy.device != x.device:
+                raise ValueError('gy must be fp32 with %d values on %s' % (n, x.device))
         cnt = ctypes.c_int64()
         _lib.check(self.lib.siren_second_order_ws_floats(ctypes.byref(self.cfg), n, 1 if want_theta else 0,
                                                          ctypes.byref(cnt)), 'siren_second_order_ws_floats')
         tws = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
         gx = torch.empty(n, self.cfg.d_in, dtype=torch.float32, device=x.device)
         gp = torch.empty(self.param_count, dtype=torch.float32, device=x.device) if want_theta else None
-        _lib.check(self.lib.siren_second_order(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(v), _ptr(tws),
-                                               _ptr(gx), _ptr(gp), _stream(x.device)), 'siren_second_order')
+        _lib.check(self.lib.siren_second_order_seeded(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(v), _ptr(gy),
+                                                      _ptr(tws), _ptr(gx), _ptr(gp), _stream(x.device)),
+                   'siren_second_order_seeded')
         return gx, gp

@@ -27,7 +27,7 @@ import torch
 from torch import nn
 
 from . import _lib
-from .autograd import JetState, SirenFunction
+from .autograd import JetState, SirenFunction, SirenJetFunction
 from .engine import SirenEngine
 
 
@@ -176,7 +176,11 @@ def _fused_apply(engine, jet, coords, weights_biases):
     x2d = coords.reshape(-1, coords.shape[-1])
     if x2d is coords:  # keep a non-leaf edge so the engine can tell which gradients autograd wants
         x2d = coords.view(coords.shape)
-    y = SirenFunction.apply(engine, jet, x2d, flat)
+    if (jet is not None and jet.active and engine.cfg.d_out == 1 and engine.grad_supported
+            and torch.is_grad_enabled() and x2d.requires_grad):
+        y, _ = SirenJetFunction.apply(engine, x2d, flat)  # J stays alive as the node's second output
+    else:
+        y = SirenFunction.apply(engine, jet, x2d, flat)
     return y.view(*lead, y.shape[-1])
 
 

@@ -280,9 +280,18 @@ def test_training_theta_grads_vs_reference(cuda, g1, loss):
     assert out['model_in'].grad is not None or loss != 'image_mse'
 
 
-def test_sdf_losses_vs_reference(cuda, g3, manifest):
-    from siren_amd import loss_functions as Lf
-    m = load_model(g3, cuda, in_features=3)
+@pytest.mark.parametrize('jet', ['auto', True])
+def test_sdf_losses_vs_reference(cuda, g3, manifest, jet, monkeypatch):
+    """sdf training (value + gradient terms). With jet=True the value and gradient cotangents meet in ONE
+    SirenJetFunction backward: the seeded W3 kernel, no first-order W2 pass and no torch recompute."""
+    from siren_amd import loss_functions as Lf, _torch_path
+    from siren_amd.engine import SirenEngine
+    if jet is True:
+        def boom(*a, **k):
+            raise AssertionError('separate first-order pass / torch fallback used on the seeded W3 path')
+        monkeypatch.setattr(SirenEngine, 'backward_params', boom)
+        monkeypatch.setattr(_torch_path, 'jacobian_vjp', boom)
+    m = load_model(g3, cuda, in_features=3, jet=jet)
     out = m({'coords': to_dev(g3['coords'], cuda)})
     terms = Lf.sdf(out, {'sdf': to_dev(g3['gt_sdf'], cuda), 'normals': to_dev(g3['gt_normals'], cuda)})
     for k, v in terms.items():
@@ -365,6 +374,39 @@ def test_w3_second_order_vs_fp64(cuda, n, d, L):
     assert none is None and torch.equal(hv, hv2)
     assert np.max(np.abs(hv.cpu().numpy() - rhv)) <= tol_rel(rhv)
     assert np.max(np.abs(gp.cpu().numpy() - rgp)) <= 1e-4 * np.max(np.abs(rgp))
+
+
+def torch_seeded_ref(x, layers, v, gy):
+    xt = torch.tensor(np.asarray(x), dtype=torch.float64, requires_grad=True)
+    params = [torch.tensor(np.asarray(t), dtype=torch.float64, requires_grad=True) for W, b in layers for t in (W, b)]
+    y = O.torch_forward(xt, params)
+    J = torch.autograd.grad(y, xt, torch.ones_like(y), create_graph=True)[0]
+    F = (J * torch.tensor(np.asarray(v), dtype=torch.float64)).sum() + \
+        (y * torch.tensor(np.asarray(gy), dtype=torch.float64)).sum()
+    grads = torch.autograd.grad(F, [xt] + params)
+    return grads[0].numpy(), torch.cat([g.reshape(-1) for g in grads[1:]]).numpy()
+
+
+@pytest.mark.parametrize('n,d,L', [(1, 3, 3), (4097, 3, 3), (1000, 2, 2), (333, 4, 1)])
+def test_w3_seeded_vs_fp64(cuda, n, d, L):
+    """siren_second_order_seeded: gradient of sum gy*y + <v, J> (the sdf backward) in one sweep."""
+    layers = random_layers(d, L, 1, seed=7 * n + d)
+    eng = engine(d, L, 1)
+    ws = eng.pack(to_dev(O.flatten(layers), cuda))
+    rng = np.random.default_rng(n + 1)
+    x = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    v = rng.normal(size=(n, d)).astype(np.float32)
+    gy = rng.normal(size=(n, 1)).astype(np.float32)
+    gx, gp = eng.second_order(ws, to_dev(x, cuda), to_dev(v, cuda), want_theta=True, gy=to_dev(gy, cuda))
+    gx2, _ = eng.second_order(ws, to_dev(x, cuda), to_dev(v, cuda), want_theta=False, gy=to_dev(gy, cuda))
+    rgx, rgp = torch_seeded_ref(x, layers, v, gy)
+    assert torch.equal(gx, gx2)
+    assert np.max(np.abs(gx.cpu().numpy() - rgx)) <= tol_rel(rgx)
+    assert np.max(np.abs(gp.cpu().numpy() - rgp)) <= 1e-4 * np.max(np.abs(rgp))
+    # a zero seed is exactly the unseeded kernel
+    gx0, gp0 = eng.second_order(ws, to_dev(x, cuda), to_dev(v, cuda), gy=torch.zeros(n, 1, device=cuda))
+    gx1, gp1 = eng.second_order(ws, to_dev(x, cuda), to_dev(v, cuda))
+    assert torch.equal(gx0, gx1) and torch.equal(gp0, gp1)
 
 
 def test_w3_trained_regime(cuda, g2, g1):
