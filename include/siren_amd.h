@@ -152,6 +152,12 @@ int32_t siren_second_order(const siren_cfg* cfg, const float* ws, const float* x
 int32_t siren_second_order_seeded(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
                                   const float* gy, float* tws, float* gx, float* gparams, void* stream);
 
+/* Diagnostics: the W1 kernel (hidden 256, 3 hidden layers) with s_memtime stamps. stamps receives
+ * 256 workgroups x 4 tiles x 4 waves x 8 events (uint64; event 0 tile start, 1..6 after GEMM 0..5, 7 tile end);
+ * unrecorded entries are left untouched. y / gx as siren_forward_grad with gy = ones. */
+int32_t siren_w1_phase_profile(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y, float* gx,
+                               uint64_t* stamps, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -184,6 +184,20 @@ int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x
     return hip_status("siren_forward_grad");
 }
 
+int32_t siren_w1_phase_profile(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y, float* gx,
+                               uint64_t* stamps, void* stream) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (cfg->n_hidden != 3 || wide(cfg) || !cfg->outermost_linear)
+        return fail(SIREN_EUNSUPPORTED, "siren_w1_phase_profile covers the hidden-256, 3-hidden-layer W1 kernel");
+    if (ws == nullptr || x == nullptr || y == nullptr || gx == nullptr || stamps == nullptr || n <= 0)
+        return fail(SIREN_EINVAL, "NULL pointer or n <= 0");
+    const int64_t blocks = (n + siren::TILE - 1) / siren::TILE;
+    siren::FusedArgs fa{ws, x, n, nullptr, y, gx, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first,
+                        cfg->omega_hidden, 0, (float*)stamps, nullptr, blocks * siren::TILE};
+    siren::launch_w1(siren::MODE_W1 | siren::MODE_PROF, tile_grid(cfg, blocks, 1), (hipStream_t)stream, fa);
+    return hip_status("siren_w1_phase_profile");
+}
+
 int32_t siren_forward_laplace(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y, float* gx,
                               float* lap, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;

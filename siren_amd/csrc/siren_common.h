@@ -34,6 +34,10 @@ constexpr int MAX_LH_GRAD = 3;    // max hidden layers of the forward+grad kerne
 // MODE_JET (W4): forward-mode Taylor jet for the Laplacian — 4 coordinates x 4 jet streams (value, d/dx_1,
 // d/dx_2, sum_i d2/dx_i2) in the 16 MFMA columns, y / grad / Laplacian in one forward sweep.
 enum { MODE_W1 = 0, MODE_STORE = 1, MODE_FWD = 2, MODE_JET = 3 };
+// w1_kernel modifier bit (MODE & MODE_BASE is the mode proper): MODE_PROF records per-GEMM s_memtime stamps
+enum { MODE_BASE = 15, MODE_PROF = 64 };
+// MODE_PROF (diagnostics, siren_w1_phase_profile): s_memtime stamps at tile start, after each GEMM and at tile end
+constexpr int PROF_TILES = 4, PROF_EVENTS = 8, PROF_BLOCKS = 256;
 __host__ __device__ constexpr bool forward_only(int mode) { return mode == MODE_FWD || mode == MODE_JET; }
 
 // Small-parameter block (head of the workspace, copied to LDS by every workgroup):
@@ -88,29 +92,20 @@ __device__ __forceinline__ void sincos_phase(float t, float& sn, float& cs) {
     cs = ((qi + 1) & 2) ? -cv : cv;
 }
 
-// Branch-free variant for the MFMA-interleaved epilogues (w1_kernel.hpp): fma Cody-Waite with a
-// full-precision pi/2 (C1 = fp32(pi/2), C2 = fp32(pi/2 - C1)); the product q*C1 is exact inside the fma, so
-// the reduction stays accurate while q is exact (|t| < 1e6 rad measured: <= 1.1e-7 absolute error on sin and
-// cos, vs 3.3e-8 for libm sinf). No data-dependent branch, so the compiler can interleave it with MFMAs.
+// sin/cos for the MFMA kernels' epilogues, via the transcendental unit: Cody-Waite reduction of t by 2 pi
+// (C1 = fp32(2 pi), C2 = 2 pi - C1; q*C1 is exact inside the fma, so r is accurate while q is exact), then
+// v_sin_f32 / v_cos_f32 on revolutions in [-1/2, 1/2]. Branch-free, 5 VALU + 2 transcendental. Max abs error
+// 3.7e-7 on |t| <= 100 (profiles/r01_vsin_accuracy.log; the earlier minimax-polynomial version: 1.1e-7 at ~30 VALU).
+// Why the instruction count matters: an f32 MFMA (v_mfma_f32_16x16x4_f32) shares the SIMD's vector issue with
+// VALU — a filler VALU is never hidden behind it (tools/micro/mfma_valu_overlap: the first costs ~14 cycles, each
+// further ~4.5) — so every epilogue instruction is paid in full: W1 70.1% -> 76.4% of the fp32 MFMA peak.
 __device__ __forceinline__ void sincos_fast(float t, float& sn, float& cs) {
-    const float q = __builtin_rintf(t * 0.636619772367581343f);
-    float r = __builtin_fmaf(-q, 1.57079637050628662109375f, t);
-    r = __builtin_fmaf(-q, -4.37113900018624283e-8f, r);
-    const float r2 = r * r;
-    const float ps = __builtin_fmaf(__builtin_fmaf(-1.9515295891e-4f, r2, 8.3321608736e-3f), r2, -1.6666654611e-1f);
-    const float sr = __builtin_fmaf(ps * r2, r, r);
-    const float pc = __builtin_fmaf(__builtin_fmaf(2.443315711809948e-5f, r2, -1.388731625493765e-3f), r2,
-                                    4.166664568298827e-2f);
-    const float cr = __builtin_fmaf(pc * r2, r2, __builtin_fmaf(-0.5f, r2, 1.0f));
-    // quadrant select and sign flip with integer bit operations (v_bfi / v_xor): no lane masks, so nothing
-    // lands in SGPR pairs when many epilogues are in flight
-    const int qi = (int)q;
-    const int odd = -(qi & 1);  // all ones when the quadrant is odd
-    const int si = __float_as_int(sr), ci = __float_as_int(cr);
-    const int sv = (ci & odd) | (si & ~odd);
-    const int cv = (si & odd) | (ci & ~odd);
-    sn = __int_as_float(sv ^ ((qi & 2) << 30));
-    cs = __int_as_float(cv ^ (((qi + 1) & 2) << 30));
+    const float q = __builtin_rintf(t * 0.159154943091895336f);
+    float r = __builtin_fmaf(-q, 6.28318548202514648f, t);
+    r = __builtin_fmaf(-q, -1.74845553146951e-7f, r);
+    const float u = r * 0.159154943091895336f;
+    sn = __builtin_amdgcn_sinf(u);
+    cs = __builtin_amdgcn_cosf(u);
 }
 
 // ---- forward-mode Taylor jets (MODE_JET, jet_kernel.hpp) ---------------------------------------------------
@@ -135,6 +130,15 @@ __device__ __forceinline__ f32x4 jet_sin(const f32x4& z, float w, float ka, floa
         out[r] = __builtin_fmaf(ka, sn, __builtin_fmaf(kb * cs, z[r], -(kg * sn) * q2));
     }
     return out;
+}
+
+// one element of jet_sin (the MFMA-interleaved epilogues of w1_kernel split a block into its 4 elements)
+__device__ __forceinline__ float jet_sin1(float z, float w, float ka, float kb, float kg) {
+    const float z0 = quad_bcast<0>(z), t1 = quad_bcast<1>(z), t2 = quad_bcast<2>(z);
+    float sn, cs;
+    sincos_fast(w * z0, sn, cs);
+    const float q2 = __builtin_fmaf(t1, t1, t2 * t2);
+    return __builtin_fmaf(ka, sn, __builtin_fmaf(kb * cs, z, -(kg * sn) * q2));
 }
 
 // Adjoint of jet_sin: given this lane's stream of the cotangent u of the output jet and of the input jet z,

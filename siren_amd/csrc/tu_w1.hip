@@ -14,6 +14,8 @@ void launch_w1(int mode, dim3 grid, hipStream_t st, const FusedArgs& a) {
             case 2: SIREN_L(2, MODE_STORE); break;
             default: SIREN_L(3, MODE_STORE); break;
         }
+    } else if (mode == (MODE_W1 | MODE_PROF)) {
+        SIREN_L(3, MODE_W1 | MODE_PROF);
     } else {
         switch (a.lh) {
             case 1: SIREN_L(1, MODE_W1); break;

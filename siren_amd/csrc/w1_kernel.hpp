@@ -94,13 +94,13 @@ __device__ __forceinline__ void lgkm_wait(f32x4& a, f32x4& b) {
 }
 
 template <int MODE>
-constexpr int npasses() { return forward_only(MODE) ? 1 : 2; }
+constexpr int npasses() { return forward_only(MODE & MODE_BASE) ? 1 : 2; }
 
 template <int LH, int MODE>
 struct W1State {
     f32x4 act[NB];     // B operand of the current GEMM (filled one block ahead)
     f32x4 acc[2][NB];  // ping-pong accumulators
-    f32x4 C[forward_only(MODE) ? 1 : LH][NB];  // cos(w z_l), l = 0 .. LH-1 (unused in forward-only modes)
+    f32x4 C[forward_only(MODE & MODE_BASE) ? 1 : LH][NB];  // cos(w z_l), l = 0 .. LH-1 (unused in forward-only modes)
     f32x4 pa0, pa1;    // prefetched first operand pair of the next slice
     float xv[MAXD];    // this lane's coordinate
     float gyv[MAXO];   // this lane's output cotangent
@@ -121,6 +121,8 @@ struct W1Ctx {
     int64_t lstride;
     unsigned ring_vaddr;  // LDS byte address of this lane's 16 B in slot 0 of the ring
     unsigned sm_vaddr;    // LDS byte address of the small-parameter block + this lane's 4*g neuron offset
+    unsigned long long* prof;  // MODE_PROF: this wave's stamp row of the current tile (nullptr: not recorded)
+    unsigned long long stamp[PROF_EVENTS];  // MODE_PROF: stamps of the current tile (uniform: SGPRs), stored at its end
     // JET: per-lane stream coefficients (stream s = lane & 3)
     float jcf[MAXD];      // first layer: z = sum_k jcf[k] W0[:, k] + jcb b0  (value: x_k; tangent s: e_{s-1})
     float jcb;            // 1 on the value stream (bias), else 0
@@ -171,16 +173,16 @@ template <int G, int LH, int MODE>
 __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& cx, int b,
                                             const EpiParams<epi_kind<G, LH>(), G, LH>& ep) {
     constexpr int KIND = epi_kind<G, LH>();
-    constexpr bool STORE = MODE == MODE_STORE;
-    constexpr bool FWD = forward_only(MODE);
-    if constexpr (MODE == MODE_JET && KIND == EPI_FIRST) {
+    constexpr bool STORE = (MODE & MODE_BASE) == MODE_STORE;
+    constexpr bool FWD = forward_only(MODE & MODE_BASE);
+    if constexpr ((MODE & MODE_BASE) == MODE_JET && KIND == EPI_FIRST) {
         f32x4 z = cx.jcf[0] * ep.v[0];
 #pragma unroll
         for (int k = 1; k < MAXD; ++k)
             if (k < cx.d) z += cx.jcf[k] * ep.v[k];
         z += cx.jcb * ep.v[4];
         st.act[b] = jet_sin(z, cx.w0, cx.ja, cx.jb0, cx.jg0);
-    } else if constexpr (MODE == MODE_JET && KIND == EPI_SINCOS) {
+    } else if constexpr ((MODE & MODE_BASE) == MODE_JET && KIND == EPI_SINCOS) {
         const f32x4 z = st.acc[(G + 1) & 1][b] + cx.jcb * ep.v[0];
         st.act[b] = jet_sin(z, cx.w, cx.ja, cx.jb, cx.jg);
     } else if constexpr (KIND == EPI_FIRST) {
@@ -336,10 +338,15 @@ __device__ __forceinline__ void w1_gemm(W1State<LH, MODE>& st, const W1Ctx& cx) 
     static_for<0, NB>([&](auto KB) { w1_slice<G, decltype(KB)::value, LH, MODE>(st, cx); });
 }
 
+__device__ __forceinline__ void prof_mark(const W1Ctx& cx, int ev) {
+    const_cast<W1Ctx&>(cx).stamp[ev] = __builtin_amdgcn_s_memtime();
+}
+
 template <int G, int LH, int MODE>
 __device__ __forceinline__ void w1_run(W1State<LH, MODE>& st, const W1Ctx& cx) {
     if constexpr (G < npasses<MODE>() * LH) {
         w1_gemm<G, LH, MODE>(st, cx);
+        if constexpr ((MODE & MODE_PROF) != 0) prof_mark(cx, G + 1);
         w1_run<G + 1, LH, MODE>(st, cx);
     }
 }
@@ -349,13 +356,13 @@ constexpr int small_floats_ct(int lh) { return SM_BIAS + (lh + 1) * H; }
 // JET mode: 16 coordinates per workgroup (4 per wave); lap (n) receives sum_j Laplacian(y_j), gx (n, d) sum_j
 // grad y_j (the quantities diff_operators.laplace / gradient return); abuf is reused as the lap pointer.
 template <int LH, int MODE>
-__global__ __launch_bounds__(THREADS, forward_only(MODE) ? 2 : 1) void w1_kernel(const float* __restrict__ ws, const float* __restrict__ x,
+__global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) void w1_kernel(const float* __restrict__ ws, const float* __restrict__ x,
                                                         int64_t n, const float* __restrict__ gy, float* __restrict__ y,
                                                         float* __restrict__ gx, int d, int o, float w0, float w,
                                                         float* __restrict__ abuf, float* __restrict__ dbuf,
                                                         int64_t n_pad) {
-    constexpr bool STORE = MODE == MODE_STORE;
-    constexpr bool JET = MODE == MODE_JET;
+    constexpr bool STORE = (MODE & MODE_BASE) == MODE_STORE;
+    constexpr bool JET = (MODE & MODE_BASE) == MODE_JET;
     constexpr int NS = npasses<MODE>() * LH * NB;
     __shared__ __attribute__((aligned(16))) float lds[W1_NBUF * SLICE + small_floats_ct(LH)];
     W1Ctx cx;
@@ -374,6 +381,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE) ? 2 : 1) void w1_kernel
     cx.seed_ones = gy == nullptr;
     cx.abuf = cx.dbuf = nullptr;
     cx.more = false;
+    cx.prof = nullptr;
     cx.stream = ws + small_pad(LH);
     cx.lstride = n_pad * H;
     const unsigned lds_base = (unsigned)(uintptr_t)((__attribute__((address_space(3))) float*)lds);
@@ -445,6 +453,13 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE) ? 2 : 1) void w1_kernel
             cx.dbuf = dbuf + toff;
         }
 
+        if constexpr ((MODE & MODE_PROF) != 0) {
+            const int64_t it = (tile - blockIdx.x) / gridDim.x;
+            cx.prof = (blockIdx.x < PROF_BLOCKS && it < PROF_TILES)
+                          ? (unsigned long long*)abuf + ((blockIdx.x * PROF_TILES + it) * WAVES + cx.wave) * PROF_EVENTS
+                          : nullptr;
+            prof_mark(cx, 0);
+        }
         w1_run<0, LH, MODE>(st, cx);
 
         if constexpr (JET) {
@@ -476,7 +491,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE) ? 2 : 1) void w1_kernel
                 if (js == 3) abuf[coord] = tot;
                 else if (js >= 1 && js <= d && gx != nullptr) gx[coord * d + js - 1] = tot;
             }
-        } else if constexpr (MODE == MODE_FWD) {
+        } else if constexpr ((MODE & MODE_BASE) == MODE_FWD) {
             // last hidden layer: z_L = acc + b_L, a_L = sin(w z_L), y = a_L Wout^T + bout (serial epilogue)
             constexpr int GL = (LH - 1) & 1;
 #pragma unroll
@@ -532,6 +547,13 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE) ? 2 : 1) void w1_kernel
                     q = sum_groups(q);
                     if (valid && cx.g == 0) gx[coord * d + k] = q;
                 }
+            }
+        }
+        if constexpr ((MODE & MODE_PROF) != 0) {
+            prof_mark(cx, PROF_EVENTS - 1);
+            if (cx.prof != nullptr && cx.lane == 0) {
+#pragma unroll
+                for (int e = 0; e < PROF_EVENTS; ++e) cx.prof[e] = cx.stamp[e];
             }
         }
     }

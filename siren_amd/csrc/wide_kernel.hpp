@@ -132,7 +132,7 @@ __global__ __launch_bounds__(THREADS, 1) void wide_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             float a, cn;
-            sincos_phase(w0 * z[r], a, cn);
+            sincos_fast(w0 * z[r], a, cn);
             sn[r] = a;
             cs[r] = cn;
         }
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(THREADS, 1) void wide_kernel(
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     float a, cn;
-                    sincos_phase(w * z[r], a, cn);
+                    sincos_fast(w * z[r], a, cn);
                     sn[r] = a;
                     cs[r] = cn;
                 }
@@ -185,7 +185,7 @@ __global__ __launch_bounds__(THREADS, 1) void wide_kernel(
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     float a, cn;
-                    sincos_phase(w * z[r], a, cn);
+                    sincos_fast(w * z[r], a, cn);
                     sn[r] = a;
                     act[rb][r] = cn;
                 }
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(THREADS, 1) void wide_kernel(
                     float fs = 1.f;
                     if (final_sine) {
                         float sn, cs;
-                        sincos_phase(w * yj, sn, cs);
+                        sincos_fast(w * yj, sn, cs);
                         yj = sn;
                         fs = cs;
                     }
