@@ -129,13 +129,21 @@ struct W1Ctx {
     float ja, jb0, jg0, jb, jg;  // a = ja sin + jb cos dz - jg sin |dz|^2  (jb0/jg0 with w0, jb/jg with w)
 };
 
-__device__ __forceinline__ void ring_issue4(const float* __restrict__ stream, float* ring, int s, int wave, int lane) {
-    const float* src = stream + (int64_t)s * SLICE + wave * 1024 + lane * 4;
-    float* dst = ring + (s % W1_NBUF) * SLICE + wave * 1024;
+// Four 1 KiB global->LDS pieces of slice s for this wave, as saddr-form global_load_lds_dwordx4: SGPR slice base
+// (+ q KiB by s_add), the per-lane 16 B as a 32-bit VGPR offset, the LDS destination in M0 — no 64-bit VALU address
+// arithmetic per piece (hipcc's builtin lowering builds a 64-bit VGPR address each time; VALU issue is what an
+// f32-MFMA kernel pays for, siren_common.h sincos_fast). wave must be wave-uniform. The loads are counted in vmcnt
+// exactly like the builtin's (the ring's counted waits are unchanged).
+__device__ __forceinline__ void ring_issue4(const float* __restrict__ stream, float* ring, int s, int wave,
+                                            unsigned lane_off) {
+    const char* src = (const char*)(stream + (int64_t)s * SLICE + wave * 1024);
+    const unsigned dst =
+        (unsigned)(uintptr_t)((__attribute__((address_space(3))) float*)(ring + (s % W1_NBUF) * SLICE + wave * 1024));
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-        __builtin_amdgcn_global_load_lds((const void*)(src + q * 256),
-                                         (__attribute__((address_space(3))) void*)(dst + q * 256), 16, 0, 0);
+    for (int q = 0; q < 4; ++q) {
+        const char* sq = src + q * 1024;
+        asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(lane_off), "s"(sq), "{m0}"(dst + q * 1024) : "memory");
+    }
 }
 
 // ---- epilogue parameters (LDS) -------------------------------------------------------------------------
@@ -273,7 +281,7 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
                 if (S + 3 < NS || cx.more) {
                     const float* sp = cx.stream;
                     asm volatile("" : "+s"(sp));  // keep slice addresses from being hoisted into SGPRs
-                    ring_issue4(sp, cx.ring, (S + 3) % NS, cx.wave, cx.lane);
+                    ring_issue4(sp, cx.ring, (S + 3) % NS, cx.wave, 16u * cx.lane);
                 }
             }
         }
@@ -371,7 +379,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
     float* sm = lds + W1_NBUF * SLICE;
     cx.sm = sm;
     cx.lane = threadIdx.x & 63;
-    cx.wave = threadIdx.x >> 6;
+    cx.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPR address math
     cx.g = cx.lane >> 4;
     const int c = cx.lane & 15;
     cx.d = d;
@@ -420,9 +428,9 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
     __syncthreads();
     // ring prologue: slices 0..2 in flight; slice 0 published; its first operand pair read
     static_assert(NS >= 3, "ring prologue issues three slices");
-    ring_issue4(cx.stream, cx.ring, 0, cx.wave, cx.lane);
-    ring_issue4(cx.stream, cx.ring, 1, cx.wave, cx.lane);
-    ring_issue4(cx.stream, cx.ring, 2, cx.wave, cx.lane);
+    ring_issue4(cx.stream, cx.ring, 0, cx.wave, 16u * cx.lane);
+    ring_issue4(cx.stream, cx.ring, 1, cx.wave, 16u * cx.lane);
+    ring_issue4(cx.stream, cx.ring, 2, cx.wave, 16u * cx.lane);
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     st.pa0 = lds_read4<0>(cx.ring_vaddr);
