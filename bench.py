@@ -86,21 +86,21 @@ def kernel_roofline(eng, ws, x, reps=10):
     return ms, achieved
 
 
-HEADLINE_KERNEL = 'w1_kernel<3,0>'   # kernel name as tools/pmc_summary.py shortens it
+HEADLINE_KERNEL = 'w1_kernel<3,640>'   # MODE_W1 | MODE_O1S | MODE_D(2), as tools/pmc_summary.py shortens it
+PMC_FILE = os.path.join(ROOT, 'profiles', 'pmc_headline.json')
 
 
 def pmc_traffic(n):
-    """HBM bytes per launch of the headline kernel from the committed rocprofv3 PMC summary
-    (profiles/*pmc*.json, written by tools/run_pmc.sh + tools/pmc_summary.py), if one matches this kernel and N."""
-    import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, 'profiles', '*pmc*.json')), reverse=True):
-        try:
-            rec = json.load(open(path))
-        except Exception:
-            continue
-        k = rec.get('kernels', {}).get(HEADLINE_KERNEL)
-        if k and rec.get('n') == n and 'hbm_bytes_per_launch' in k:
-            return round(k['hbm_bytes_per_launch'])
+    """HBM bytes per launch of the headline kernel from the committed rocprofv3 PMC summary of the current kernel
+    (profiles/pmc_headline.json: tools/gpu_round.sh's FETCH_SIZE / WRITE_SIZE passes through tools/pmc_summary.py),
+    if it holds this kernel at this N; else None."""
+    try:
+        rec = json.load(open(PMC_FILE))
+    except Exception:
+        return None
+    k = rec.get('kernels', {}).get(HEADLINE_KERNEL)
+    if k and rec.get('n') == n and 'hbm_bytes_per_launch' in k:
+        return round(k['hbm_bytes_per_launch'])
     return None
 
 

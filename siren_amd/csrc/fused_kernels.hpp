@@ -24,35 +24,42 @@ namespace siren {
 // Forward slices are stored for l = 1..LH, reverse slices for l = LH..1: exactly the order the fused
 // kernel consumes them, so its ring loader walks the workspace linearly.
 // ------------------------------------------------------------------------------------------------------
+// With base > 0 (hidden 256) a second, phase-scaled copy follows at ws + base for w1_kernel: W0^T and b0 times
+// s0 = w0 / 2 pi, hidden-layer slices and biases times s = w / 2 pi (W_out, b_out and the seed unscaled), so that
+// kernel's accumulators are phases in revolutions (sincos_rev) and its reverse GEMMs return s W^T delta.
 __global__ void pack_kernel(const float* __restrict__ p, float* __restrict__ ws, int d, int o, int lh,
-                            int64_t spad, int64_t total, int h) {
+                            int64_t spad, int64_t total, int h, int64_t base, float s0, float s) {
     // h = hidden width (256: the H kernels, 512: wide_kernel.hpp); a slice is 16 K-rows x h out-neurons
     const ParamOffsets off(d, o, lh, h);
     const SmallLayout sl(h);
     const int nb = h / 16;
     const int64_t slice_floats = 16 * (int64_t)h;
-    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-         idx += (int64_t)gridDim.x * blockDim.x) {
-        float v = 0.f;
+    for (int64_t gidx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; gidx < total;
+         gidx += (int64_t)gridDim.x * blockDim.x) {
+        const bool scaled = base > 0 && gidx >= base;
+        const int64_t idx = scaled ? gidx - base : gidx;
+        float v = 0.f, sc = 1.f;
         if (idx < spad) {
             const int e = (int)idx;
             if (e < sl.wo) {
                 const int k = e / h, n = e % h;
                 v = k < d ? p[off.w0 + (int64_t)n * d + k] : 0.f;
+                sc = s0;
             } else if (e < sl.seed) {
                 const int j = (e - sl.wo) / h, n = (e - sl.wo) % h;
                 v = j < o ? p[off.wout + (int64_t)j * h + n] : 0.f;
             } else if (e < sl.bout) {
                 const int n = e - sl.seed;
-                float s = 0.f;
-                for (int j = 0; j < o; ++j) s += p[off.wout + (int64_t)j * h + n];
-                v = s;
+                float acc = 0.f;
+                for (int j = 0; j < o; ++j) acc += p[off.wout + (int64_t)j * h + n];
+                v = acc;
             } else if (e < sl.bias) {
                 const int j = e - sl.bout;
                 v = j < o ? p[off.bout + j] : 0.f;
             } else if (e < sl.floats(lh)) {
                 const int l = (e - sl.bias) / h, n = (e - sl.bias) % h;
                 v = p[off.b(l) + n];
+                sc = l == 0 ? s0 : s;
             }
         } else {
             const int64_t e = idx - spad;
@@ -67,8 +74,9 @@ __global__ void pack_kernel(const float* __restrict__ p, float* __restrict__ ws,
                 const int l = lh - (int)(s2 / nb), kb = (int)(s2 % nb);
                 v = p[off.w(l) + (int64_t)(16 * kb + 4 * g + r) * h + 16 * blk + i];
             }
+            sc = s;
         }
-        ws[idx] = v;
+        ws[gidx] = scaled ? v * sc : v;
     }
 }
 

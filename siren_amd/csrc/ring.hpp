@@ -10,12 +10,11 @@ namespace siren {
 __device__ __forceinline__ void ring_issue(const float* __restrict__ stream, float* ring, int s, int nslices,
                                            int wave, int lane) {
     if (s < nslices) {
-        const float* src = stream + (int64_t)s * SLICE + wave * 1024 + lane * 4;
-        float* dst = ring + (s % NBUF) * SLICE + wave * 1024;
+        const int wu = __builtin_amdgcn_readfirstlane(wave);
+        const char* src = (const char*)(stream + (int64_t)s * SLICE + wu * 1024);
+        const unsigned dst = lds_addr(ring + (s % NBUF) * SLICE + wu * 1024);
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            __builtin_amdgcn_global_load_lds((const void*)(src + q * 256),
-                                             (__attribute__((address_space(3))) void*)(dst + q * 256), 16, 0, 0);
+        for (int q = 0; q < 4; ++q) glds_x4(src + q * 1024, 16u * lane, dst + q * 1024);
     }
 }
 

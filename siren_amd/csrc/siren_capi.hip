@@ -45,17 +45,32 @@ int hip_status(const char* what) {
 
 bool wide(const siren_cfg* cfg) { return cfg->hidden == 512; }
 
-// packed workspace: small block + forward slices + transposed slices (16 x hidden floats each)
+// packed workspace: small block + forward slices + transposed slices (16 x hidden floats each); at hidden 256 a
+// second, phase-scaled copy follows for w1_kernel (pack_kernel: weights and biases times w / 2 pi, so its
+// accumulators are phases in revolutions and each sin/cos epilogue saves ~4 VALU — siren_common.h sincos_rev)
 int64_t small_pad(const siren_cfg* cfg) { return siren::SmallLayout(cfg->hidden).pad(cfg->n_hidden); }
-int64_t ws_floats(const siren_cfg* cfg) {
+int64_t ws_base(const siren_cfg* cfg) {
     const int64_t h = cfg->hidden;
     return small_pad(cfg) + 2ll * cfg->n_hidden * (h / 16) * (16 * h);
 }
+int64_t ws_floats(const siren_cfg* cfg) { return wide(cfg) ? ws_base(cfg) : 2 * ws_base(cfg); }
+// the phase-scaled image needs w0, w != 0 (its reverse multipliers are w0 / s and 2 pi with s = w / 2 pi)
+bool w1_ok(const siren_cfg* cfg) { return !wide(cfg) && cfg->omega_first != 0.f && cfg->omega_hidden != 0.f; }
+const float* w1_ws(const siren_cfg* cfg, const float* ws) { return ws + ws_base(cfg); }
+constexpr float kInv2Pi = 0.159154943091895336f;
 
 // Persistent grid for W1 / STORE (one workgroup per CU): each walks tiles blockIdx.x, + gridDim.x, ... with its
 // weight ring streaming across tile boundaries (+1 % on W1, profiles/r01_ab_w1_persist.log). The forward-only
 // modes (2 workgroups per CU) measured slower persistent and keep one workgroup per tile.
 // SIREN_FLAG_NO_PERSIST: one workgroup per tile (A/B).
+// W1 instantiation: the specialised d_out == 1 / ones-cotangent bodies for d_in 2 and 3 at 3 hidden layers
+// (image fit, SDF), the general body otherwise
+int w1_mode(const siren_cfg* cfg, const float* gy) {
+    if (cfg->n_hidden == 3 && cfg->d_out == 1 && gy == nullptr && (cfg->d_in == 2 || cfg->d_in == 3))
+        return siren::MODE_W1 | siren::MODE_O1S | siren::MODE_D(cfg->d_in);
+    return siren::MODE_W1;
+}
+
 dim3 tile_grid(const siren_cfg* cfg, int64_t tiles, int per_cu) {
     if ((cfg->reserved & SIREN_FLAG_NO_PERSIST) != 0) return dim3((unsigned)tiles);
     static int cus[64] = {0};
@@ -130,6 +145,7 @@ int32_t siren_pack(const siren_cfg* cfg, const float* params, float* ws, void* s
     if (int rc = check_cfg(cfg, true)) return rc;
     if (params == nullptr || ws == nullptr) return fail(SIREN_EINVAL, "params/ws is NULL");
     siren::launch_pack(params, ws, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden, small_pad(cfg), ws_floats(cfg),
+                       wide(cfg) ? 0 : ws_base(cfg), cfg->omega_first * kInv2Pi, cfg->omega_hidden * kInv2Pi,
                        (hipStream_t)stream);
     return hip_status("siren_pack");
 }
@@ -146,9 +162,11 @@ int32_t siren_forward(const siren_cfg* cfg, const float* ws, const float* x, int
                         cfg->omega_hidden, cfg->outermost_linear ? 0 : 1, nullptr, nullptr, 0};
     if (wide(cfg))
         siren::launch_wide(siren::MODE_FWD, grid, (hipStream_t)stream, fa, nullptr);
-    else if (cfg->outermost_linear && cfg->n_hidden <= 5 && (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0)
+    else if (cfg->outermost_linear && cfg->n_hidden <= 5 && (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0 &&
+             w1_ok(cfg)) {
+        fa.ws = w1_ws(cfg, ws);
         siren::launch_w0(grid, (hipStream_t)stream, fa);  // 2 WGs/CU: persistence measured slower
-    else
+    } else
         siren::launch_legacy_fwd(grid, (hipStream_t)stream, fa);
     return hip_status("siren_forward");
 }
@@ -177,39 +195,41 @@ int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x
         fa.n_pad = n_pad;  // per-layer scratch stride
         siren::launch_wide(siren::MODE_W1, grid, (hipStream_t)stream, fa, spill);
         (void)hipFreeAsync(spill, (hipStream_t)stream);
-    } else if ((cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) != 0 || fs)
+    } else if ((cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) != 0 || fs || !w1_ok(cfg)) {
         siren::launch_legacy_grad(false, grid, (hipStream_t)stream, fa);
-    else
-        siren::launch_w1(siren::MODE_W1, tile_grid(cfg, blocks, 1), (hipStream_t)stream, fa);
+    } else {
+        fa.ws = w1_ws(cfg, ws);
+        siren::launch_w1(w1_mode(cfg, gy), tile_grid(cfg, blocks, 1), (hipStream_t)stream, fa);
+    }
     return hip_status("siren_forward_grad");
 }
 
 int32_t siren_w1_phase_profile(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y, float* gx,
                                uint64_t* stamps, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
-    if (cfg->n_hidden != 3 || wide(cfg) || !cfg->outermost_linear)
+    if (cfg->n_hidden != 3 || !w1_ok(cfg) || !cfg->outermost_linear)
         return fail(SIREN_EUNSUPPORTED, "siren_w1_phase_profile covers the hidden-256, 3-hidden-layer W1 kernel");
     if (ws == nullptr || x == nullptr || y == nullptr || gx == nullptr || stamps == nullptr || n <= 0)
         return fail(SIREN_EINVAL, "NULL pointer or n <= 0");
     const int64_t blocks = (n + siren::TILE - 1) / siren::TILE;
-    siren::FusedArgs fa{ws, x, n, nullptr, y, gx, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first,
+    siren::FusedArgs fa{w1_ws(cfg, ws), x, n, nullptr, y, gx, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first,
                         cfg->omega_hidden, 0, (float*)stamps, nullptr, blocks * siren::TILE};
-    siren::launch_w1(siren::MODE_W1 | siren::MODE_PROF, tile_grid(cfg, blocks, 1), (hipStream_t)stream, fa);
+    siren::launch_w1(w1_mode(cfg, nullptr) | siren::MODE_PROF, tile_grid(cfg, blocks, 1), (hipStream_t)stream, fa);
     return hip_status("siren_w1_phase_profile");
 }
 
 int32_t siren_forward_laplace(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y, float* gx,
                               float* lap, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
-    if (wide(cfg) || cfg->d_in > 2 || !cfg->outermost_linear || cfg->n_hidden > 5)
-        return fail(SIREN_EUNSUPPORTED,
-                    "siren_forward_laplace covers hidden 256, in_features <= 2, linear output, 1..5 hidden layers");
+    if (!w1_ok(cfg) || cfg->d_in > 2 || !cfg->outermost_linear || cfg->n_hidden > 5)
+        return fail(SIREN_EUNSUPPORTED, "siren_forward_laplace covers hidden 256, in_features <= 2, linear output, "
+                                        "1..5 hidden layers, nonzero omegas");
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
     if (n == 0) return SIREN_OK;
     if (ws == nullptr || x == nullptr || lap == nullptr) return fail(SIREN_EINVAL, "ws/x/lap is NULL");
     const int64_t blocks = (n + 15) / 16;  // 4 coordinates x 4 jet streams per wave
     if (blocks > 0x7fffffffll) return fail(SIREN_EINVAL, "n too large");
-    siren::launch_w4(dim3((unsigned)blocks), (hipStream_t)stream, ws, x, n, y, gx, lap, cfg->d_in, cfg->d_out,
+    siren::launch_w4(dim3((unsigned)blocks), (hipStream_t)stream, w1_ws(cfg, ws), x, n, y, gx, lap, cfg->d_in, cfg->d_out,
                      cfg->n_hidden, cfg->omega_first, cfg->omega_hidden);
     return hip_status("siren_forward_laplace");
 }
@@ -248,9 +268,10 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
                         cfg->omega_hidden, fs, abuf, dbuf, plan.n_pad};
     if (wide(cfg))
         siren::launch_wide(siren::MODE_STORE, grid, st, fa, spill);
-    else if ((cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0 && !fs)
+    else if ((cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0 && !fs && w1_ok(cfg)) {
+        fa.ws = w1_ws(cfg, ws);
         siren::launch_w1(siren::MODE_STORE, tile_grid(cfg, plan.n_pad / siren::TILE, 1), st, fa);
-    else
+    } else
         siren::launch_legacy_grad(true, grid, st, fa);
     if (int rc = hip_status("siren_backward (fused store)")) return rc;
     const unsigned quads = (unsigned)((cfg->hidden / 256) * (cfg->hidden / 256));

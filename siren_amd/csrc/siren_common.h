@@ -34,8 +34,13 @@ constexpr int MAX_LH_GRAD = 3;    // max hidden layers of the forward+grad kerne
 // MODE_JET (W4): forward-mode Taylor jet for the Laplacian — 4 coordinates x 4 jet streams (value, d/dx_1,
 // d/dx_2, sum_i d2/dx_i2) in the 16 MFMA columns, y / grad / Laplacian in one forward sweep.
 enum { MODE_W1 = 0, MODE_STORE = 1, MODE_FWD = 2, MODE_JET = 3 };
-// w1_kernel modifier bit (MODE & MODE_BASE is the mode proper): MODE_PROF records per-GEMM s_memtime stamps
-enum { MODE_BASE = 15, MODE_PROF = 64 };
+// w1_kernel modifier bits (MODE & MODE_BASE is the mode proper): MODE_PROF records per-GEMM s_memtime stamps;
+// MODE_O1S specialises d_out == 1 with the all-ones output cotangent (gy == NULL); MODE_D(k) fixes d_in = k at
+// compile time. Both only remove runtime-uniform branches and selects from the epilogues (whose VALU count is the
+// kernel's overhead, see sincos_fast).
+enum { MODE_BASE = 15, MODE_PROF = 64, MODE_O1S = 128 };
+constexpr int MODE_D(int k) { return k << 8; }
+constexpr int mode_din(int mode) { return (mode >> 8) & 7; }
 // MODE_PROF (diagnostics, siren_w1_phase_profile): s_memtime stamps at tile start, after each GEMM and at tile end
 constexpr int PROF_TILES = 4, PROF_EVENTS = 8, PROF_BLOCKS = 256;
 __host__ __device__ constexpr bool forward_only(int mode) { return mode == MODE_FWD || mode == MODE_JET; }
@@ -92,6 +97,17 @@ __device__ __forceinline__ void sincos_phase(float t, float& sn, float& cs) {
     cs = ((qi + 1) & 2) ? -cv : cv;
 }
 
+// One 1 KiB global->LDS piece (16 B per lane) in the saddr form: wave-uniform source base (SGPR pair) + the lane's
+// 32-bit byte offset (VGPR) -> LDS at m0 (wave-uniform byte address). hipcc lowers __builtin_amdgcn_global_load_lds
+// to a 64-bit VGPR address built with VALU for every piece; VALU issue is what the f32-MFMA kernels pay for (see
+// sincos_fast below). Counted in vmcnt like any load; the kernels' ring protocols wait on it explicitly.
+__device__ __forceinline__ void glds_x4(const void* sbase, unsigned lane_off, unsigned m0) {
+    asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(lane_off), "s"(sbase), "{m0}"(m0) : "memory");
+}
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+    return (unsigned)(uintptr_t)((__attribute__((address_space(3))) const void*)p);
+}
+
 // sin/cos for the MFMA kernels' epilogues, via the transcendental unit: Cody-Waite reduction of t by 2 pi
 // (C1 = fp32(2 pi), C2 = 2 pi - C1; q*C1 is exact inside the fma, so r is accurate while q is exact), then
 // v_sin_f32 / v_cos_f32 on revolutions in [-1/2, 1/2]. Branch-free, 5 VALU + 2 transcendental. Max abs error
@@ -106,6 +122,16 @@ __device__ __forceinline__ void sincos_fast(float t, float& sn, float& cs) {
     const float u = r * 0.159154943091895336f;
     sn = __builtin_amdgcn_sinf(u);
     cs = __builtin_amdgcn_cosf(u);
+}
+
+// sin/cos of 2 pi u for a phase already in revolutions (w1_kernel's phase-scaled pack: weights and biases carry
+// w / 2 pi, so the MFMA accumulators hold u = w z / 2 pi directly). r = u - rint(u) is exact, so the reduction costs
+// 2 VALU instead of sincos_fast's 5; the argument's own rounding is one fp32 rounding of w z, like the reference's
+// fl(30 z) (modules.py:34).
+__device__ __forceinline__ void sincos_rev(float u, float& sn, float& cs) {
+    const float r = u - __builtin_rintf(u);
+    sn = __builtin_amdgcn_sinf(r);
+    cs = __builtin_amdgcn_cosf(r);
 }
 
 // ---- forward-mode Taylor jets (MODE_JET, jet_kernel.hpp) ---------------------------------------------------
@@ -132,13 +158,19 @@ __device__ __forceinline__ f32x4 jet_sin(const f32x4& z, float w, float ka, floa
     return out;
 }
 
-// one element of jet_sin (the MFMA-interleaved epilogues of w1_kernel split a block into its 4 elements)
-__device__ __forceinline__ float jet_sin1(float z, float w, float ka, float kb, float kg) {
-    const float z0 = quad_bcast<0>(z), t1 = quad_bcast<1>(z), t2 = quad_bcast<2>(z);
-    float sn, cs;
-    sincos_fast(w * z0, sn, cs);
-    const float q2 = __builtin_fmaf(t1, t1, t2 * t2);
-    return __builtin_fmaf(ka, sn, __builtin_fmaf(kb * cs, z, -(kg * sn) * q2));
+// jet_sin on a phase-scaled jet (w1_kernel's revolution-domain pack: z is already w z / 2 pi on every stream, so
+// kb = 2 pi [s != 0], kg = 4 pi^2 [s == 3] give the same a_i = w cos z_i and a_3 = w cos z_3 - w^2 sin |z_12|^2)
+__device__ __forceinline__ f32x4 jet_sin_rev(const f32x4& z, float ka, float kb, float kg) {
+    f32x4 out;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float z0 = quad_bcast<0>(z[r]), t1 = quad_bcast<1>(z[r]), t2 = quad_bcast<2>(z[r]);
+        float sn, cs;
+        sincos_rev(z0, sn, cs);
+        const float q2 = __builtin_fmaf(t1, t1, t2 * t2);
+        out[r] = __builtin_fmaf(ka, sn, __builtin_fmaf(kb * cs, z[r], -(kg * sn) * q2));
+    }
+    return out;
 }
 
 // Adjoint of jet_sin: given this lane's stream of the cotangent u of the output jet and of the input jet z,

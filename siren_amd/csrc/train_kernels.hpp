@@ -21,13 +21,12 @@ __device__ __forceinline__ void wg_issue(const float* __restrict__ dsrc, const f
                                          int64_t t, int64_t t1, int k, int wave, int lane, int64_t tstride) {
     if (t < t1) {
         float* slot = ring + (k % WG_NBUF) * WG_SLOT;
+        const int wu = __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-            const int chunk = wave * 8 + q;  // 32 chunks of 1 KiB: 0..15 delta tile, 16..31 activation tile
-            const float* src = (chunk < 16 ? dsrc + t * tstride + chunk * 256
-                                           : asrc + t * tstride + (chunk - 16) * 256) + lane * 4;
-            __builtin_amdgcn_global_load_lds((const void*)src,
-                                             (__attribute__((address_space(3))) void*)(slot + chunk * 256), 16, 0, 0);
+            const int chunk = wu * 8 + q;  // 32 chunks of 1 KiB: 0..15 delta tile, 16..31 activation tile
+            const float* src = chunk < 16 ? dsrc + t * tstride + chunk * 256 : asrc + t * tstride + (chunk - 16) * 256;
+            glds_x4(src, 16u * lane, lds_addr(slot + chunk * 256));
         }
     }
 }

@@ -16,6 +16,12 @@ void launch_w1(int mode, dim3 grid, hipStream_t st, const FusedArgs& a) {
         }
     } else if (mode == (MODE_W1 | MODE_PROF)) {
         SIREN_L(3, MODE_W1 | MODE_PROF);
+    } else if (mode == (MODE_W1 | MODE_O1S | MODE_D(2)) && a.lh == 3) {
+        SIREN_L(3, MODE_W1 | MODE_O1S | MODE_D(2));
+    } else if (mode == (MODE_W1 | MODE_O1S | MODE_D(3)) && a.lh == 3) {
+        SIREN_L(3, MODE_W1 | MODE_O1S | MODE_D(3));
+    } else if (mode == (MODE_W1 | MODE_O1S | MODE_D(2) | MODE_PROF) && a.lh == 3) {
+        SIREN_L(3, MODE_W1 | MODE_O1S | MODE_D(2) | MODE_PROF);
     } else {
         switch (a.lh) {
             case 1: SIREN_L(1, MODE_W1); break;

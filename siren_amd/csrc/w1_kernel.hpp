@@ -112,7 +112,10 @@ struct W1Ctx {
     float* ring;
     const float* sm;
     int d, o, wave, lane, g;
-    float w0, w;
+    // phase-scaled pack (weights carry w / 2 pi, pack_kernel): w = 2 pi multiplies the reverse GEMM output s W^T delta
+    // into W^T delta . w cos, w0 = w0_true / s does the same for layer 0, wsd = w_true seeds delta_L, inv_s0 = 1 / s0
+    // undoes the first layer's scale in gx
+    float w0, w, wsd, inv_s0;
     bool seed_ones;
     float* abuf;  // STORE: lane-adjusted tile base of layer 0; layer l at + l * lstride
     float* dbuf;
@@ -137,13 +140,9 @@ struct W1Ctx {
 __device__ __forceinline__ void ring_issue4(const float* __restrict__ stream, float* ring, int s, int wave,
                                             unsigned lane_off) {
     const char* src = (const char*)(stream + (int64_t)s * SLICE + wave * 1024);
-    const unsigned dst =
-        (unsigned)(uintptr_t)((__attribute__((address_space(3))) float*)(ring + (s % W1_NBUF) * SLICE + wave * 1024));
+    const unsigned dst = lds_addr(ring + (s % W1_NBUF) * SLICE + wave * 1024);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const char* sq = src + q * 1024;
-        asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(lane_off), "s"(sq), "{m0}"(dst + q * 1024) : "memory");
-    }
+    for (int q = 0; q < 4; ++q) glds_x4(src + q * 1024, lane_off, dst + q * 1024);
 }
 
 // ---- epilogue parameters (LDS) -------------------------------------------------------------------------
@@ -189,12 +188,12 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
         for (int k = 1; k < MAXD; ++k)
             if (k < cx.d) z += cx.jcf[k] * ep.v[k];
         z += cx.jcb * ep.v[4];
-        st.act[b] = jet_sin(z, cx.w0, cx.ja, cx.jb0, cx.jg0);
+        st.act[b] = jet_sin_rev(z, cx.ja, cx.jb0, cx.jg0);
     } else if constexpr ((MODE & MODE_BASE) == MODE_JET && KIND == EPI_SINCOS) {
         const f32x4 z = st.acc[(G + 1) & 1][b] + cx.jcb * ep.v[0];
-        st.act[b] = jet_sin(z, cx.w, cx.ja, cx.jb, cx.jg);
+        st.act[b] = jet_sin_rev(z, cx.ja, cx.jb, cx.jg);
     } else if constexpr (KIND == EPI_FIRST) {
-        f32x4 z = st.xv[0] * ep.v[0];
+        f32x4 z = st.xv[0] * ep.v[0];  // phase u_0 = w0 (x W0^T + b0) / 2 pi: the pack carries the scale
 #pragma unroll
         for (int k = 1; k < MAXD; ++k)
             if (k < cx.d) z += st.xv[k] * ep.v[k];
@@ -203,7 +202,7 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             float sn, cs;
-            sincos_fast(cx.w0 * z[r], sn, cs);
+            sincos_rev(z[r], sn, cs);
             st.act[b][r] = sn;
             cs4[r] = cs;
         }
@@ -215,7 +214,7 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             float sn, cs;
-            sincos_fast(cx.w * z[r], sn, cs);
+            sincos_rev(z[r], sn, cs);
             st.act[b][r] = sn;
             cs4[r] = cs;
         }
@@ -227,7 +226,7 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             float a, c;
-            sincos_fast(cx.w * z[r], a, c);
+            sincos_rev(z[r], a, c);
             sn[r] = a;
             cs[r] = c;
         }
@@ -242,7 +241,7 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
             }
         }
         if (cx.seed_ones) ga = ep.v[5];
-        st.act[b] = (ga * cs) * cx.w;
+        st.act[b] = (ga * cs) * cx.wsd;
         if constexpr (STORE) store_block(cx.dbuf + LH * cx.lstride, b, st.act[b]);
     } else {
         constexpr int L = 2 * LH - G;  // delta_L = u_L . cos(w z_L) . w,  1 <= L < LH
@@ -382,10 +381,21 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
     cx.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPR address math
     cx.g = cx.lane >> 4;
     const int c = cx.lane & 15;
+    if constexpr (mode_din(MODE) != 0) d = mode_din(MODE);
+    if constexpr ((MODE & MODE_O1S) != 0) {
+        o = 1;
+        gy = nullptr;
+    }
     cx.d = d;
     cx.o = o;
-    cx.w0 = w0;
-    cx.w = w;
+    {
+        constexpr float two_pi = 6.28318530717958648f;
+        const float s = w * 0.159154943091895336f;  // hidden-layer scale of the phase-scaled pack
+        cx.w0 = w0 / s;
+        cx.w = two_pi;
+        cx.wsd = w;
+        cx.inv_s0 = two_pi / w0;
+    }
     cx.seed_ones = gy == nullptr;
     cx.abuf = cx.dbuf = nullptr;
     cx.more = false;
@@ -417,13 +427,12 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
     };
     load_inputs(blockIdx.x);
     if constexpr (JET) {
+        // jet coefficients on phase-scaled jets: w / s = 2 pi for every layer (jet_sin_rev)
         const float val = js == 0 ? 1.f : 0.f;
         cx.jcb = val;
         cx.ja = val;
-        cx.jb0 = js == 0 ? 0.f : w0;
-        cx.jg0 = js == 3 ? w0 * w0 : 0.f;
-        cx.jb = js == 0 ? 0.f : w;
-        cx.jg = js == 3 ? w * w : 0.f;
+        cx.jb0 = cx.jb = js == 0 ? 0.f : 6.28318530717958648f;
+        cx.jg0 = cx.jg = js == 3 ? 39.4784176043574344f : 0.f;
     }
     __syncthreads();
     // ring prologue: slices 0..2 in flight; slice 0 published; its first operand pair read
@@ -477,7 +486,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
             for (int rb = 0; rb < NB; ++rb) {
                 const int nb = 16 * rb + 4 * cx.g;
                 const f32x4 z = st.acc[GL][rb] + cx.jcb * *(const f32x4*)(sm + SM_BIAS + LH * H + nb);
-                const f32x4 a = jet_sin(z, w, cx.ja, cx.jb, cx.jg);
+                const f32x4 a = jet_sin_rev(z, cx.ja, cx.jb, cx.jg);
 #pragma unroll
                 for (int j = 0; j < MAXO; ++j) {
                     if (j < o) {
@@ -510,7 +519,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     float a, cc;
-                    sincos_fast(w * z[r], a, cc);
+                    sincos_rev(z[r], a, cc);
                     sn[r] = a;
                 }
 #pragma unroll
@@ -537,10 +546,11 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
                     if (y != nullptr && valid && cx.g == 0) y[coord * o + j] = yj;
                 }
             }
-            // delta_0 = u_0 . cos(w0 z_0) . w0 ;  gx = delta_0 W0
+            // delta_0 = u_0 . cos(w0 z_0) . w0 (u_0 = s W_1^T delta_1 from the scaled pack: cx.w0 = w0 / s);
+            // gx = delta_0 W0 (the LDS W0^T carries s0: cx.inv_s0)
             constexpr int GL = (2 * LH - 1) & 1;
 #pragma unroll
-            for (int rb = 0; rb < NB; ++rb) st.act[rb] = (st.acc[GL][rb] * st.C[0][rb]) * w0;
+            for (int rb = 0; rb < NB; ++rb) st.act[rb] = (st.acc[GL][rb] * st.C[0][rb]) * cx.w0;
             if constexpr (STORE) store_tile(cx.dbuf, st.act);
 #pragma unroll
             for (int k = 0; k < MAXD; ++k) {
@@ -552,7 +562,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
                         q += wk[0] * st.act[rb][0] + wk[1] * st.act[rb][1] + wk[2] * st.act[rb][2] +
                              wk[3] * st.act[rb][3];
                     }
-                    q = sum_groups(q);
+                    q = sum_groups(q) * cx.inv_s0;
                     if (valid && cx.g == 0) gx[coord * d + k] = q;
                 }
             }

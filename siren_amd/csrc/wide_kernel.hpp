@@ -32,12 +32,11 @@ constexpr int WSMALL_MAX = 9 * WH + 4 + (MAX_LH_FWD + 1) * WH;
 __device__ __forceinline__ void wring_issue(const float* __restrict__ stream, float* ring, int s, int nslices,
                                             int wave, int lane) {
     if (s < nslices) {
-        const float* src = stream + (int64_t)s * WSLICE + wave * 2048 + lane * 4;
-        float* dst = ring + (s % WNBUF) * WSLICE + wave * 2048;
+        const int wu = __builtin_amdgcn_readfirstlane(wave);
+        const char* src = (const char*)(stream + (int64_t)s * WSLICE + wu * 2048);
+        const unsigned dst = lds_addr(ring + (s % WNBUF) * WSLICE + wu * 2048);
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-            __builtin_amdgcn_global_load_lds((const void*)(src + q * 256),
-                                             (__attribute__((address_space(3))) void*)(dst + q * 256), 16, 0, 0);
+        for (int q = 0; q < 8; ++q) glds_x4(src + q * 1024, 16u * lane, dst + q * 1024);
     }
 }
 

@@ -45,7 +45,7 @@ class SirenEngine:
         # the W3 second-order kernel: hidden 256, scalar output, linear output layer
         # the W4 jet kernel (fused Laplacian): hidden 256, d_in <= 2, linear output, 1..5 hidden layers
         self.laplace_supported = (self.supported and int(hidden) == 256 and int(d_in) <= 2 and 1 <= n_hidden <= 5
-                                  and bool(outermost_linear))
+                                  and bool(outermost_linear) and omega_first != 0 and omega_hidden != 0)
         self.second_order_supported = (self.supported and int(hidden) == 256 and 1 <= n_hidden <= 3
                                        and int(d_out) == 1 and bool(outermost_linear))
 

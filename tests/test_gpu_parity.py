@@ -209,7 +209,11 @@ def test_full_size_properties(cuda):
     _, vab = eng.forward_grad(ws, x, 2 * ga + gb, want_y=False)
     assert torch.allclose(vab, 2 * va + vb, atol=1e-4 * float(vab.abs().max()))
     _, v1 = eng.forward_grad(ws, x, torch.ones(n, 1, device=cuda), want_y=False)
-    assert torch.equal(v1, gx)     # explicit ones == seed path, bit for bit
+    # explicit ones == the seed path. The seed path runs the d_in/d_out-specialised W1 body, whose fma contraction
+    # may differ from the general body's by an ulp of a phase; at |w z| ~ 50 rad one ulp is ~4e-6 rad, so the two
+    # agree to rounding (10x inside the parity tolerance), not bit for bit
+    dv = float((v1 - gx).abs().max())
+    assert dv <= 1e-5 * float(gx.abs().max()), dv
 
 
 def test_engine_validation(cuda):

@@ -47,7 +47,7 @@ def test_param_count_and_workspace(lib):
     c = ctypes.c_int64()
     assert lib.siren_param_count(ctypes.byref(cfg), ctypes.byref(c)) == 0 and c.value == 198401
     assert lib.siren_workspace_floats(ctypes.byref(cfg), ctypes.byref(c)) == 0
-    assert c.value == 4096 + 2 * 3 * 16 * 4096
+    assert c.value == 2 * (4096 + 2 * 3 * 16 * 4096)  # unscaled image + the W1 kernel's phase-scaled copy
     assert lib.siren_train_ws_floats(ctypes.byref(cfg), 1000, ctypes.byref(c)) == 0 and c.value > 0
     bad = _lib.SirenCfg(2, 128, 3, 1, 30., 30., 1, 0)
     assert lib.siren_workspace_floats(ctypes.byref(bad), ctypes.byref(c)) == _lib.SIREN_EUNSUPPORTED
