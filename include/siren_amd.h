@@ -134,11 +134,12 @@ int32_t siren_laplace_backward(const siren_cfg* cfg, const float* ws, const floa
  * primal activations and adjoints of every layer plus 2*S partial slabs). */
 int32_t siren_second_order_ws_floats(const siren_cfg* cfg, int64_t n, int32_t want_theta, int64_t* count);
 
-/* W3, second-order adjoint for hidden 256, d_out == 1 (the backward of the dPhi/dx graph node that gradients_mse / sdf /
+/* W3, second-order adjoint for hidden 256, d_out <= 4, linear output (the backward of the dPhi/dx graph node that gradients_mse / sdf /
  * divergence differentiate, diff_operators.py:27-43, loss_functions.py:84-89, 214-238): with v (n, d_in) the
  * cotangent of J = dPhi/dx,
  *   gx (n, d_in)          = H(x) v                      (Hessian-vector product)
  *   gparams (param_count) = d/dtheta sum_c <v_c, J(x_c)> (skipped when gparams == NULL)
+ * (J = sum_j dPhi_j/dx, what diff_operators.gradient records for a vector output; see siren_second_order_ex)
  * Forward primal+tangent sweep and reverse sweep in one kernel (per-layer state spilled to tws), then the split-K
  * MFMA weight-gradient kernel over K = 2n and a deterministic slab reduction. */
 int32_t siren_second_order(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
@@ -151,6 +152,18 @@ int32_t siren_second_order(const siren_cfg* cfg, const float* ws, const float* x
  * siren_second_order. */
 int32_t siren_second_order_seeded(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
                                   const float* gy, float* tws, float* gx, float* gparams, void* stream);
+
+/* W3 for vector outputs (diff_operators.jacobian / hessian, diff_operators.py:5-24, 46-59; the helmholtz_pml /
+ * wave_pml losses, loss_functions.py:112-211): the backward of the vjp node gx = J^T u, with per-coordinate output
+ * weighting u (n, d_out) (NULL = ones), first-order seed gy (n, d_out) (NULL = none) and v (n, d_in) the cotangent
+ * of gx:
+ *   gx (n, d_in)          = d/dx     F,   F = sum_c gy_c . y_c + <v_c, J(x_c)^T u_c>
+ *   gparams (param_count) = d/dtheta F    (skipped when gparams == NULL)
+ *   ydot (n, d_out)       = J(x_c) v_c = dF/du_c (skipped when ydot == NULL)
+ * One W3 sweep; siren_second_order / _seeded are this entry with u = ydot = NULL. Same workspace. */
+int32_t siren_second_order_ex(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
+                              const float* u, const float* gy, float* tws, float* gx, float* gparams, float* ydot,
+                              void* stream);
 
 /* Diagnostics: the W1 kernel (hidden 256, 3 hidden layers) with s_memtime stamps. stamps receives
  * 256 workgroups x 4 tiles x 4 waves x 8 events (uint64; event 0 tile start, 1..6 after GEMM 0..5, 7 tile end);

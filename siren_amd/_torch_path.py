@@ -1,6 +1,6 @@
 """Device-side torch restatement of the SIREN op sequence, used ONLY for the higher-order adjoints that have no
-HIP kernel yet: third derivatives (the backward of a Hessian-vector product node: laplace_mse training, W4s),
-second derivatives of hidden-512 networks, and vector outputs (d_out > 1) under create_graph.
+HIP kernel yet: third derivatives (the backward of a Hessian-vector product node built by an unfused divergence or
+the PML losses), theta-gradients under create_graph, and second derivatives of hidden-512 networks.
 
 It runs on the same ROCm device as the kernels (never on the CPU) and re-records the reference's op order
 (modules.py:23-24 matmul + bias, :34 sin(w z)) so autograd can differentiate it to any order. The first-order
@@ -74,17 +74,22 @@ def vjp_vjp(cfg, x, flat, gy, ggx, create_graph):
     return rx, rp, rgy
 
 
-def hvp_vjp(cfg, x, flat, v, g, create_graph):
-    """d/d(x, theta, v) of <g, H(x) v> (d_out == 1)."""
+def hvp_vjp(cfg, x, flat, v, g, create_graph, u=None):
+    """d/d(x, theta, v, u) of <g, d/dx <v, J(x)^T u>> (u (n, d_out), None = ones)."""
     with torch.enable_grad():
         vr = v if v.requires_grad else v.detach().requires_grad_(True)
+        ur = None
+        if u is not None:
+            ur = u if u.requires_grad else u.detach().requires_grad_(True)
         y = forward(cfg, x, flat)
-        J = torch.autograd.grad(y, x, torch.ones_like(y), create_graph=True)[0]
+        J = torch.autograd.grad(y, x, torch.ones_like(y) if ur is None else ur, create_graph=True)[0]
         hv = torch.autograd.grad(J, x, vr, create_graph=True)[0]
-        rx, rp, rv = _grads(hv, [x, flat, vr], g, create_graph)
+        rx, rp, rv, ru = _grads(hv, [x, flat, vr, ur], g, create_graph)
     if not v.requires_grad:
         rv = None
-    return rx, rp, rv
+    if u is None or not u.requires_grad:
+        ru = None
+    return rx, rp, rv, ru
 
 
 def laplacian(cfg, x, flat):

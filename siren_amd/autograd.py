@@ -19,10 +19,10 @@ next nodes), because ctx.needs_input_grad is static: autograd.grad(y, [x]) must 
 
 Second-order adjoints (SirenJetFunction/SirenVJP.backward: gradients_mse / sdf training, the Laplacian's
 Hessian-vector products) run on the W3 kernel (siren_second_order[_seeded]) for hidden 256 and
-d_out == 1. laplace_mse training runs the W4s kernels (SirenLaplace). Only derivatives the reference's losses never
-take through our nodes — theta-gradients under create_graph (meta-learning), third order through a SirenHVP node
-built by an unfused divergence(), second order at hidden 512 and vector outputs — are recomputed through
-siren_amd._torch_path with device torch ops.
+d_out <= 4 (vector outputs through an output weighting u: jacobian / hessian, helmholtz_pml / wave_pml).
+laplace_mse training runs the W4s kernels (SirenLaplace). Only theta-gradients under create_graph (meta-learning),
+third derivatives through a SirenHVP node (an unfused divergence(), the PML losses' training backward) and second
+order at hidden 512 are recomputed through siren_amd._torch_path with device torch ops.
 """
 import torch
 
@@ -155,26 +155,30 @@ class SirenJetFunction(torch.autograd.Function):
 
 
 class SirenHVP(torch.autograd.Function):
-    """H(x; theta) v (d_out == 1) as a graph node: forward = W3 kernel (x part only); its own backward (a third
-    derivative: laplace_mse training) is recomputed with device torch ops."""
+    """d/dx <v, J(x)^T u> = sum_j u_j H_j(x) v as a graph node (u (n, d_out), None = ones: H v for d_out == 1):
+    forward = W3 kernel (x part only, siren_second_order_ex); its own backward (a third derivative: laplace_mse
+    through an unfused divergence, helmholtz_pml / wave_pml training) is recomputed with device torch ops."""
 
     @staticmethod
-    def forward(ctx, engine, ws, x, flat, v):
-        gx, _ = engine.second_order(ws, x, v.contiguous(), want_theta=False)
+    def forward(ctx, engine, ws, x, flat, v, u=None):
+        gx, _ = engine.second_order(ws, x, v.contiguous(), want_theta=False, u=u)
         ctx.engine = engine
-        ctx.save_for_backward(x, flat, v)
+        ctx.save_for_backward(x, flat, v, u)
         return gx
 
     @staticmethod
     def backward(ctx, g):
-        x, flat, v = ctx.saved_tensors
-        rx, rp, rv = _torch_path.hvp_vjp(ctx.engine.cfg, x, flat, v, g, create_graph=torch.is_grad_enabled())
-        return None, None, rx, rp, rv
+        x, flat, v, u = ctx.saved_tensors
+        rx, rp, rv, ru = _torch_path.hvp_vjp(ctx.engine.cfg, x, flat, v, g, create_graph=torch.is_grad_enabled(),
+                                             u=u)
+        return None, None, rx, rp, rv, ru
 
 
 class SirenVJP(torch.autograd.Function):
-    """gx = sum_j gy_j dPhi_j/dx as a graph node; forward is the fused W1 kernel. For d_out == 1 its backward is
-    the W3 kernel with v = gy * ggx (plus <ggx, J> for gy, from the W1 kernel)."""
+    """gx = J^T gy = sum_j gy_j dPhi_j/dx as a graph node; forward is the fused W1 kernel. Its backward is the W3
+    kernel with output weighting u = gy and v = ggx (siren_second_order_ex), which also returns ggy = J ggx in the
+    same sweep; under create_graph, an x-only request becomes a differentiable SirenHVP node (the second
+    jacobian() of helmholtz_pml / wave_pml, hessian())."""
 
     @staticmethod
     def forward(ctx, engine, ws, x, flat, gy):
@@ -187,21 +191,21 @@ class SirenVJP(torch.autograd.Function):
     def backward(ctx, ggx):
         x, flat, gy = ctx.saved_tensors
         eng = ctx.engine
-        w3_ok = eng.second_order_supported
-        if torch.is_grad_enabled() or not w3_ok:
-            gx, gp, ggy = _torch_path.vjp_vjp(eng.cfg, x, flat, gy, ggx, create_graph=torch.is_grad_enabled())
-            return None, None, gx, gp, ggy
         # tensor inputs in order: ws (0), x (1), flat (2), gy (3)
         need_x = ctx.needs_input_grad[2] and _will_execute(ctx, 1)
         need_p = ctx.needs_input_grad[3] and _will_execute(ctx, 2)
         need_gy = ctx.needs_input_grad[4] and _will_execute(ctx, 3)
+        if not (need_x or need_p or need_gy):
+            return None, None, None, None, None
         ggx = ggx.contiguous()
-        gx = gp = ggy = None
-        if need_x or need_p:
-            gx, gp = eng.second_order(ctx.ws, x, (gy * ggx).contiguous(), want_theta=need_p)
-        if need_gy:
-            _, J = eng.forward_grad(ctx.ws, x, want_y=False)
-            ggy = (J * ggx).sum(-1, keepdim=True)
+        if not eng.second_order_supported or (torch.is_grad_enabled() and (need_p or need_gy)):
+            gx, gp, ggy = _torch_path.vjp_vjp(eng.cfg, x, flat, gy, ggx, create_graph=torch.is_grad_enabled())
+            return None, None, gx, gp, ggy
+        if torch.is_grad_enabled():  # x only, differentiable
+            return None, None, SirenHVP.apply(eng, ctx.ws, x, flat, ggx, gy), None, None
+        res = eng.second_order(ctx.ws, x, ggx, want_theta=need_p, u=gy, want_ydot=need_gy)
+        gx, gp = res[0], res[1]
+        ggy = res[2] if need_gy else None
         return None, None, (gx if need_x else None), gp, ggy
 
 

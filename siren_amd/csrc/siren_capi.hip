@@ -388,12 +388,17 @@ int32_t siren_second_order(const siren_cfg* cfg, const float* ws, const float* x
 
 int32_t siren_second_order_seeded(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
                                   const float* gy, float* tws, float* gx, float* gparams, void* stream) {
+    return siren_second_order_ex(cfg, ws, x, n, v, nullptr, gy, tws, gx, gparams, nullptr, stream);
+}
+
+int32_t siren_second_order_ex(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
+                              const float* u, const float* gy, float* tws, float* gx, float* gparams, float* ydot,
+                              void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (cfg->n_hidden > siren::MAX_LH_GRAD)
         return fail(SIREN_EUNSUPPORTED, "siren_second_order needs 1 <= num_hidden_layers <= 3");
-    if (cfg->d_out != 1 || !cfg->outermost_linear || wide(cfg))
-        return fail(SIREN_EUNSUPPORTED,
-                    "siren_second_order covers hidden 256, d_out == 1 with a linear output layer");
+    if (!cfg->outermost_linear || wide(cfg))
+        return fail(SIREN_EUNSUPPORTED, "siren_second_order covers hidden 256 with a linear output layer");
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
     if (ws == nullptr || tws == nullptr || gx == nullptr || (n > 0 && (x == nullptr || v == nullptr)))
         return fail(SIREN_EINVAL, "ws/x/v/tws/gx is NULL");
@@ -412,8 +417,8 @@ int32_t siren_second_order_seeded(const siren_cfg* cfg, const float* ws, const f
     float* Dt = D + plan.buf_floats;
     float* partial = Dt + plan.buf_floats;
     const dim3 grid((unsigned)(plan.n_pad / siren::TILE));
-    siren::launch_w3(theta, grid, st, ws, x, v, gy, n, gx, spill, A, At, D, Dt, plan.n_pad, cfg->d_in, cfg->n_hidden,
-                     cfg->omega_first, cfg->omega_hidden);
+    siren::launch_w3(theta, grid, st, ws, x, v, gy, u, ydot, cfg->d_out, n, gx, spill, A, At, D, Dt, plan.n_pad,
+                     cfg->d_in, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden);
     if (int rc = hip_status("siren_second_order (w3)")) return rc;
     if (!theta) return SIREN_OK;
     const dim3 wgrid((unsigned)plan.splits, (unsigned)cfg->n_hidden);
@@ -423,7 +428,7 @@ int32_t siren_second_order_seeded(const siren_cfg* cfg, const float* ws, const f
                         cfg->n_hidden, 0, siren::H);
     if (int rc = hip_status("siren_second_order (wgrad)")) return rc;
     const float* a_last = A + (int64_t)cfg->n_hidden * plan.n_pad * siren::H;  // a_L rows (first-order seed)
-    siren::launch_small_w3(dim3((unsigned)plan.splits), st, At, D, Dt, a_last, x, v, gy, n, plan.n_pad, plan.tps,
+    siren::launch_small_w3(dim3((unsigned)plan.splits), st, At, D, Dt, a_last, x, v, gy, u, n, plan.n_pad, plan.tps,
                            partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden);
     if (int rc = hip_status("siren_second_order (small)")) return rc;
     const siren::ParamOffsets off(cfg->d_in, cfg->d_out, cfg->n_hidden);

@@ -114,7 +114,8 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
 // read as broadcasts; the tile loop is unrolled so each thread keeps several 64 B row loads in flight (the first
 // version walked one tile at a time and was latency-bound at 7x its HBM time).
 //   EDGE_W2 : rows delta_0, a_L:            dW0 = delta_0^T x, db0 = sum delta_0, dWout = gy^T a_L, dbout = sum gy
-//   EDGE_W3 : rows zb_0, zdb_0, adot_L:     dW0 = zdb_0^T v + zb_0^T x, db0 = sum zb_0, dWout = sum adot_L, dbout = 0
+//   EDGE_W3 : rows zb_0, zdb_0, adot_L:     dW0 = zdb_0^T v + zb_0^T x, db0 = sum zb_0, dWout = u^T adot_L
+//             (u = output weighting, ones when NULL), dbout = 0
 //             (+ with a first-order seed gy, rows a_L: dWout += gy^T a_L, dbout = sum gy)
 //   EDGE_JET: rows zb_0 jet, a_L jet (16 columns = 4 coordinates x 4 streams, scalars per coordinate):
 //             dW0[:, k] = sum zb_0,value x_k + zb_0,tangent k, db0 = sum zb_0,value, dWout = sum glap a_L,second
@@ -125,14 +126,18 @@ template <int KIND>
 __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__ r0, const float* __restrict__ r1,
                                                        const float* __restrict__ r2, const float* __restrict__ r3,
                                                        const float* __restrict__ x, const float* __restrict__ sc,
-                                                       const float* __restrict__ sgy, int64_t n, int64_t ntiles,
+                                                       const float* __restrict__ sgy, const float* __restrict__ su,
+                                                       int64_t n, int64_t ntiles,
                                                        int64_t tps, float* __restrict__ partial, int64_t P, int d,
                                                        int o, int lh, int h) {
-    // per-column scalars of one chunk: [col][0..3] = x (d_in <= 4), [col][4..7] = gy / v / glap, [col][8] = the
-    // first-order seed gy of a seeded W3 (sgy != nullptr: rows r3 = a_L add sum gy a_L to dWout, sum gy to dbout)
+    // per-column scalars of one chunk: [col][0..3] = x (d_in <= 4), [col][4..7] = gy / v / glap, [col][8..11] = the
+    // first-order seed gy (n, o) of a seeded W3 (sgy != nullptr: rows r3 = a_L add gy^T a_L to dWout, sum gy to
+    // dbout), [col][12..15] = W3's output weighting u (n, o) (ones when su == nullptr)
     constexpr int CPT = KIND == EDGE_JET ? 4 : 16;  // coordinates per tile
-    __shared__ __attribute__((aligned(16))) float scal[EDGE_CHUNK * CPT][9];
+    constexpr int NSC = KIND == EDGE_W3 ? 16 : 9;
+    __shared__ __attribute__((aligned(16))) float scal[EDGE_CHUNK * CPT][NSC];
     const bool seeded = KIND == EDGE_W3 && sgy != nullptr;
+    const bool weighted = KIND == EDGE_W3 && su != nullptr;
     const ParamOffsets off(d, o, lh, h);
     const int s = blockIdx.x;
     const int64_t t0 = (int64_t)s * tps, t1 = t0 + tps < ntiles ? t0 + tps : ntiles;
@@ -142,7 +147,7 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
     for (int tb = 0; tb < h; tb += THREADS) {
         const int t = tb + threadIdx.x;
         float gw0[MAXD] = {0.f, 0.f, 0.f, 0.f}, gb0 = 0.f;
-        float gwo[MAXO] = {0.f, 0.f, 0.f, 0.f}, gbo = 0.f;
+        float gwo[MAXO] = {0.f, 0.f, 0.f, 0.f}, gbo = 0.f, gbj[MAXO] = {0.f, 0.f, 0.f, 0.f};
         for (int64_t c0 = t0; c0 < t1; c0 += EDGE_CHUNK) {
             const int nt = (int)(t1 - c0 < EDGE_CHUNK ? t1 - c0 : EDGE_CHUNK);
             __syncthreads();
@@ -153,7 +158,15 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
                 for (int k = 0; k < MAXD; ++k) scal[e][k] = (ok && k < d) ? x[cd * d + k] : 0.f;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) scal[e][4 + j] = (ok && j < ns) ? sc[cd * ns + j] : 0.f;
-                scal[e][8] = (ok && seeded) ? sgy[cd] : 0.f;
+                if constexpr (KIND == EDGE_W3) {
+#pragma unroll
+                    for (int j = 0; j < MAXO; ++j) {
+                        scal[e][8 + j] = (ok && seeded && j < o) ? sgy[cd * o + j] : 0.f;
+                        scal[e][12 + j] = weighted ? ((ok && j < o) ? su[cd * o + j] : 0.f) : 1.f;
+                    }
+                } else {
+                    scal[e][8] = 0.f;
+                }
             }
             __syncthreads();
             if (t < h) {
@@ -193,8 +206,11 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
                                 } else {
 #pragma unroll
                                     for (int k = 0; k < MAXD; ++k) gw0[k] += cv[q][r] * sv[4 + k] + av[q][r] * sv[k];
-                                    gwo[0] += bv[q][r] + sv[8] * ev[q][r];
-                                    gbo += sv[8];
+#pragma unroll
+                                    for (int j = 0; j < MAXO; ++j) {
+                                        gwo[j] += sv[12 + j] * bv[q][r] + sv[8 + j] * ev[q][r];
+                                        gbj[j] += sv[8 + j];
+                                    }
                                 }
                             }
                         }
@@ -212,9 +228,15 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
                 for (int j = 0; j < MAXO; ++j)
                     if (j < o) out[off.wout + (int64_t)j * h + t] = gwo[j];
                 if (t < o) out[off.bout + t] = gbo;
+            } else if constexpr (KIND == EDGE_W3) {
+#pragma unroll
+                for (int j = 0; j < MAXO; ++j) {
+                    if (j < o) out[off.wout + (int64_t)j * h + t] = gwo[j];
+                    if (j < o && t == j) out[off.bout + t] = gbj[j];
+                }
             } else {
                 for (int j = 0; j < o; ++j) out[off.wout + (int64_t)j * h + t] = gwo[0];
-                if (t < o) out[off.bout + t] = KIND == EDGE_W3 ? gbo : 0.f;
+                if (t < o) out[off.bout + t] = 0.f;
             }
         }
     }

@@ -13,22 +13,23 @@ void launch_wgrad(dim3 grid, hipStream_t st, const float* abuf, const float* dbu
 void launch_small(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* gy,
                   int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d, int o, int lh, int h) {
     hipLaunchKernelGGL(edge_kernel<EDGE_W2>, grid, dim3(THREADS), 0, st, dbuf, abuf + (int64_t)lh * n_pad * h,
-                       (const float*)nullptr, (const float*)nullptr, x, gy, (const float*)nullptr, n, n_pad / 16, tps,
-                       partial, P, d, o, lh, h);
+                       (const float*)nullptr, (const float*)nullptr, x, gy, (const float*)nullptr, (const float*)nullptr, n,
+                       n_pad / 16, tps, partial, P, d, o, lh, h);
 }
 
 void launch_small_w3(dim3 grid, hipStream_t st, const float* At, const float* D, const float* Dt, const float* AL,
-                     const float* x, const float* v, const float* gy, int64_t n, int64_t n_pad, int64_t tps,
-                     float* partial, int64_t P, int d, int o, int lh) {
+                     const float* x, const float* v, const float* gy, const float* u, int64_t n, int64_t n_pad,
+                     int64_t tps, float* partial, int64_t P, int d, int o, int lh) {
     hipLaunchKernelGGL(edge_kernel<EDGE_W3>, grid, dim3(THREADS), 0, st, D, At + (int64_t)lh * n_pad * H, Dt, AL, x, v,
-                       gy, n, n_pad / 16, tps, partial, P, d, o, lh, H);
+                       gy, u, n, n_pad / 16, tps, partial, P, d, o, lh, H);
 }
 
 void launch_small_jet(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x,
                       const float* glap, int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d,
                       int o, int lh) {
     hipLaunchKernelGGL(edge_kernel<EDGE_JET>, grid, dim3(THREADS), 0, st, dbuf, abuf + (int64_t)lh * 4 * n_pad * H,
-                       (const float*)nullptr, (const float*)nullptr, x, glap, (const float*)nullptr, n, n_pad / 4, tps,
+                       (const float*)nullptr, (const float*)nullptr, x, glap, (const float*)nullptr, (const float*)nullptr,
+                       n, n_pad / 4, tps,
                        partial, P, d, o, lh, H);
 }
 

@@ -6,10 +6,10 @@
 namespace siren {
 
 void launch_w3(bool theta, dim3 grid, hipStream_t st, const float* ws, const float* x, const float* v, const float* gy,
-               int64_t n, float* gx, float* spill, float* A, float* At, float* D, float* Dt, int64_t n_pad, int d, int lh,
+               const float* u, float* ydot, int o, int64_t n, float* gx, float* spill, float* A, float* At, float* D, float* Dt, int64_t n_pad, int d, int lh,
                float w0, float w) {
 #define SIREN_L(LHV, TH)                                                                                      \
-    hipLaunchKernelGGL((w3_kernel<LHV, TH>), grid, dim3(THREADS), 0, st, ws, x, v, gy, n, gx, spill, A, At, D, Dt, n_pad, \
+    hipLaunchKernelGGL((w3_kernel<LHV, TH>), grid, dim3(THREADS), 0, st, ws, x, v, gy, u, ydot, o, n, gx, spill, A, At, D, Dt, n_pad, \
                        d, w0, w)
     if (theta) {
         switch (lh) {

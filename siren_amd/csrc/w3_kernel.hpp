@@ -1,4 +1,4 @@
-// w3_kernel.hpp — second-order adjoint of the SIREN (work unit W3), d_out == 1, for gfx950.
+// w3_kernel.hpp — second-order adjoint of the SIREN (work unit W3) for gfx950.
 //
 // What autograd asks of the graph node J(x; theta) = dPhi/dx when a loss depends on the gradient
 // (loss_functions.py:84-89 gradients_mse, :214-238 sdf; and every divergence() call inside laplace,
@@ -15,8 +15,12 @@
 //       adb_{l-1} = W_l^T zdb_l,  ab_{l-1} = W_l^T zb_l,  gx = W0^T zb_0
 //   weight gradients (THETA): dW_l = zdb_l ad_{l-1}^T + zb_l a_{l-1}^T (the split-K wgrad kernel, K = 2N),
 //       db_l = sum zb_l, dW0 = zdb_0 v^T + zb_0 x^T, dWout = sum (ad_L + gy a_L), dbout = sum gy.
-// Optional first-order seed gy (n): the same sweep then returns the gradient of sum_c gy_c y_c + <v_c, J(x_c)>
+// Optional first-order seed gy (n, o): the same sweep then returns the gradient of sum_c gy_c . y_c + <v_c, J(x_c)>
 // (the sdf loss's value and gradient terms in ONE backward; the first-order adjoint rides in ab, which is linear).
+// Vector outputs (d_out = o > 1, diff_operators.jacobian/hessian, loss_functions.py:112-211): an optional output
+// weighting u (n, o) makes the tangent functional sum_c <v_c, J(x_c)^T u_c> (adb_L = Wout^T u_c; u == NULL means
+// all ones, i.e. J = sum_j dPhi_j/dx as diff_operators.gradient records it), and the optional output ydot (n, o) is
+// the forward tangent J(x_c) v_c = d/du of that functional (the gy-cotangent of a vjp node).
 // (c_l, zd_l, a_l) of every layer go to a per-wave spill area in HBM in the forward sweep and come back in the
 // reverse sweep (coalesced 1 KiB per block; a WG's 768 KiB usually still sits in the 256 MiB Infinity Cache).
 // Same weight stream (packed forward + transposed slices) and 3-slot LDS ring as the W1 kernels.
@@ -69,6 +73,7 @@ __device__ __forceinline__ f32x4* spill_at(float* wave_spill, int l, int q, int 
 template <int LH, bool THETA>
 __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict__ ws, const float* __restrict__ x,
                                                         const float* __restrict__ v, const float* __restrict__ gy,
+                                                        const float* __restrict__ u, float* __restrict__ ydot, int o,
                                                         int64_t n, float* __restrict__ gx,
                                                         float* __restrict__ spill, float* __restrict__ A,
                                                         float* __restrict__ At, float* __restrict__ D,
@@ -168,16 +173,42 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
         }
     }
 
-    // ---- reverse: seed at layer L (adb_L = Wout^T, ab_L = gy Wout^T; gy = 0 without a first-order seed) -------
-    const float gyv = (gy != nullptr && valid) ? gy[coord] : 0.f;
+    // ---- ydot = Wout ad_L (the forward tangent of y along v) ---------------------------------------------------
+    if (ydot != nullptr) {
+        for (int j = 0; j < o; ++j) {
+            float p = 0.f;
+#pragma unroll
+            for (int rb = 0; rb < NB; ++rb) {
+                const f32x4 wj = *(const f32x4*)(sm + SM_WO + j * H + 16 * rb + 4 * g);
+                p += wj[0] * actt[rb][0] + wj[1] * actt[rb][1] + wj[2] * actt[rb][2] + wj[3] * actt[rb][3];
+            }
+            p = sum_groups(p);
+            if (valid && g == 0) ydot[coord * o + j] = p;
+        }
+    }
+    // ---- reverse: seed at layer L (adb_L = Wout^T u, ab_L = Wout^T gy; u = ones when NULL, gy = 0 when NULL) ----
+    float gyv[MAXO], uv[MAXO];
+#pragma unroll
+    for (int j = 0; j < MAXO; ++j) {
+        gyv[j] = (gy != nullptr && valid && j < o) ? gy[coord * o + j] : 0.f;
+        uv[j] = (u != nullptr && valid && j < o) ? u[coord * o + j] : 0.f;
+    }
 #pragma unroll
     for (int rb = 0; rb < NB; ++rb) {
-        const f32x4 adb = *(const f32x4*)(sm + SM_SEED + 16 * rb + 4 * g);
+        f32x4 adb = *(const f32x4*)(sm + SM_SEED + 16 * rb + 4 * g);
+        f32x4 abseed = {0.f, 0.f, 0.f, 0.f};
+        if (u != nullptr) adb = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < MAXO; ++j) {
+            const f32x4 wj = *(const f32x4*)(sm + SM_WO + j * H + 16 * rb + 4 * g);  // zero rows for j >= o
+            abseed = abseed + gyv[j] * wj;
+            if (u != nullptr) adb = adb + uv[j] * wj;
+        }
         const f32x4 cs = *spill_at(wsp, LH, 0, rb, lane);
         const f32x4 zd = *spill_at(wsp, LH, 1, rb, lane);
         const f32x4 sn = *spill_at(wsp, LH, 2, rb, lane);
         actt[rb] = (w * cs) * adb;
-        actp[rb] = (w * cs) * (gyv * adb) - (w * w) * sn * zd * adb;
+        actp[rb] = (w * cs) * abseed - (w * w) * sn * zd * adb;
         if (THETA) {
             store_block(D + LH * lstride + toff, rb, actp[rb]);
             store_block(Dt + LH * lstride + toff, rb, actt[rb]);

@@ -37,7 +37,8 @@ def laplace(y, x):
 def jacobian(y, x):
     """(B, N, out, in) Jacobian and a NaN status flag (diff_operators.py:46-59)."""
     b, n = y.shape[:2]
-    jac = torch.zeros(b, n, y.shape[-1], x.shape[-1], device=y.device, dtype=y.dtype)
+    # the reference's buffer has the default dtype (diff_operators.py:49), so an fp64 graph is rounded to fp32 here
+    jac = torch.zeros(b, n, y.shape[-1], x.shape[-1], device=y.device)
     for i in range(y.shape[-1]):
         y_flat = y[..., i].view(-1, 1)
         jac[:, :, i, :] = grad(y_flat, x, torch.ones_like(y_flat), create_graph=True)[0]
@@ -49,7 +50,7 @@ def hessian(y, x):
     """(B, N, out, in, in) Hessian and a NaN status flag (diff_operators.py:5-24)."""
     b, n = y.shape[:2]
     grad_y = torch.ones_like(y[..., 0])
-    h = torch.zeros(b, n, y.shape[-1], x.shape[-1], x.shape[-1], device=y.device, dtype=y.dtype)
+    h = torch.zeros(b, n, y.shape[-1], x.shape[-1], x.shape[-1], device=y.device)  # default dtype, as :12
     for i in range(y.shape[-1]):
         dydx = grad(y[..., i], x, grad_y, create_graph=True)[0]
         for j in range(x.shape[-1]):

@@ -42,12 +42,12 @@ class SirenEngine:
         self.ws_floats = cnt.value if self.supported else 0
         # hidden 256 keeps cos(w z_l) of every layer in registers (1..3 hidden layers); hidden 512 spills it
         self.grad_supported = self.supported and (1 <= n_hidden <= 3 or int(hidden) == 512)
-        # the W3 second-order kernel: hidden 256, scalar output, linear output layer
+        # the W3 second-order kernel: hidden 256, d_out <= 4 (vector outputs via an output weighting), linear output
         # the W4 jet kernel (fused Laplacian): hidden 256, d_in <= 2, linear output, 1..5 hidden layers
         self.laplace_supported = (self.supported and int(hidden) == 256 and int(d_in) <= 2 and 1 <= n_hidden <= 5
                                   and bool(outermost_linear) and omega_first != 0 and omega_hidden != 0)
         self.second_order_supported = (self.supported and int(hidden) == 256 and 1 <= n_hidden <= 3
-                                       and int(d_out) == 1 and bool(outermost_linear))
+                                       and int(d_out) <= 4 and bool(outermost_linear))
 
     # ------------------------------------------------------------------------------------------------------
     def _require(self):
@@ -180,30 +180,33 @@ class SirenEngine:
                    'siren_backward')
         return gx, gp
 
-    def second_order(self, ws, x, v, want_theta=True, gy=None):
-        """W3: (H v, d/dtheta sum <v, dPhi/dx>) for d_out == 1 — the backward of the dPhi/dx graph node
-        (gradients_mse / sdf / divergence). With a first-order seed gy (n, 1) the same sweep returns the gradient of
-        sum gy*y + <v, dPhi/dx> (siren_second_order_seeded). Returns (gx, gparams or None)."""
+    def second_order(self, ws, x, v, want_theta=True, gy=None, u=None, want_ydot=False):
+        """W3: the backward of the vjp node gx = J^T u (u (n, d_out), None = ones, i.e. diff_operators.gradient's
+        dPhi/dx) given its cotangent v (n, d_in): H v and d/dtheta of F = sum <v, J^T u> (+ sum gy . y with a
+        first-order seed gy (n, d_out)) in ONE sweep (siren_second_order_ex). Returns (gx, gparams or None), plus
+        ydot = J v (n, d_out) = dF/du when want_ydot."""
         self._require()
         if not self.second_order_supported:
-            raise _lib.SirenUnsupported('siren_second_order covers hidden 256, d_out == 1, linear output, '
+            raise _lib.SirenUnsupported('siren_second_order covers hidden 256, d_out <= 4, linear output, '
                                         '1..3 hidden layers')
         x = self._check_x(x)
-        n = x.shape[0]
+        n, o = x.shape[0], self.cfg.d_out
         v = v.contiguous()
         if v.shape != x.shape or v.dtype != torch.float32 or v.device != x.device:
             raise ValueError('v must be fp32 %s on %s' % (tuple(x.shape), x.device))
-        if gy is not None:
-            gy = gy.contiguous()
-            if gy.numel() != n or gy.dtype != torch.float32 or gy.device != x.device:
-                raise ValueError('gy must be fp32 with %d values on %s' % (n, x.device))
+        for name, t in (('gy', gy), ('u', u)):
+            if t is not None and (t.numel() != n * o or t.dtype != torch.float32 or t.device != x.device):
+                raise ValueError('%s must be fp32 with %d values on %s' % (name, n * o, x.device))
+        gy = gy.contiguous() if gy is not None else None
+        u = u.contiguous() if u is not None else None
         cnt = ctypes.c_int64()
         _lib.check(self.lib.siren_second_order_ws_floats(ctypes.byref(self.cfg), n, 1 if want_theta else 0,
                                                          ctypes.byref(cnt)), 'siren_second_order_ws_floats')
         tws = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
         gx = torch.empty(n, self.cfg.d_in, dtype=torch.float32, device=x.device)
         gp = torch.empty(self.param_count, dtype=torch.float32, device=x.device) if want_theta else None
-        _lib.check(self.lib.siren_second_order_seeded(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(v), _ptr(gy),
-                                                      _ptr(tws), _ptr(gx), _ptr(gp), _stream(x.device)),
-                   'siren_second_order_seeded')
-        return gx, gp
+        ydot = torch.empty(n, o, dtype=torch.float32, device=x.device) if want_ydot else None
+        _lib.check(self.lib.siren_second_order_ex(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(v), _ptr(u),
+                                                  _ptr(gy), _ptr(tws), _ptr(gx), _ptr(gp), _ptr(ydot),
+                                                  _stream(x.device)), 'siren_second_order_ex')
+        return (gx, gp, ydot) if want_ydot else (gx, gp)

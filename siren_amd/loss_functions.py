@@ -43,3 +43,84 @@ def sdf(model_output, gt):
             'inter': inter_constraint.mean() * 1e2,
             'normal_constraint': normal_constraint.mean() * 1e2,
             'grad_constraint': grad_constraint.mean() * 5e1}
+
+
+def wave_pml(model_output, gt):
+    """Wave-equation loss (loss_functions.py:112-136): Dirichlet + Neumann terms on the t = 0 set and the residual
+    u_tt - c^2 (u_xx + u_yy) elsewhere. x = (t, x, y). The second derivatives are jacobian-of-jacobian: with
+    siren_amd models both sweeps run on the HIP kernels (W1 vjp nodes, then the W3 kernel's vector-output form)."""
+    from .diff_operators import jacobian
+    sbv = gt['source_boundary_values']
+    x, y = model_output['model_in'], model_output['model_out']
+    slowness, mask = gt['squared_slowness'], gt['dirichlet_mask']
+    batch_size = x.shape[1]
+    du, _ = jacobian(y, x)
+    dudt = du[..., 0]
+    if torch.all(mask):
+        diff_hom = torch.zeros(1, device=y.device, dtype=y.dtype)
+    else:
+        hess, _ = jacobian(du[..., 0, :], x)
+        lap = hess[..., 1, 1, None] + hess[..., 2, 2, None]
+        diff_hom = hess[..., 0, 0, None] - 1 / slowness * lap
+    dirichlet = y[mask] - sbv[mask]
+    neumann = dudt[mask]
+    return {'dirichlet': torch.abs(dirichlet).sum() * batch_size / 1e1,
+            'neumann': torch.abs(neumann).sum() * batch_size / 1e2,
+            'diff_constraint_hom': torch.abs(diff_hom).sum()}
+
+
+def helmholtz_pml(model_output, gt):
+    """Helmholtz loss with a perfectly matched layer (loss_functions.py:139-211): complex field y = (re, im) per
+    source, PML stretch factors ex, ey over the outer 0.5 of [-1, 1]^2, residual
+    d/dx1 (ey/ex du/dx1) + d/dx2 (ex/ey du/dx2) + ex ey k^2 m u  (m = squared slowness), split into the source set
+    and the rest; the 'pretrain' / full-waveform-inversion variants follow the reference's branches."""
+    from .diff_operators import jacobian
+    from .modules import compl_div, compl_mul
+    sbv = gt['source_boundary_values']
+    rec = gt.get('rec_boundary_values')
+    k = gt['wavenumber'].float().to(model_output['model_out'].dtype)
+    x, y = model_output['model_in'], model_output['model_out']
+    slowness = gt['squared_slowness'].repeat(1, 1, y.shape[-1] // 2)
+    batch_size = x.shape[1]
+    fwi = False
+    pred_slowness = None
+    if 'pretrain' in gt:
+        pred_slowness = y[:, :, -1] + 1.
+        if torch.all(gt['pretrain'] == -1):
+            fwi = True
+            pred_slowness = torch.clamp(y[:, :, -1], min=-0.999) + 1.
+            init = torch.stack((torch.ones_like(pred_slowness), torch.zeros_like(pred_slowness)), dim=-1)
+            slowness = torch.stack((pred_slowness, torch.zeros_like(pred_slowness)), dim=-1)
+            outer = (torch.abs(x[..., 0, None]) > 0.75) | (torch.abs(x[..., 1, None]) > 0.75)
+            slowness = torch.where(outer, init, slowness)
+        y = y[:, :, :-1]
+    du, _ = jacobian(y, x)
+    dudx1, dudx2 = du[..., 0], du[..., 1]
+    a0, lpml = 5.0, 0.5
+    d_w = -torch.clamp(x[..., 0] + (1.0 - lpml), max=0)
+    d_e = torch.clamp(x[..., 0] - (1.0 - lpml), min=0)
+    d_s = -torch.clamp(x[..., 1] + (1.0 - lpml), max=0)
+    d_n = torch.clamp(x[..., 1] - (1.0 - lpml), min=0)
+    sx = k * a0 * ((d_w / lpml) ** 2 + (d_e / lpml) ** 2)[..., None]
+    sy = k * a0 * ((d_n / lpml) ** 2 + (d_s / lpml) ** 2)[..., None]
+    ex = torch.cat((torch.ones_like(sx), -sx / k), dim=-1)
+    ey = torch.cat((torch.ones_like(sy), -sy / k), dim=-1)
+    reps = dudx1.shape[-1] // 2
+    A = compl_div(ey, ex).repeat(1, 1, reps)
+    B = compl_div(ex, ey).repeat(1, 1, reps)
+    C = compl_mul(ex, ey).repeat(1, 1, reps)
+    a, _ = jacobian(compl_mul(A, dudx1), x)
+    b, _ = jacobian(compl_mul(B, dudx2), x)
+    c = compl_mul(compl_mul(C, slowness), k ** 2 * y)
+    diff_hom = a[..., 0] + b[..., 1] + c
+    on = torch.where(sbv != 0., diff_hom - sbv, torch.zeros_like(diff_hom))
+    off = torch.where(sbv == 0., diff_hom, torch.zeros_like(diff_hom))
+    if fwi:
+        data_term = torch.where(rec != 0, y - rec, torch.zeros_like(y))
+    elif pred_slowness is not None:
+        data_term = pred_slowness - slowness[..., 0]
+    else:
+        data_term = torch.zeros(1, device=y.device, dtype=y.dtype)
+    return {'diff_constraint_on': torch.abs(on).sum() * batch_size / 1e3,
+            'diff_constraint_off': torch.abs(off).sum(),
+            'data_term': torch.abs(data_term).sum() * batch_size / 1}

@@ -377,3 +377,31 @@ class Siren(nn.Module):
             activations['_'.join((str(layer.__class__), '%d' % count))] = x
             count += 1
         return activations
+
+
+# ----------------------------------------------------------------------------------------------------------
+# Complex helpers of the PML losses (modules.py:636-673): a complex field is stored as interleaved channels
+# (re_0, im_0, re_1, im_1, ...) along the last dimension.
+# ----------------------------------------------------------------------------------------------------------
+def _interleave(re, im):
+    return torch.stack((re, im), dim=-1).flatten(-2)
+
+
+def compl_conj(x):
+    """Complex conjugate: negate the odd (imaginary) channels."""
+    return _interleave(x[..., ::2], -x[..., 1::2])
+
+
+def compl_div(x, y):
+    """x / y channel-pair-wise: ((ac + bd) + i (bc - ad)) / (c^2 + d^2)."""
+    a, b, c, d = x[..., ::2], x[..., 1::2], y[..., ::2], y[..., 1::2]
+    den = c ** 2 + d ** 2
+    return _interleave((a * c + b * d) / den, (b * c - a * d) / den)
+
+
+def compl_mul(x, y):
+    """x * y channel-pair-wise; the imaginary part uses the reference's three-multiplication form
+    (a + b)(c + d) - ac - bd, so the rounding matches."""
+    a, b, c, d = x[..., ::2], x[..., 1::2], y[..., ::2], y[..., 1::2]
+    ac, bd = a * c, b * d
+    return _interleave(ac - bd, (a + b) * (c + d) - ac - bd)

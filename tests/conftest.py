@@ -67,3 +67,21 @@ def weights_of(fx):
 
 def g1_layers(fx):
     return weights_of(fx)[1]
+
+
+@pytest.fixture(scope='session')
+def g6():
+    return load_golden('g6')
+
+
+def pml_case(g6, tag):
+    """(coords (1, n, d), gt dict, flat params, layers) of the G6 Helmholtz ('H') or wave ('W') case."""
+    sub = {k[len(tag) + 1:]: v for k, v in g6.items() if k.startswith(tag + '_')}
+    gt = {k[3:]: v for k, v in sub.items() if k.startswith('gt_')}
+    flat, layers = weights_of(sub)
+    return sub['coords'], gt, flat, layers
+
+
+def pml_ref_grads(g6, tag):
+    keys = ['net.net.%d.0.%s' % (i, k) for i in range(5) for k in ('weight', 'bias')]
+    return np.concatenate([g6['%s_grad_%s' % (tag, k)].reshape(-1) for k in keys])

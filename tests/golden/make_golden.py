@@ -16,8 +16,11 @@ Fixtures:
   G3  5x256 d3 o1 SDF batch (sphere, 2048 on + 2048 off surface): the four `sdf` loss terms and theta-grads.
   G4  5x512 d3 o3, 1024 coords: model_out and image_mse theta-grads.
   G5  config-1 trajectory: 256^2 synthetic image, 300 full-batch Adam steps (lr 1e-4), loss every 10 steps, PSNR.
+  G6  vector outputs / PML losses: 5x256 d2 o2 (helmholtz_pml, loss_functions.py:139-211)
+      and 5x256 d3 o1 (wave_pml, loss_functions.py:112-136), 1024 coords each: jacobian / hessian
+      (diff_operators.py:5-24, 46-59), the loss terms and their fp64 theta-grads.
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--skip-fit]
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--skip-fit] [--only-g6]
 """
 import argparse
 import json
@@ -107,10 +110,84 @@ def fixture_outputs(modules, D, L, net, coords, targets, prefix, store, meta, lo
         meta[f'{prefix}_{name}_f64_maxabs'] = float(np.max(np.abs(a64)))
 
 
+def pml_batch(d, n, seed):
+    """Synthetic PML inputs with the layouts of dataio.SingleHelmholtzSource / WaveSource (dataio.py:208-380): coords
+    U[-1,1]^d with the last 128 points near the source at the origin, a Gaussian source (complex (re, im) for
+    Helmholtz; (n, 1) for the wave equation, with the t = 0 slice as the Dirichlet set)."""
+    gen = torch.Generator().manual_seed(seed)
+    c = torch.rand(n, d, generator=gen, dtype=torch.float64) * 2 - 1
+    c[-128:, d - 2:] = torch.randn(128, 2, generator=gen, dtype=torch.float64) * 0.05
+    r2 = (c[:, d - 2:] ** 2).sum(-1, keepdim=True)
+    g = torch.exp(-r2 / (2 * 0.05 ** 2))
+    g = torch.where(g > 1e-3, g, torch.zeros_like(g))
+    return c, g
+
+
+def make_g6(modules, D, L, meta):
+    store = {}
+    # Helmholtz: 5x256 d2 o2 (real, imaginary), wavenumber 20, homogeneous medium
+    c2, g2 = pml_batch(2, 1024, 6)
+    coords = c2.float()[None]
+    gt = {'source_boundary_values': torch.cat([g2, 0.5 * g2], -1).float()[None],
+          'squared_slowness': torch.cat([torch.ones(1024, 1), torch.zeros(1024, 1)], -1)[None],
+          'wavenumber': torch.tensor([[20.]])}
+    store.update({'H_coords': coords.numpy(), **{'H_gt_' + k: v.numpy() for k, v in gt.items()}})
+    torch.manual_seed(6)
+    net = modules.SingleBVPNet(type='sine', in_features=2, out_features=2)
+    for k, v in state_to_np(net.state_dict()).items():
+        store['H_w_' + k] = v
+    net = net.double()
+    out = net({'coords': coords.double()})
+    jac, _ = D.jacobian(out['model_out'], out['model_in'])
+    hes, _ = D.hessian(out['model_out'], out['model_in'])
+    store['H_model_out_f64'] = out['model_out'].detach().numpy()
+    store['H_jacobian_f64'] = jac.detach().numpy()
+    store['H_hessian_f64'] = hes.detach().numpy()
+    ld = L.helmholtz_pml(out, {k: v.double() for k, v in gt.items()})
+    for k, v in ld.items():
+        meta[f'G6_helmholtz_{k}_f64'] = float(v.sum())
+    grads, total = grads_of(net, ld)
+    meta['G6_helmholtz_total_f64'] = total
+    for k, v in grads.items():
+        store[f'H_grad_{k}'] = v
+    # wave: 5x256 d3 (t, x, y) o1; t = 0 slice is the Dirichlet set carrying the initial Gaussian
+    c3, g3 = pml_batch(3, 1024, 7)
+    c3[:256, 0] = 0.
+    c3[-128:, 0] = 0.
+    mask = c3[:, :1] == 0.
+    coords = c3.float()[None]
+    gt = {'source_boundary_values': torch.where(mask, g3, torch.zeros_like(g3)).float()[None],
+          'squared_slowness': torch.ones(1, 1024, 1), 'dirichlet_mask': mask[None]}
+    store.update({'W_coords': coords.numpy(), **{'W_gt_' + k: v.numpy() for k, v in gt.items()}})
+    torch.manual_seed(7)
+    net = modules.SingleBVPNet(type='sine', in_features=3, out_features=1)
+    for k, v in state_to_np(net.state_dict()).items():
+        store['W_w_' + k] = v
+    net = net.double()
+    out = net({'coords': coords.double()})
+    ld = L.wave_pml(out, {k: (v.double() if v.dtype != torch.bool else v) for k, v in gt.items()})
+    for k, v in ld.items():
+        meta[f'G6_wave_{k}_f64'] = float(v.sum())
+    grads, total = grads_of(net, ld)
+    meta['G6_wave_total_f64'] = total
+    for k, v in grads.items():
+        store[f'W_grad_{k}'] = v
+    np.savez_compressed(os.path.join(OUT, 'golden_g6.npz'), **store)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--skip-fit', action='store_true', help='reuse the G5 weights already in golden_fit.npz')
+    ap.add_argument('--only-g6', action='store_true', help='add G6 to the existing fixtures and manifest')
     args = ap.parse_args()
+    if args.only_g6:
+        modules, D, L = import_reference()
+        with open(os.path.join(OUT, 'manifest.json')) as f:
+            meta = json.load(f)
+        make_g6(modules, D, L, meta)
+        with open(os.path.join(OUT, 'manifest.json'), 'w') as f:
+            json.dump(meta, f, indent=1, sort_keys=True)
+        return
     modules, D, L = import_reference()
     torch.set_num_threads(os.cpu_count())
     meta = {'torch': torch.__version__, 'generated_by': 'tests/golden/make_golden.py', 'reference': REF}
