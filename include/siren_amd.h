@@ -171,6 +171,27 @@ int32_t siren_second_order_ex(const siren_cfg* cfg, const float* ws, const float
 int32_t siren_w1_phase_profile(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y, float* gx,
                                uint64_t* stamps, void* stream);
 
+/* ---- per-step kernels around the network ---------------------------------------------
+ * Device-side dataio.PointCloud.__getitem__ (dataio.py:420-442): from a resident point cloud pc_coords /
+ * pc_normals (m, 3), write 2k samples: rows [0, k) = k on-surface points drawn uniformly with replacement (coords,
+ * normals, sdf 0), rows [k, 2k) = k off-surface points uniform in [-1, 1)^3 (normals -1, sdf -1). coords, normals
+ * (2k, 3), sdf (2k, 1). A counter RNG of (seed, step, row) (step_kernels.hpp) replaces np.random: reproducible
+ * for a given (seed, step), nothing crosses PCIe (training.py:53-54). */
+int32_t siren_sample_sdf(const float* pc_coords, const float* pc_normals, int64_t m, int64_t k, uint64_t seed,
+                         uint64_t step, float* coords, float* normals, float* sdf, void* stream);
+
+/* fp32 values of device scratch siren_adam_step needs when clipping (per-block norm partials + the norm). */
+int32_t siren_adam_scratch_floats(int64_t* count);
+
+/* torch.nn.utils.clip_grad_norm_(max_norm) + torch.optim.Adam.step (training.py:17, 98-104; amsgrad off, no weight
+ * decay) over ONE flat fp32 bucket of n parameters: c = min(1, max_norm / (||g|| + 1e-6)) (no clip when
+ * max_norm <= 0), m = b1 m + (1 - b1) c g, v = b2 v + (1 - b2) (c g)^2, p -= lr / (1 - b1^step) * m /
+ * (sqrt(v / (1 - b2^step)) + eps). step >= 1 is Adam's step count after this update. The global norm stays on the
+ * device (scratch[1024] receives it); buffers 16-byte aligned. */
+int32_t siren_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, float lr,
+                        float beta1, float beta2, float eps, int64_t step, float max_norm, float* scratch,
+                        void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -15,6 +15,11 @@ Two restatements of xvdp/siren (/root/reference, read as text only):
   (loss_functions.py:8-12 image_mse, :84-89 gradients_mse, :104-109 laplace_mse, :214-238 sdf) and as the
   "reference CPU path" that bench.py times on the GPU box's host cores (cpu_baseline, kind "port").
 
+* per-step work: sample_sdf restates the device PointCloud sampler (dataio.py:420-442)
+  with the engine's counter RNG — bit-exact, but "parity unpinned" against the reference, whose np.random draws
+  have no golden; adam_steps restates torch.optim.Adam + clip_grad_norm_ (training.py:17, 98-104), pinned on the
+  GPU box against torch's own implementation (tests/test_gpu_step.py).
+
 Parity is pinned: tests/test_oracle.py checks both restatements against the golden vectors that
 tests/golden/make_golden.py produced by running the reference itself.
 """
@@ -201,3 +206,50 @@ def torch_param_grads(name, x, layers, gt, dtype='float64', **kw):
     grads = torch.autograd.grad(total, params, allow_unused=True)
     grads = [torch.zeros_like(p) if g is None else g for g, p in zip(grads, params)]
     return np.concatenate([g.detach().numpy().reshape(-1) for g in grads]), float(total)
+
+
+# ----------------------------------------------------------------------------------------------------------
+# per-step work: the device sampler's counter RNG and Adam + clip, restated
+# ----------------------------------------------------------------------------------------------------------
+_M64 = (1 << 64) - 1
+
+
+def _mix64(z):
+    z = (z + 0x9E3779B97F4A7C15) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def _rng64(seed, step, i):
+    return _mix64((_mix64(seed ^ _mix64(step)) + i) & _M64)
+
+
+def sample_sdf(pc, pn, k, seed, step):
+    """dataio.PointCloud.__getitem__ (dataio.py:420-442) with the counter RNG of siren_sample_sdf
+    (siren_amd/csrc/step_kernels.hpp): rows [0, k) = pc/pn[floor(r m / 2^64)], sdf 0; rows [k, 2k) = uniform
+    2 u - 1 with u = (r >> 40) 2^-24, normals -1, sdf -1. Exact (integer arithmetic, fp32-exact floats)."""
+    m = pc.shape[0]
+    idx = np.array([(_rng64(seed, step, i) * m) >> 64 for i in range(k)], dtype=np.int64)
+    u = np.array([[_rng64(seed, step, k + 3 * j + q) >> 40 for q in range(3)] for j in range(k)], dtype=np.float64)
+    off = (2. * (u * 2. ** -24) - 1.).astype(np.float32)
+    coords = np.concatenate([pc[idx], off], 0).astype(np.float32)
+    normals = np.concatenate([pn[idx], -np.ones((k, 3), np.float32)], 0).astype(np.float32)
+    sdf = np.concatenate([np.zeros((k, 1), np.float32), -np.ones((k, 1), np.float32)], 0)
+    return coords, normals, sdf, idx
+
+
+def adam_steps(p, grads, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, max_norm=None):
+    """torch.optim.Adam (amsgrad off, no weight decay) after clip_grad_norm_ (training.py:17, 98-104), fp64, over a
+    flat vector for a sequence of gradients; returns the final parameters."""
+    p = np.array(p, np.float64)
+    m = np.zeros_like(p)
+    v = np.zeros_like(p)
+    for t, g in enumerate(grads, 1):
+        g = np.array(g, np.float64)
+        if max_norm:
+            g = g * min(1., max_norm / (np.sqrt(np.sum(g * g)) + 1e-6))
+        m = m + (1 - betas[0]) * (g - m)
+        v = betas[1] * v + (1 - betas[1]) * g * g
+        p = p - lr / (1 - betas[0] ** t) * m / (np.sqrt(v) / np.sqrt(1 - betas[1] ** t) + eps)
+    return p

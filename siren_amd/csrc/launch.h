@@ -55,4 +55,11 @@ void launch_small(dim3 grid, hipStream_t st, const float* abuf, const float* dbu
 void launch_reduce(dim3 grid, hipStream_t st, const float* partial, int64_t S, int64_t P, float* gp, int64_t S2,
                    int64_t lo, int64_t hi);
 
+constexpr int STEP_BLOCKS = 1024;  // partial sums of the clip-norm pass (4 workgroups per CU)
+// tu_step.hip: device point-cloud sampling (dataio.py:420-442), clip_grad_norm_ + Adam over the flat bucket
+void launch_sample_sdf(hipStream_t st, const float* pc, const float* pn, int64_t m, int64_t k, uint64_t seed,
+                       uint64_t step, float* coords, float* normals, float* sdf);
+void launch_adam(hipStream_t st, float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
+                 float eps, float bc1, float bc2, float max_norm, float* scratch);
+
 }  // namespace siren

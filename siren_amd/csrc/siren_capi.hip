@@ -438,4 +438,38 @@ int32_t siren_second_order_ex(const siren_cfg* cfg, const float* ws, const float
     return hip_status("siren_second_order (reduce)");
 }
 
+// ---- per-step kernels -------------------------------------------------------------------
+int32_t siren_sample_sdf(const float* pc_coords, const float* pc_normals, int64_t m, int64_t k, uint64_t seed,
+                         uint64_t step, float* coords, float* normals, float* sdf, void* stream) {
+    if (m <= 0 || k < 0) return fail(SIREN_EINVAL, "siren_sample_sdf: need m > 0 and k >= 0");
+    if (k == 0) return SIREN_OK;
+    if (pc_coords == nullptr || pc_normals == nullptr || coords == nullptr || normals == nullptr || sdf == nullptr)
+        return fail(SIREN_EINVAL, "siren_sample_sdf: NULL pointer");
+    siren::launch_sample_sdf((hipStream_t)stream, pc_coords, pc_normals, m, k, seed, step, coords, normals, sdf);
+    return hip_status("siren_sample_sdf");
+}
+
+int32_t siren_adam_scratch_floats(int64_t* count) {
+    if (count == nullptr) return fail(SIREN_EINVAL, "count is NULL");
+    *count = siren::STEP_BLOCKS + 4;
+    return SIREN_OK;
+}
+
+int32_t siren_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, float lr,
+                        float beta1, float beta2, float eps, int64_t step, float max_norm, float* scratch,
+                        void* stream) {
+    if (n < 0 || step < 1) return fail(SIREN_EINVAL, "siren_adam_step: need n >= 0 and step >= 1");
+    if (n == 0) return SIREN_OK;
+    if (params == nullptr || grads == nullptr || exp_avg == nullptr || exp_avg_sq == nullptr ||
+        (max_norm > 0.f && scratch == nullptr))
+        return fail(SIREN_EINVAL, "siren_adam_step: NULL pointer");
+    const uintptr_t al = (uintptr_t)params | (uintptr_t)grads | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq;
+    if ((al & 15) != 0) return fail(SIREN_EINVAL, "siren_adam_step: buffers must be 16-byte aligned");
+    // bias corrections in double on the host (torch computes 1 - beta ** step in Python floats)
+    const double bc1 = 1.0 - std::pow((double)beta1, (double)step), bc2 = 1.0 - std::pow((double)beta2, (double)step);
+    siren::launch_adam((hipStream_t)stream, params, grads, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, (float)bc1,
+                       (float)bc2, max_norm, scratch);
+    return hip_status("siren_adam_step");
+}
+
 }  // extern "C"

@@ -20,6 +20,10 @@ class _NullWriter:
         pass
 
 
+def _host(losses):
+    return torch.stack([torch.as_tensor(v).float().cpu() for v in losses]).numpy() if losses else np.zeros(0)
+
+
 def _writer(summaries_dir):
     try:
         from torch.utils.tensorboard import SummaryWriter
@@ -30,12 +34,15 @@ def _writer(summaries_dir):
 
 def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_checkpoint, model_dir, loss_fn,
           summary_fn=None, val_dataloader=None, double_precision=False, clip_grad=False, use_lbfgs=False,
-          loss_schedules=None, device='cuda', log=print, writer=None):
+          loss_schedules=None, device='cuda', log=print, writer=None, fused_adam=False):
     if double_precision:
         raise NotImplementedError('siren_amd computes in fp32 (the reference default)')
     if use_lbfgs:
         optim = torch.optim.LBFGS(lr=lr, params=model.parameters(), max_iter=50000, max_eval=50000,
                                   history_size=50, line_search_fn='strong_wolfe')
+    elif fused_adam:  # clip + Adam in two HIP launches over one flat bucket, norm kept on the device (optim.py)
+        from .optim import FusedAdam
+        optim = FusedAdam(model.parameters(), lr=lr, max_norm=(1. if clip_grad is True else clip_grad) or None)
     else:
         optim = torch.optim.Adam(lr=lr, params=model.parameters())
     checkpoints_dir = os.path.join(model_dir, 'checkpoints')
@@ -60,7 +67,7 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
     for epoch in range(epochs):
         if not epoch % epochs_til_checkpoint and epoch and rank == 0:
             torch.save(model.state_dict(), os.path.join(checkpoints_dir, 'model_epoch_%04d.pth' % epoch))
-            np.savetxt(os.path.join(checkpoints_dir, 'train_losses_epoch_%04d.txt' % epoch), np.array(train_losses))
+            np.savetxt(os.path.join(checkpoints_dir, 'train_losses_epoch_%04d.txt' % epoch), _host(train_losses))
         for model_input, gt in train_dataloader:
             start = time.time()
             model_input = {k: v.to(device) for k, v in model_input.items()}
@@ -74,7 +81,7 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
                     return loss
                 optim.step(closure)
             model_output, train_loss = step_losses(model_input, gt, total_steps)
-            train_losses.append(float(train_loss))
+            train_losses.append(train_loss.detach())  # device scalar: no per-step host sync (training.py:86)
             writer.add_scalar('total_train_loss', train_loss, total_steps)
             if not total_steps % steps_til_summary and rank == 0:
                 torch.save(model.state_dict(), os.path.join(checkpoints_dir, 'model_current.pth'))
@@ -84,14 +91,15 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
                 optim.zero_grad()
                 train_loss.backward()
                 distributed.allreduce_gradients(list(model.parameters()), world)
-                if clip_grad:
+                if clip_grad and not fused_adam:
                     max_norm = 1. if isinstance(clip_grad, bool) else clip_grad
                     torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
                 optim.step()
             if not total_steps % steps_til_summary and rank == 0:
-                log('Epoch %d, Total loss %0.6f, iteration time %0.6f' % (epoch, train_losses[-1], time.time() - start))
+                log('Epoch %d, Total loss %0.6f, iteration time %0.6f' % (epoch, float(train_losses[-1]),
+                                                                           time.time() - start))
             total_steps += 1
     if rank == 0:
         torch.save(model.state_dict(), os.path.join(checkpoints_dir, 'model_final.pth'))
-        np.savetxt(os.path.join(checkpoints_dir, 'train_losses_final.txt'), np.array(train_losses))
-    return train_losses
+        np.savetxt(os.path.join(checkpoints_dir, 'train_losses_final.txt'), _host(train_losses))
+    return [float(v) for v in _host(train_losses)]
