@@ -159,6 +159,54 @@ def config_rates(device, steps=5):
     inp, gt_sdf = dataio.sphere_sdf_batch(1 << 18, device=device)  # 2^18 on + 2^18 off surface = 2^19
     n = inp['coords'].shape[1]
     res['sdf_5x256_d3_train_mcoords_s'] = rate(m, inp['coords'], lambda o: LF.sdf(o, gt_sdf), n)
+    # configs[2] as the reference's loop runs it (train_sdf.py: PointCloud resampled every step, clip_grad):
+    # device sampler (siren_sample_sdf) + fused clip + Adam (siren_adam_step) inside the timed step
+    from siren_amd.optim import FusedAdam
+    g = torch.Generator().manual_seed(0)
+    d = torch.randn(1 << 20, 3, generator=g, dtype=torch.float64)
+    d = d / d.norm(dim=-1, keepdim=True)
+    pcd = dataio.PointCloud(points=torch.cat([d * 0.5, d], 1).numpy(), on_surface_points=1 << 18, device=device)
+    torch.manual_seed(0)
+    m = SingleBVPNet(in_features=3, verbose=False).to(device)
+    fopt = FusedAdam(m.parameters(), lr=1e-4, max_norm=1.)
+
+    def sdf_step(i):
+        inp_i, gt_i = pcd.sample(i)
+        out = m({'coords': inp_i['coords'][None]})
+        total = sum(v.mean() for v in LF.sdf(out, {k: v[None] for k, v in gt_i.items()}).values())
+        fopt.zero_grad()
+        total.backward()
+        fopt.step()
+    sdf_step(0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        sdf_step(1 + i)
+    torch.cuda.synchronize()
+    res['sdf_5x256_d3_train_device_sampling_fused_adam_mcoords_s'] = round(
+        (1 << 19) * steps / (time.perf_counter() - t0) / 1e6, 3)
+    # the per-step kernels alone (HBM-bound): sampler algorithmic bytes = k (index gather: 24 B read) + 2k rows
+    # written (coords 12 + normals 12 + sdf 4 B); Adam = 28 B / parameter (g, m, v, p read; m, v, p written)
+    st = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    ev[0].record(st)
+    for i in range(20):
+        pcd.sample(100 + i)
+    ev[1].record(st)
+    ev[2].record(st)
+    for _ in range(20):
+        fopt.step()
+    ev[3].record(st)
+    torch.cuda.synchronize()
+    k = 1 << 18
+    ms_s, ms_a = ev[0].elapsed_time(ev[1]) / 20, ev[2].elapsed_time(ev[3]) / 20
+    P = sum(p.numel() for p in m.parameters())
+    # (event spans over 20 back-to-back calls: host-launch-inclusive; the kernel-only durations are in the
+    # rocprofv3 summary, profiles/r01_step_kernels_stats.csv)
+    res['step_kernels'] = {'sample_sdf_us_per_call': round(ms_s * 1e3, 2),
+                           'sample_sdf_bytes': 24 * k + 2 * k * 28,
+                           'clip_adam_us_per_call': round(ms_a * 1e3, 2),
+                           'clip_adam_bytes': 28 * P, 'params': P}
     # configs[3]: video fit, 5x512 d3 o3 image_mse (W2 at hidden 512), 2^18 coords per GPU
     torch.manual_seed(0)
     m = SingleBVPNet(in_features=3, out_features=3, hidden_features=512, verbose=False).to(device)

@@ -22,8 +22,9 @@ __host__ __device__ inline uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
+__host__ __device__ inline uint64_t rng_key(uint64_t seed, uint64_t step) { return mix64(seed ^ mix64(step)); }
 __host__ __device__ inline uint64_t rng64(uint64_t seed, uint64_t step, uint64_t i) {
-    return mix64(mix64(seed ^ mix64(step)) + i);
+    return mix64(rng_key(seed, step) + i);
 }
 // 24 high bits -> [0, 1) exactly representable; 2u - 1 in [-1, 1)
 __host__ __device__ inline float unit24(uint64_t h) { return (float)(h >> 40) * 5.9604644775390625e-08f; }
@@ -31,13 +32,14 @@ __host__ __device__ inline float unit24(uint64_t h) { return (float)(h >> 40) * 
 // Counter layout: on-surface point i draws index rng64(seed, step, i); off-surface point i draws its three
 // coordinates from rng64(seed, step, k + 3 i + c), c = 0..2. Index = floor(r * m / 2^64) (multiply-high: unbiased
 // to 2^-64 / m, no modulo).
+// key = rng_key(seed, step), hoisted to the host: one mix64 per random word in the kernel
 __global__ void sample_sdf_kernel(const float* __restrict__ pc, const float* __restrict__ pn, int64_t m, int64_t k,
-                                  uint64_t seed, uint64_t step, float* __restrict__ coords,
+                                  uint64_t key, float* __restrict__ coords,
                                   float* __restrict__ normals, float* __restrict__ sdf) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 2 * k; i += (int64_t)gridDim.x * blockDim.x) {
         float c[3], nv[3], s;
         if (i < k) {
-            const uint64_t r = rng64(seed, step, (uint64_t)i);
+            const uint64_t r = mix64(key + (uint64_t)i);
             const int64_t idx = (int64_t)__umul64hi(r, (uint64_t)m);
 #pragma unroll
             for (int q = 0; q < 3; ++q) {
@@ -49,7 +51,7 @@ __global__ void sample_sdf_kernel(const float* __restrict__ pc, const float* __r
             const int64_t j = i - k;
 #pragma unroll
             for (int q = 0; q < 3; ++q) {
-                c[q] = 2.f * unit24(rng64(seed, step, (uint64_t)(k + 3 * j + q))) - 1.f;
+                c[q] = 2.f * unit24(mix64(key + (uint64_t)(k + 3 * j + q))) - 1.f;
                 nv[q] = -1.f;
             }
             s = -1.f;

@@ -9,8 +9,8 @@ namespace siren {
 void launch_sample_sdf(hipStream_t st, const float* pc, const float* pn, int64_t m, int64_t k, uint64_t seed,
                        uint64_t step, float* coords, float* normals, float* sdf) {
     const int64_t blocks = std::min<int64_t>((2 * k + 255) / 256, 8192);
-    hipLaunchKernelGGL(sample_sdf_kernel, dim3((unsigned)blocks), dim3(256), 0, st, pc, pn, m, k, seed, step, coords,
-                       normals, sdf);
+    hipLaunchKernelGGL(sample_sdf_kernel, dim3((unsigned)blocks), dim3(256), 0, st, pc, pn, m, k, rng_key(seed, step),
+                       coords, normals, sdf);
 }
 
 void launch_adam(hipStream_t st, float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
