@@ -192,6 +192,25 @@ int32_t siren_adam_step(float* params, const float* grads, float* exp_avg, float
                         float beta1, float beta2, float eps, int64_t step, float max_norm, float* scratch,
                         void* stream);
 
+/* ---- batched (hypernetwork) weights ----------------------------------------------------
+ * BatchLinear with per-element weights W (B, out, in), b (B, out) (modules.py:16-25; HyperNetwork.forward,
+ * meta_modules.py:41-53) applied to coords (B, n, d_in). Element b reads params + b * param_count (state-dict
+ * order, as siren_pack), ws + b * workspace_floats, x + b * n * d_in, and writes y + b * n * d_out, gx + b * n * d_in,
+ * gparams + b * param_count. batch <= 65535. */
+int32_t siren_pack_batched(const siren_cfg* cfg, const float* params, int64_t batch, float* ws, void* stream);
+/* W0 for every element in ONE grouped launch (grid.y = element) at hidden 256, linear output, 1..5 hidden layers;
+ * other configurations run siren_forward element by element. */
+int32_t siren_forward_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
+                              float* y, void* stream);
+/* W1 (y, J^T gy) for every element in ONE grouped launch (hidden 256, linear output, 1..3 hidden layers; the
+ * persistent grid is split across the elements); gy (B, n, d_out) nullable = ones. */
+int32_t siren_forward_grad_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
+                                   const float* gy, float* y, float* gx, void* stream);
+/* W2 per element (the hypernetwork needs each element's theta-gradient): siren_backward on the stream, element by
+ * element, sharing tws (siren_train_ws_floats(cfg, n)). gx nullable. */
+int32_t siren_backward_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
+                               const float* gy, float* tws, float* gx, float* gparams, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

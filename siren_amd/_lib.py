@@ -47,6 +47,10 @@ _SIGS = {
     'siren_second_order_ws_floats': [_CFG, _I64, ctypes.c_int32, ctypes.POINTER(_I64)],
     'siren_second_order': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P],
     'siren_second_order_seeded': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P, _P],
+    'siren_pack_batched': [_CFG, _P, _I64, _P, _P],
+    'siren_forward_batched': [_CFG, _P, _P, _I64, _I64, _P, _P],
+    'siren_forward_grad_batched': [_CFG, _P, _P, _I64, _I64, _P, _P, _P, _P],
+    'siren_backward_batched': [_CFG, _P, _P, _I64, _I64, _P, _P, _P, _P, _P],
     'siren_sample_sdf': [_P, _P, _I64, _I64, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P],
     'siren_adam_scratch_floats': [ctypes.POINTER(_I64)],
     'siren_adam_step': [_P, _P, _P, _P, _I64, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _I64,

@@ -209,6 +209,43 @@ class SirenVJP(torch.autograd.Function):
         return None, None, (gx if need_x else None), gp, ggy
 
 
+class SirenBatchedFunction(torch.autograd.Function):
+    """y (B, n, d_out) = Phi(x_b; theta_b) for per-element weights theta (B, P) — BatchLinear with batched W
+    (modules.py:16-25) under a HyperNetwork (meta_modules.py:41-53, 81-92). Forward: one grouped W0 launch over the
+    batch (siren_forward_batched). Backward: gx from one grouped W1 launch; theta-gradients (what flows back into the
+    hypernetwork) from the W2 pipeline per element (siren_backward_batched). Under create_graph each element
+    becomes a SirenVJP node (W1 forward, W3 backward) and theta-gradients recompute with device torch ops."""
+
+    @staticmethod
+    def forward(ctx, engine, x, flat):
+        ws = engine.pack_batched(flat)
+        y = engine.forward_batched(ws, x)
+        ctx.engine, ctx.ws = engine, ws
+        ctx.save_for_backward(x, flat)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, flat = ctx.saved_tensors
+        engine, ws = ctx.engine, ctx.ws
+        need_x = ctx.needs_input_grad[1] and _will_execute(ctx, 0)
+        need_p = ctx.needs_input_grad[2] and _will_execute(ctx, 1)
+        gy = gy.contiguous()
+        gx = gp = None
+        if not torch.is_grad_enabled():
+            if need_p:
+                gx, gp = engine.backward_params_batched(ws, x, gy)
+            elif need_x:
+                _, gx = engine.forward_grad_batched(ws, x, gy, want_y=False)
+            return None, (gx if need_x else None), gp
+        if need_x:
+            gx = torch.stack([SirenVJP.apply(engine, ws[b], x[b], flat[b], gy[b]) for b in range(x.shape[0])])
+        if need_p:
+            gp = torch.stack([_torch_path.vjp_params(engine.cfg, x[b], flat[b], gy[b], create_graph=True)
+                              for b in range(x.shape[0])])
+        return None, gx, gp
+
+
 class SirenLaplace(torch.autograd.Function):
     """Laplacian sum_j sum_i d2 Phi_j/dx_i2 (n, 1) as ONE graph node: forward = the W4 jet kernel
     (siren_forward_laplace: y, grad and Laplacian in one forward-mode sweep). diff_operators.laplace routes here

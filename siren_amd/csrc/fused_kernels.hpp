@@ -28,7 +28,11 @@ namespace siren {
 // s0 = w0 / 2 pi, hidden-layer slices and biases times s = w / 2 pi (W_out, b_out and the seed unscaled), so that
 // kernel's accumulators are phases in revolutions (sincos_rev) and its reverse GEMMs return s W^T delta.
 __global__ void pack_kernel(const float* __restrict__ p, float* __restrict__ ws, int d, int o, int lh,
-                            int64_t spad, int64_t total, int h, int64_t base, float s0, float s) {
+                            int64_t spad, int64_t total, int h, int64_t base, float s0, float s,
+                            int64_t p_bstride) {
+    // grouped over batched weights (grid.y = batch element): params rows of p_bstride, workspaces of total floats
+    p += (int64_t)blockIdx.y * p_bstride;
+    ws += (int64_t)blockIdx.y * total;
     // h = hidden width (256: the H kernels, 512: wide_kernel.hpp); a slice is 16 K-rows x h out-neurons
     const ParamOffsets off(d, o, lh, h);
     const SmallLayout sl(h);

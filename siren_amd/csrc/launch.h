@@ -18,11 +18,12 @@ struct FusedArgs {
     float* abuf;
     float* dbuf;
     int64_t n_pad;
+    int64_t ws_bstride = 0;  // w1_kernel grouped launch: packed-workspace stride between batch elements (grid.y)
 };
 
 // tu_legacy.hip
 void launch_pack(const float* p, float* ws, int d, int o, int lh, int h, int64_t spad, int64_t total, int64_t base,
-                 float s0, float s, hipStream_t st);
+                 float s0, float s, hipStream_t st, int batch = 1, int64_t p_bstride = 0);
 void launch_legacy_fwd(dim3 grid, hipStream_t st, const FusedArgs& a);
 void launch_legacy_grad(bool store, dim3 grid, hipStream_t st, const FusedArgs& a);
 // tu_w1.hip: mode 0 = W1, 1 = STORE (W2 stage 1); tu_w0.hip: forward only

@@ -472,4 +472,83 @@ int32_t siren_adam_step(float* params, const float* grads, float* exp_avg, float
     return hip_status("siren_adam_step");
 }
 
+// ---- batched (hypernetwork) weights: BatchLinear with W (B, out, in) (modules.py:16-25, meta_modules.py:41-53) ----
+// Element b uses params + b * param_count, ws + b * ws_floats, x + b * n * d_in, y + b * n * d_out, ...
+// W0 / W1 on hidden 256 (the w1_kernel family) run as ONE grouped launch (grid.y = batch element); other
+// configurations and the W2 backward run the single-network entry points element by element on the stream.
+bool grouped_ok(const siren_cfg* cfg) {
+    return w1_ok(cfg) && cfg->outermost_linear && (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0;
+}
+
+int32_t siren_pack_batched(const siren_cfg* cfg, const float* params, int64_t batch, float* ws, void* stream) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (batch < 0 || batch > 65535) return fail(SIREN_EINVAL, "batch must be in [0, 65535]");
+    if (batch == 0) return SIREN_OK;
+    if (params == nullptr || ws == nullptr) return fail(SIREN_EINVAL, "params/ws is NULL");
+    siren::launch_pack(params, ws, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden, small_pad(cfg), ws_floats(cfg),
+                       wide(cfg) ? 0 : ws_base(cfg), cfg->omega_first * kInv2Pi, cfg->omega_hidden * kInv2Pi,
+                       (hipStream_t)stream, (int)batch, param_count(cfg));
+    return hip_status("siren_pack_batched");
+}
+
+int32_t siren_forward_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
+                              float* y, void* stream) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (n < 0 || batch < 0 || batch > 65535) return fail(SIREN_EINVAL, "need n >= 0 and 0 <= batch <= 65535");
+    if (n == 0 || batch == 0) return SIREN_OK;
+    if (ws == nullptr || x == nullptr || y == nullptr) return fail(SIREN_EINVAL, "ws/x/y is NULL");
+    const int64_t W = ws_floats(cfg), blocks = (n + siren::TILE - 1) / siren::TILE;
+    if (!(grouped_ok(cfg) && cfg->n_hidden <= 5)) {
+        for (int64_t b = 0; b < batch; ++b)
+            if (int rc = siren_forward(cfg, ws + b * W, x + b * n * cfg->d_in, n, y + b * n * cfg->d_out, stream))
+                return rc;
+        return SIREN_OK;
+    }
+    if (blocks > 0x7fffffffll) return fail(SIREN_EINVAL, "n too large");
+    siren::FusedArgs fa{w1_ws(cfg, ws), x, n, nullptr, y, nullptr, cfg->d_in, cfg->d_out, cfg->n_hidden,
+                        cfg->omega_first, cfg->omega_hidden, 0, nullptr, nullptr, 0, W};
+    siren::launch_w0(dim3((unsigned)blocks, (unsigned)batch), (hipStream_t)stream, fa);
+    return hip_status("siren_forward_batched");
+}
+
+int32_t siren_forward_grad_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
+                                   const float* gy, float* y, float* gx, void* stream) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (n < 0 || batch < 0 || batch > 65535) return fail(SIREN_EINVAL, "need n >= 0 and 0 <= batch <= 65535");
+    if (n == 0 || batch == 0) return SIREN_OK;
+    if (ws == nullptr || x == nullptr || gx == nullptr) return fail(SIREN_EINVAL, "ws/x/gx is NULL");
+    const int64_t W = ws_floats(cfg), blocks = (n + siren::TILE - 1) / siren::TILE;
+    const int d = cfg->d_in, o = cfg->d_out;
+    if (!(grouped_ok(cfg) && cfg->n_hidden <= siren::MAX_LH_GRAD)) {
+        for (int64_t b = 0; b < batch; ++b)
+            if (int rc = siren_forward_grad(cfg, ws + b * W, x + b * n * d, n, gy ? gy + b * n * o : nullptr,
+                                            y ? y + b * n * o : nullptr, gx + b * n * d, stream))
+                return rc;
+        return SIREN_OK;
+    }
+    siren::FusedArgs fa{w1_ws(cfg, ws), x, n, gy, y, gx, d, o, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden,
+                        0, nullptr, nullptr, 0, W};
+    // persistent grid split across the batch: about one workgroup per CU in total
+    const dim3 g1 = tile_grid(cfg, blocks, 1);
+    const int64_t per = std::max<int64_t>(1, ((int64_t)g1.x + batch - 1) / batch);
+    const int64_t gxs = (cfg->reserved & SIREN_FLAG_NO_PERSIST) != 0 ? blocks : std::min(blocks, per);
+    siren::launch_w1(w1_mode(cfg, gy), dim3((unsigned)gxs, (unsigned)batch), (hipStream_t)stream, fa);
+    return hip_status("siren_forward_grad_batched");
+}
+
+int32_t siren_backward_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
+                               const float* gy, float* tws, float* gx, float* gparams, void* stream) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (n < 0 || batch < 0) return fail(SIREN_EINVAL, "need n >= 0 and batch >= 0");
+    if (batch > 0 && (ws == nullptr || gy == nullptr || gparams == nullptr || (n > 0 && x == nullptr)))
+        return fail(SIREN_EINVAL, "ws/x/gy/gparams is NULL");
+    const int64_t W = ws_floats(cfg), P = param_count(cfg);
+    const int d = cfg->d_in, o = cfg->d_out;
+    for (int64_t b = 0; b < batch; ++b)
+        if (int rc = siren_backward(cfg, ws + b * W, x + b * n * d, n, gy + b * n * o, tws, nullptr,
+                                    gx ? gx + b * n * d : nullptr, gparams + b * P, stream))
+            return rc;
+    return SIREN_OK;
+}
+
 }  // extern "C"

@@ -7,7 +7,7 @@ namespace siren {
 void launch_w1(int mode, dim3 grid, hipStream_t st, const FusedArgs& a) {
 #define SIREN_L(LHV, M)                                                                                       \
     hipLaunchKernelGGL((w1_kernel<LHV, M>), grid, dim3(THREADS), 0, st, a.ws, a.x, a.n, a.gy, a.y, a.gx, a.d, a.o, \
-                       a.w0, a.w, a.abuf, a.dbuf, a.n_pad)
+                       a.w0, a.w, a.abuf, a.dbuf, a.n_pad, a.ws_bstride)
     if (mode == MODE_STORE) {
         switch (a.lh) {
             case 1: SIREN_L(1, MODE_STORE); break;

@@ -8,7 +8,7 @@ void launch_w4(dim3 grid, hipStream_t st, const float* ws, const float* x, int64
                int d, int o, int lh, float w0, float w) {
 #define SIREN_L(LHV)                                                                                             \
     hipLaunchKernelGGL((w1_kernel<LHV, MODE_JET>), grid, dim3(THREADS), 0, st, ws, x, n, (const float*)nullptr, y, \
-                       gx, d, o, w0, w, lap, (float*)nullptr, (int64_t)0)
+                       gx, d, o, w0, w, lap, (float*)nullptr, (int64_t)0, (int64_t)0)
     switch (lh) {
         case 1: SIREN_L(1); break;
         case 2: SIREN_L(2); break;

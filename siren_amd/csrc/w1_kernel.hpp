@@ -367,7 +367,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
                                                         int64_t n, const float* __restrict__ gy, float* __restrict__ y,
                                                         float* __restrict__ gx, int d, int o, float w0, float w,
                                                         float* __restrict__ abuf, float* __restrict__ dbuf,
-                                                        int64_t n_pad) {
+                                                        int64_t n_pad, int64_t ws_bstride) {
     constexpr bool STORE = (MODE & MODE_BASE) == MODE_STORE;
     constexpr bool JET = (MODE & MODE_BASE) == MODE_JET;
     constexpr int NS = npasses<MODE>() * LH * NB;
@@ -388,6 +388,14 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
     }
     cx.d = d;
     cx.o = o;
+    if (ws_bstride != 0) {  // grouped launch over batched (hypernetwork) weights: blockIdx.y = batch element
+        const int64_t b = blockIdx.y;
+        ws += b * ws_bstride;
+        x += b * n * d;
+        if (y != nullptr) y += b * n * o;
+        if (gx != nullptr) gx += b * n * d;
+        if (gy != nullptr) gy += b * n * o;
+    }
     {
         constexpr float two_pi = 6.28318530717958648f;
         const float s = w * 0.159154943091895336f;  // hidden-layer scale of the phase-scaled pack

@@ -180,6 +180,73 @@ class SirenEngine:
                    'siren_backward')
         return gx, gp
 
+    # ---- batched (hypernetwork) weights: element b of (B, ...) tensors uses its own parameter row ------------
+    def _check_xb(self, x):
+        if not isinstance(x, torch.Tensor) or x.device.type != 'cuda' or x.dtype != torch.float32:
+            raise RuntimeError('siren_amd batched coords must be fp32 on a ROCm device')
+        if x.dim() != 3 or x.shape[2] != self.cfg.d_in:
+            raise ValueError('batched coords must be (B, n, %d); got %s' % (self.cfg.d_in, tuple(x.shape)))
+        return x.contiguous()
+
+    def pack_batched(self, flat):
+        """flat (B, param_count) -> packed workspaces (B, ws_floats), one grouped launch."""
+        self._require()
+        if flat.dim() != 2 or flat.shape[1] != self.param_count or flat.dtype != torch.float32 \
+                or flat.device.type != 'cuda':
+            raise ValueError('batched params must be fp32 (B, %d) on a ROCm device' % self.param_count)
+        flat = flat.contiguous()
+        ws = torch.empty(flat.shape[0], self.ws_floats, dtype=torch.float32, device=flat.device)
+        _lib.check(self.lib.siren_pack_batched(ctypes.byref(self.cfg), _ptr(flat), flat.shape[0], _ptr(ws),
+                                               _stream(flat.device)), 'siren_pack_batched')
+        return ws
+
+    def forward_batched(self, ws, x):
+        """W0 over (B, n, d_in) with per-element weights -> (B, n, d_out)."""
+        self._require()
+        x = self._check_xb(x)
+        B, n = x.shape[:2]
+        y = torch.empty(B, n, self.cfg.d_out, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_forward_batched(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, B, _ptr(y),
+                                                  _stream(x.device)), 'siren_forward_batched')
+        return y
+
+    def forward_grad_batched(self, ws, x, gy=None, want_y=True):
+        """W1 over (B, n, d_in): (y | None, J^T gy) with per-element weights."""
+        self._require()
+        if not self.grad_supported:
+            raise _lib.SirenUnsupported('siren_forward_grad needs 1 <= num_hidden_layers <= 3 at hidden 256')
+        x = self._check_xb(x)
+        B, n = x.shape[:2]
+        if gy is not None:
+            gy = gy.contiguous()
+            if gy.shape != (B, n, self.cfg.d_out):
+                raise ValueError('gy must be (%d, %d, %d)' % (B, n, self.cfg.d_out))
+        y = torch.empty(B, n, self.cfg.d_out, dtype=torch.float32, device=x.device) if want_y else None
+        gx = torch.empty_like(x)
+        _lib.check(self.lib.siren_forward_grad_batched(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, B, _ptr(gy),
+                                                       _ptr(y), _ptr(gx), _stream(x.device)),
+                   'siren_forward_grad_batched')
+        return y, gx
+
+    def backward_params_batched(self, ws, x, gy):
+        """W2 per element: (gx (B, n, d_in), gparams (B, param_count))."""
+        self._require()
+        if not self.grad_supported:
+            raise _lib.SirenUnsupported('siren_backward needs 1 <= num_hidden_layers <= 3 at hidden 256')
+        x = self._check_xb(x)
+        B, n = x.shape[:2]
+        gy = gy.contiguous()
+        cnt = ctypes.c_int64()
+        _lib.check(self.lib.siren_train_ws_floats(ctypes.byref(self.cfg), n, ctypes.byref(cnt)),
+                   'siren_train_ws_floats')
+        tws = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
+        gx = torch.empty_like(x)
+        gp = torch.empty(B, self.param_count, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_backward_batched(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, B, _ptr(gy),
+                                                   _ptr(tws), _ptr(gx), _ptr(gp), _stream(x.device)),
+                   'siren_backward_batched')
+        return gx, gp
+
     def second_order(self, ws, x, v, want_theta=True, gy=None, u=None, want_ydot=False):
         """W3: the backward of the vjp node gx = J^T u (u (n, d_out), None = ones, i.e. diff_operators.gradient's
         dPhi/dx) given its cotangent v (n, d_in): H v and d/dtheta of F = sum <v, J^T u> (+ sum gy . y with a

@@ -27,7 +27,7 @@ import torch
 from torch import nn
 
 from . import _lib
-from .autograd import JetState, SirenFunction, SirenJetFunction
+from .autograd import JetState, SirenBatchedFunction, SirenFunction, SirenJetFunction
 from .engine import SirenEngine
 
 
@@ -165,10 +165,12 @@ def _fused_apply(engine, jet, coords, weights_biases):
     if not engine.supported:
         raise _lib.SirenUnsupported('siren_amd fused kernels do not cover this network: %s'
                                     % engine.unsupported_reason)
+    if weights_biases[0][0].dim() == 3:
+        return _fused_apply_batched(engine, coords, weights_biases)
     parts = []
     for W, b in weights_biases:
         if W.dim() != 2:
-            raise _lib.SirenUnsupported('batched (hypernetwork) weights are not covered by the fused kernels yet')
+            raise _lib.SirenUnsupported('mixed batched / unbatched layer weights')
         parts.append(W.reshape(-1))
         parts.append(b.reshape(-1) if b is not None else W.new_zeros(W.shape[0]))
     flat = torch.cat(parts)
@@ -182,6 +184,27 @@ def _fused_apply(engine, jet, coords, weights_biases):
     else:
         y = SirenFunction.apply(engine, jet, x2d, flat)
     return y.view(*lead, y.shape[-1])
+
+
+def _fused_apply_batched(engine, coords, weights_biases):
+    """BatchLinear with batched weights (modules.py:16-25): W (B, out, in), b (B, out), coords (B, N, d_in) (or
+    (1, N, d_in), broadcast over B as matmul does) -> (B, N, d_out) through SirenBatchedFunction."""
+    B = weights_biases[0][0].shape[0]
+    parts = []
+    for W, b in weights_biases:
+        if W.dim() != 3 or W.shape[0] != B:
+            raise _lib.SirenUnsupported('batched weights need W (B, out, in) on every layer')
+        parts.append(W.reshape(B, -1))
+        parts.append(b.reshape(B, -1) if b is not None else W.new_zeros(B, W.shape[1]))
+    flat = torch.cat(parts, dim=1)
+    if coords.dim() != 3:
+        raise _lib.SirenUnsupported('batched weights need coords of shape (B, N, d_in)')
+    x = coords.expand(B, -1, -1) if coords.shape[0] == 1 and B > 1 else coords
+    if x.shape[0] != B:
+        raise ValueError('coords batch %d does not match the weights batch %d' % (x.shape[0], B))
+    if x is coords:
+        x = coords.view(coords.shape)  # a non-leaf edge, as in _fused_apply
+    return SirenBatchedFunction.apply(engine, x, flat)
 
 
 # ----------------------------------------------------------------------------------------------------------

@@ -85,3 +85,8 @@ def pml_case(g6, tag):
 def pml_ref_grads(g6, tag):
     keys = ['net.net.%d.0.%s' % (i, k) for i in range(5) for k in ('weight', 'bias')]
     return np.concatenate([g6['%s_grad_%s' % (tag, k)].reshape(-1) for k in keys])
+
+
+@pytest.fixture(scope='session')
+def g7():
+    return load_golden('g7')

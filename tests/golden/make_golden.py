@@ -16,13 +16,17 @@ Fixtures:
   G3  5x256 d3 o1 SDF batch (sphere, 2048 on + 2048 off surface): the four `sdf` loss terms and theta-grads.
   G4  5x512 d3 o3, 1024 coords: model_out and image_mse theta-grads.
   G5  config-1 trajectory: 256^2 synthetic image, 300 full-batch Adam steps (lr 1e-4), loss every 10 steps, PSNR.
+  G7  batched (hypernetwork) weights: the reference's HyperNetwork (meta_modules.py:10-53)
+      predicts 3 sets of 5x256 d2 o1 weights from 3 embeddings; SingleBVPNet(params=...) on (3, 512, 2) coords:
+      the predicted weights, model_out, gradient and the image_mse gradient w.r.t. the predicted weights.
   G6  vector outputs / PML losses: 5x256 d2 o2 (helmholtz_pml, loss_functions.py:139-211)
       and 5x256 d3 o1 (wave_pml, loss_functions.py:112-136), 1024 coords each: jacobian / hessian
       (diff_operators.py:5-24, 46-59), the loss terms and their fp64 theta-grads.
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--skip-fit] [--only-g6]
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--skip-fit] [--only g6,g7]
 """
 import argparse
+from collections import OrderedDict
 import json
 import os
 import sys
@@ -175,16 +179,45 @@ def make_g6(modules, D, L, meta):
     np.savez_compressed(os.path.join(OUT, 'golden_g6.npz'), **store)
 
 
+def make_g7(modules, D, L, meta):
+    import meta_modules
+    torch.manual_seed(8)
+    hypo = modules.SingleBVPNet(type='sine', in_features=2, out_features=1)
+    hyper = meta_modules.HyperNetwork(hyper_in_features=8, hyper_hidden_layers=1, hyper_hidden_features=32,
+                                      hypo_module=hypo)
+    z = torch.randn(3, 8)
+    gen = torch.Generator().manual_seed(7)
+    coords = torch.rand(3, 512, 2, generator=gen) * 2 - 1
+    gt = synth_image(coords)
+    with torch.no_grad():
+        params = hyper(z)
+    store = {'coords': coords.numpy(), 'gt_img': gt.numpy()}
+    for k, v in params.items():
+        store['p_' + k] = v.numpy().astype(np.float32)
+    p64 = OrderedDict((k, v.double().requires_grad_(True)) for k, v in params.items())
+    hypo = hypo.double()
+    out = hypo({'coords': coords.double()}, params=p64)
+    store['G7_model_out_f64'] = out['model_out'].detach().numpy()
+    store['G7_gradient_f64'] = D.gradient(out['model_out'], out['model_in']).detach().numpy()
+    loss = L.image_mse(None, out, {'img': gt.double()})['img_loss'].mean()
+    meta['G7_image_mse_f64'] = float(loss)
+    grads = torch.autograd.grad(loss, list(p64.values()))
+    for k, g in zip(p64.keys(), grads):
+        store['G7_grad_' + k] = g.numpy().astype(np.float32)
+    np.savez_compressed(os.path.join(OUT, 'golden_g7.npz'), **store)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--skip-fit', action='store_true', help='reuse the G5 weights already in golden_fit.npz')
-    ap.add_argument('--only-g6', action='store_true', help='add G6 to the existing fixtures and manifest')
+    ap.add_argument('--only', default='', help='comma list of late fixtures (g6, g7) to add to the existing set')
     args = ap.parse_args()
-    if args.only_g6:
+    if args.only:
         modules, D, L = import_reference()
         with open(os.path.join(OUT, 'manifest.json')) as f:
             meta = json.load(f)
-        make_g6(modules, D, L, meta)
+        for name in args.only.split(','):
+            {'g6': make_g6, 'g7': make_g7}[name](modules, D, L, meta)
         with open(os.path.join(OUT, 'manifest.json'), 'w') as f:
             json.dump(meta, f, indent=1, sort_keys=True)
         return

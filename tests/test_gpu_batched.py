@@ -1,0 +1,99 @@
+"""Batched (hypernetwork) weights on the HIP kernels: BatchLinear with W (B, out, in)
+(modules.py:16-25) under the reference's HyperNetwork (meta_modules.py:10-53). The grouped W0 / W1 launches must
+equal the single-network kernels element by element (bitwise: every tile runs the same instruction stream), and
+the drop-in SingleBVPNet(params=...) must match the reference's G7 golden (tests/golden/make_golden.py).
+Needs an MI355X."""
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import siren_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def tol_rel(ref, rel=1e-4):
+    return rel * max(1., float(np.max(np.abs(ref))))
+
+
+def random_flat(B, d, L, o, H=256, seed=0):
+    rng = np.random.default_rng(seed)
+    rows = []
+    for _ in range(B):
+        dims = [d] + [H] * (L + 1) + [o]
+        layers = []
+        for i, (fi, fo) in enumerate(zip(dims[:-1], dims[1:])):
+            bound = 1. / fi if i == 0 else np.sqrt(6. / fi) / 30.
+            layers.append((rng.uniform(-bound, bound, (fo, fi)).astype(np.float32),
+                           (rng.uniform(-1, 1, fo) / np.sqrt(fi)).astype(np.float32)))
+        rows.append(O.flatten(layers))
+    return np.stack(rows).astype(np.float32)
+
+
+@pytest.mark.parametrize('B,n,d,L,o,H', [(4, 4097, 2, 3, 1, 256), (3, 65, 3, 3, 1, 256), (2, 1000, 3, 2, 3, 256),
+                                         (5, 300, 2, 5, 1, 256), (2, 700, 3, 3, 3, 512)])
+def test_grouped_launch_equals_per_element(cuda, B, n, d, L, o, H):
+    from siren_amd.engine import SirenEngine
+    eng = SirenEngine(d, H, L, o)
+    flat = torch.tensor(random_flat(B, d, L, o, H, seed=B * n), device=cuda)
+    x = torch.rand(B, n, d, device=cuda) * 2 - 1
+    gy = torch.randn(B, n, o, device=cuda)
+    wsb = eng.pack_batched(flat)
+    yb = eng.forward_batched(wsb, x)
+    grad_ok = eng.grad_supported
+    if grad_ok:
+        y1b, gxb = eng.forward_grad_batched(wsb, x, gy)
+        gxp, gpp = eng.backward_params_batched(wsb, x, gy)
+    for b in range(B):
+        ws = eng.pack(flat[b])
+        assert torch.equal(ws, wsb[b])
+        assert torch.equal(eng.forward(ws, x[b]), yb[b])
+        if grad_ok:
+            y1, gx = eng.forward_grad(ws, x[b], gy[b])
+            assert torch.equal(y1, y1b[b]) and torch.equal(gx, gxb[b])
+            gx2, gp2 = eng.backward_params(ws, x[b], gy[b])
+            assert torch.equal(gp2, gpp[b]) and torch.equal(gx2, gxp[b])
+
+
+def test_hypo_params_forward_gradient_and_theta_grads_vs_reference(cuda, g7):
+    """SingleBVPNet(model_input, params=hypernetwork output) == the reference's G7 (fp64): model_out, gradient
+    (create_graph, per-element W1 nodes) and the image_mse gradient w.r.t. the predicted weights (per-element W2)."""
+    from siren_amd.modules import SingleBVPNet
+    from siren_amd import diff_operators as D, loss_functions as LF
+    m = SingleBVPNet(in_features=2, out_features=1, verbose=False).to(cuda)
+    params = OrderedDict((k[2:], torch.tensor(v, device=cuda, requires_grad=True))
+                         for k, v in g7.items() if k.startswith('p_'))
+    coords = torch.tensor(g7['coords'], device=cuda)
+    out = m({'coords': coords}, params=params)
+    y = out['model_out']
+    assert y.shape == (3, 512, 1)
+    assert np.max(np.abs(y.detach().cpu().numpy() - g7['G7_model_out_f64'])) <= 1e-4
+    g = D.gradient(y, out['model_in'])
+    rg = g7['G7_gradient_f64']
+    assert np.max(np.abs(g.detach().cpu().numpy() - rg)) <= tol_rel(rg)
+    loss = LF.image_mse(None, out, {'img': torch.tensor(g7['gt_img'], device=cuda)})['img_loss']
+    grads = torch.autograd.grad(loss, list(params.values()))
+    for (k, _), gr in zip(params.items(), grads):
+        ref = g7['G7_grad_' + k]
+        assert np.max(np.abs(gr.cpu().numpy() - ref)) <= 1e-4 * max(np.max(np.abs(ref)), 1e-30) + 1e-12, k
+
+
+def test_hypernetwork_end_to_end(cuda, g7):
+    """HyperNetwork on the device predicting the hypo weights, backward into the hypernetwork's own parameters."""
+    from siren_amd.meta_modules import HyperNetwork
+    from siren_amd.modules import SingleBVPNet
+    torch.manual_seed(8)
+    hypo = SingleBVPNet(in_features=2, out_features=1, verbose=False)
+    hyper = HyperNetwork(hyper_in_features=8, hyper_hidden_layers=1, hyper_hidden_features=32, hypo_module=hypo)
+    z = torch.randn(3, 8)
+    hypo, hyper = hypo.to(cuda), hyper.to(cuda)
+    params = hyper(z.to(cuda))
+    for k, v in params.items():
+        assert np.max(np.abs(v.detach().cpu().numpy() - g7['p_' + k])) <= 1e-6 * max(1., np.max(np.abs(g7['p_' + k])))
+    out = hypo({'coords': torch.tensor(g7['coords'], device=cuda)}, params=params)
+    assert np.max(np.abs(out['model_out'].detach().cpu().numpy() - g7['G7_model_out_f64'])) <= 1e-4
+    loss = ((out['model_out'] - torch.tensor(g7['gt_img'], device=cuda)) ** 2).mean()
+    loss.backward()
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in hyper.parameters())

@@ -133,3 +133,20 @@ def test_get_mgrid_matches_reference_formula():
     assert float(g.min()) == -1. and float(g.max()) == 1.
     g3 = get_mgrid((1, 4, 5), 3)
     assert g3.shape == (20, 3) and float(g3[:, 0].max()) == -1.   # dim 0 divides by max(s0 - 1, 1)
+
+
+def test_hypernetwork_predicts_reference_weights(g7):
+    """siren_amd.meta_modules.HyperNetwork (meta_modules.py:10-53, 136-154) built under the reference's seed
+    predicts the reference's hypo-network weights exactly (same RNG consumption, plain torch on the CPU)."""
+    import torch
+    from siren_amd.meta_modules import HyperNetwork
+    from siren_amd.modules import SingleBVPNet
+    torch.manual_seed(8)
+    hypo = SingleBVPNet(in_features=2, out_features=1, verbose=False)
+    hyper = HyperNetwork(hyper_in_features=8, hyper_hidden_layers=1, hyper_hidden_features=32, hypo_module=hypo)
+    z = torch.randn(3, 8)
+    with torch.no_grad():
+        params = hyper(z)
+    assert list(params.keys()) == ['net.net.%d.0.%s' % (i, k) for i in range(5) for k in ('weight', 'bias')]
+    for k, v in params.items():
+        assert np.array_equal(v.numpy(), g7['p_' + k]), k
