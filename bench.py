@@ -207,6 +207,18 @@ def config_rates(device, steps=5):
                            'sample_sdf_bytes': 24 * k + 2 * k * 28,
                            'clip_adam_us_per_call': round(ms_a * 1e3, 2),
                            'clip_adam_bytes': 28 * P, 'params': P}
+    # §8f row 2: batched hypernetwork weights, a meta-batch of 32 64x64 images (grouped W1 launch over the batch)
+    eng_b = SirenEngine(2, 256, 3, 1)
+    flat_b = torch.randn(32, eng_b.param_count, device=device) * 0.01
+    xb = torch.rand(32, 4096, 2, device=device) * 2 - 1
+    wsb = eng_b.pack_batched(flat_b)
+    eng_b.forward_grad_batched(wsb, xb)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng_b.forward_grad_batched(wsb, xb)
+    torch.cuda.synchronize()
+    res['hypernet_b32x4096_grouped_w1_mcoords_s'] = round(32 * 4096 * steps / (time.perf_counter() - t0) / 1e6, 3)
     # configs[3]: video fit, 5x512 d3 o3 image_mse (W2 at hidden 512), 2^18 coords per GPU
     torch.manual_seed(0)
     m = SingleBVPNet(in_features=3, out_features=3, hidden_features=512, verbose=False).to(device)

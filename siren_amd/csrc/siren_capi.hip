@@ -71,8 +71,7 @@ int w1_mode(const siren_cfg* cfg, const float* gy) {
     return siren::MODE_W1;
 }
 
-dim3 tile_grid(const siren_cfg* cfg, int64_t tiles, int per_cu) {
-    if ((cfg->reserved & SIREN_FLAG_NO_PERSIST) != 0) return dim3((unsigned)tiles);
+int cu_count() {
     static int cus[64] = {0};
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -82,7 +81,12 @@ dim3 tile_grid(const siren_cfg* cfg, int64_t tiles, int per_cu) {
         if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
         cus[dev] = v;
     }
-    const int64_t g = (int64_t)cus[dev] * per_cu;
+    return cus[dev];
+}
+
+dim3 tile_grid(const siren_cfg* cfg, int64_t tiles, int per_cu) {
+    if ((cfg->reserved & SIREN_FLAG_NO_PERSIST) != 0) return dim3((unsigned)tiles);
+    const int64_t g = (int64_t)cu_count() * per_cu;
     return dim3((unsigned)(tiles < g ? tiles : g));
 }
 
@@ -498,7 +502,10 @@ int32_t siren_forward_batched(const siren_cfg* cfg, const float* ws, const float
     if (n == 0 || batch == 0) return SIREN_OK;
     if (ws == nullptr || x == nullptr || y == nullptr) return fail(SIREN_EINVAL, "ws/x/y is NULL");
     const int64_t W = ws_floats(cfg), blocks = (n + siren::TILE - 1) / siren::TILE;
-    if (!(grouped_ok(cfg) && cfg->n_hidden <= 5)) {
+    // elements that fill the chip on their own run one by one: concurrent elements would stream several weight
+    // sets through each XCD's L2 (measured 7 % slower at 8 x 2^16, profiles/r01_batched.log)
+    const int64_t cus = cu_count();
+    if (!(grouped_ok(cfg) && cfg->n_hidden <= 5) || blocks >= 4 * cus) {
         for (int64_t b = 0; b < batch; ++b)
             if (int rc = siren_forward(cfg, ws + b * W, x + b * n * cfg->d_in, n, y + b * n * cfg->d_out, stream))
                 return rc;
@@ -519,7 +526,8 @@ int32_t siren_forward_grad_batched(const siren_cfg* cfg, const float* ws, const 
     if (ws == nullptr || x == nullptr || gx == nullptr) return fail(SIREN_EINVAL, "ws/x/gx is NULL");
     const int64_t W = ws_floats(cfg), blocks = (n + siren::TILE - 1) / siren::TILE;
     const int d = cfg->d_in, o = cfg->d_out;
-    if (!(grouped_ok(cfg) && cfg->n_hidden <= siren::MAX_LH_GRAD)) {
+    const int64_t cus = cu_count();
+    if (!(grouped_ok(cfg) && cfg->n_hidden <= siren::MAX_LH_GRAD) || blocks >= 2 * cus) {
         for (int64_t b = 0; b < batch; ++b)
             if (int rc = siren_forward_grad(cfg, ws + b * W, x + b * n * d, n, gy ? gy + b * n * o : nullptr,
                                             y ? y + b * n * o : nullptr, gx + b * n * d, stream))
@@ -529,7 +537,7 @@ int32_t siren_forward_grad_batched(const siren_cfg* cfg, const float* ws, const 
     siren::FusedArgs fa{w1_ws(cfg, ws), x, n, gy, y, gx, d, o, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden,
                         0, nullptr, nullptr, 0, W};
     // persistent grid split across the batch: about one workgroup per CU in total
-    const dim3 g1 = tile_grid(cfg, blocks, 1);
+    const dim3 g1 = tile_grid(cfg, blocks * batch, 1);  // min(all tiles, CUs)
     const int64_t per = std::max<int64_t>(1, ((int64_t)g1.x + batch - 1) / batch);
     const int64_t gxs = (cfg->reserved & SIREN_FLAG_NO_PERSIST) != 0 ? blocks : std::min(blocks, per);
     siren::launch_w1(w1_mode(cfg, gy), dim3((unsigned)gxs, (unsigned)batch), (hipStream_t)stream, fa);

@@ -32,7 +32,7 @@ def random_flat(B, d, L, o, H=256, seed=0):
     return np.stack(rows).astype(np.float32)
 
 
-@pytest.mark.parametrize('B,n,d,L,o,H', [(4, 4097, 2, 3, 1, 256), (3, 65, 3, 3, 1, 256), (2, 1000, 3, 2, 3, 256),
+@pytest.mark.parametrize('B,n,d,L,o,H', [(4, 4097, 2, 3, 1, 256), (3, 65, 3, 3, 1, 256), (2, 40000, 2, 3, 1, 256), (2, 1000, 3, 2, 3, 256),
                                          (5, 300, 2, 5, 1, 256), (2, 700, 3, 3, 3, 512)])
 def test_grouped_launch_equals_per_element(cuda, B, n, d, L, o, H):
     from siren_amd.engine import SirenEngine
