@@ -211,6 +211,19 @@ int32_t siren_forward_grad_batched(const siren_cfg* cfg, const float* ws, const 
 int32_t siren_backward_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
                                const float* gy, float* tws, float* gx, float* gparams, void* stream);
 
+/* ---- stored-forward W2 split (hidden 256, linear output, 1..3 hidden layers) ----------------------------------
+ * The training forward (model(model_input), training.py:72) keeps what the backward needs, so
+ * train_loss.backward() (training.py:96) runs the L reverse GEMMs only instead of recomputing the forward:
+ *   siren_forward_store : W0 (y) + a_l tiles and cos(w z_l) of every sine layer into tws
+ *   siren_backward_stored: reverse sweep from the stored cos + split-K MFMA wgrad + edge layers + slab reduction,
+ *                          same outputs as siren_backward (gx, gparams); tws must hold siren_forward_store's output
+ * tws: siren_train_stored_ws_floats(cfg, n) floats (siren_train_ws_floats + the cos buffer). */
+int32_t siren_train_stored_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count);
+int32_t siren_forward_store(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y, float* tws,
+                            void* stream);
+int32_t siren_backward_stored(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* gy,
+                              float* tws, float* gx, float* gparams, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

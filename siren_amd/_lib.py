@@ -47,6 +47,9 @@ _SIGS = {
     'siren_second_order_ws_floats': [_CFG, _I64, ctypes.c_int32, ctypes.POINTER(_I64)],
     'siren_second_order': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P],
     'siren_second_order_seeded': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P, _P],
+    'siren_train_stored_ws_floats': [_CFG, _I64, ctypes.POINTER(_I64)],
+    'siren_forward_store': [_CFG, _P, _P, _I64, _P, _P, _P],
+    'siren_backward_stored': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P],
     'siren_pack_batched': [_CFG, _P, _I64, _P, _P],
     'siren_forward_batched': [_CFG, _P, _P, _I64, _I64, _P, _P],
     'siren_forward_grad_batched': [_CFG, _P, _P, _I64, _I64, _P, _P, _P, _P],

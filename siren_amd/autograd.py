@@ -29,6 +29,11 @@ import torch
 from . import _torch_path
 
 
+# SirenFunction under a parameter-gradient graph stores the forward for a reverse-only backward;
+# False keeps the recompute-in-backward pipeline (A/B timing, tests)
+STORED_FORWARD = True
+
+
 def _will_execute(ctx, i):
     """Does the autograd engine need the gradient of tensor input i (in forward-argument order of tensors)?"""
     try:
@@ -57,9 +62,14 @@ class JetState:
 
 class SirenFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, engine, jet, x, flat):
+    def forward(ctx, engine, jet, x, flat, store=False):
         ws = engine.pack(flat)
-        y = engine.forward(ws, x)
+        ctx.tws = None
+        if store and engine.stored_supported and STORED_FORWARD:
+            # training forward: keep a_l / cos(w z_l) so the weight-gradient backward is reverse-only
+            y, ctx.tws = engine.forward_store(ws, x)
+        else:
+            y = engine.forward(ws, x)
         ctx.engine, ctx.jet, ctx.ws = engine, jet, ws
         ctx.save_for_backward(x, flat)
         return y
@@ -74,12 +84,15 @@ class SirenFunction(torch.autograd.Function):
         gy = gy.contiguous()
         if not torch.is_grad_enabled():
             if need_p:
-                gx, gp = engine.backward_params(ws, x, gy)
+                if ctx.tws is not None:
+                    gx, gp = engine.backward_stored(ws, x, gy, ctx.tws)
+                else:
+                    gx, gp = engine.backward_params(ws, x, gy)
                 if not need_x:
                     gx = None
             elif need_x:
                 _, gx = engine.forward_grad(ws, x, gy, want_y=False)
-            return None, None, gx, gp
+            return None, None, gx, gp, None
         # create_graph=True: results must be differentiable functions of (x, theta, gy)
         if need_x:
             if ctx.jet is not None and not need_p:
@@ -87,7 +100,7 @@ class SirenFunction(torch.autograd.Function):
             gx = SirenVJP.apply(engine, ws, x, flat, gy)
         if need_p:
             gp = _torch_path.vjp_params(engine.cfg, x, flat, gy, create_graph=True)
-        return None, None, gx, gp
+        return None, None, gx, gp, None
 
 
 class SirenJetFunction(torch.autograd.Function):

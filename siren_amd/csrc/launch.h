@@ -26,9 +26,11 @@ void launch_pack(const float* p, float* ws, int d, int o, int lh, int h, int64_t
                  float s0, float s, hipStream_t st, int batch = 1, int64_t p_bstride = 0);
 void launch_legacy_fwd(dim3 grid, hipStream_t st, const FusedArgs& a);
 void launch_legacy_grad(bool store, dim3 grid, hipStream_t st, const FusedArgs& a);
-// tu_w1.hip: mode 0 = W1, 1 = STORE (W2 stage 1); tu_w0.hip: forward only
+// tu_w1.hip: mode 0 = W1, 1 = STORE (W2 stage 1), MODE_REV (stored-forward W2 reverse); tu_w0.hip: forward only,
+// launch_w0s = MODE_FWDS
 void launch_w1(int mode, dim3 grid, hipStream_t st, const FusedArgs& a);
 void launch_w0(dim3 grid, hipStream_t st, const FusedArgs& a);
+void launch_w0s(dim3 grid, hipStream_t st, const FusedArgs& a);
 // tu_w4.hip: JET mode (16 coordinates per workgroup); lap (n) = sum_j Laplacian(y_j), gx (n, d) = sum_j grad y_j
 void launch_w4(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, float* y, float* gx, float* lap,
                int d, int o, int lh, float w0, float w);

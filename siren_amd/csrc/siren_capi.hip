@@ -290,6 +290,74 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
     return hip_status("siren_backward (reduce)");
 }
 
+// ---- stored-forward W2 split: the training forward keeps a_l and cos(w z_l) so the backward is reverse-only ----
+bool stored_ok(const siren_cfg* cfg) {
+    return w1_ok(cfg) && cfg->outermost_linear && cfg->n_hidden <= siren::MAX_LH_GRAD &&
+           (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0;
+}
+
+int32_t siren_train_stored_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (!stored_ok(cfg))
+        return fail(SIREN_EUNSUPPORTED, "the stored-forward W2 split covers hidden 256, linear output, 1..3 hidden layers");
+    if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
+    const TrainPlan plan(cfg, n);
+    *count = plan.total + plan.act_floats;  // + the lane-major cos buffer (same size as the a_l tiles)
+    return SIREN_OK;
+}
+
+int32_t siren_forward_store(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y, float* tws,
+                            void* stream) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (!stored_ok(cfg))
+        return fail(SIREN_EUNSUPPORTED, "the stored-forward W2 split covers hidden 256, linear output, 1..3 hidden layers");
+    if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    if (n == 0) return SIREN_OK;
+    if (ws == nullptr || x == nullptr || y == nullptr || tws == nullptr) return fail(SIREN_EINVAL, "ws/x/y/tws is NULL");
+    const TrainPlan plan(cfg, n);
+    float* abuf = tws;
+    float* cbuf = tws + plan.total;
+    siren::FusedArgs fa{w1_ws(cfg, ws), x, n, nullptr, y, nullptr, cfg->d_in, cfg->d_out, cfg->n_hidden,
+                        cfg->omega_first, cfg->omega_hidden, 0, abuf, cbuf, plan.n_pad};
+    siren::launch_w0s(dim3((unsigned)(plan.n_pad / siren::TILE)), (hipStream_t)stream, fa);
+    return hip_status("siren_forward_store");
+}
+
+int32_t siren_backward_stored(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* gy,
+                              float* tws, float* gx, float* gparams, void* stream) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (!stored_ok(cfg))
+        return fail(SIREN_EUNSUPPORTED, "the stored-forward W2 split covers hidden 256, linear output, 1..3 hidden layers");
+    if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    if (ws == nullptr || gy == nullptr || tws == nullptr || gx == nullptr || gparams == nullptr ||
+        (n > 0 && x == nullptr))
+        return fail(SIREN_EINVAL, "ws/x/gy/tws/gx/gparams is NULL");
+    const TrainPlan plan(cfg, n);
+    const hipStream_t st = (hipStream_t)stream;
+    const int64_t P = param_count(cfg);
+    if (n == 0) {
+        (void)hipMemsetAsync(gparams, 0, P * sizeof(float), st);
+        return hip_status("siren_backward_stored");
+    }
+    float* abuf = tws;
+    float* dbuf = tws + plan.act_floats;
+    float* partial = tws + 2 * plan.act_floats;
+    float* cbuf = tws + plan.total;
+    siren::FusedArgs fa{w1_ws(cfg, ws), x, n, gy, nullptr, gx, cfg->d_in, cfg->d_out, cfg->n_hidden,
+                        cfg->omega_first, cfg->omega_hidden, 0, cbuf, dbuf, plan.n_pad};
+    siren::launch_w1(siren::MODE_REV, tile_grid(cfg, plan.n_pad / siren::TILE, 1), st, fa);
+    if (int rc = hip_status("siren_backward_stored (reverse)")) return rc;
+    siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden, 1), st, abuf, dbuf, plan.n_pad, plan.tps,
+                        partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1, cfg->hidden);
+    if (int rc = hip_status("siren_backward_stored (wgrad)")) return rc;
+    siren::launch_small(dim3((unsigned)plan.splits), st, abuf, dbuf, x, gy, n, plan.n_pad, plan.tps, partial, P,
+                        cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden);
+    if (int rc = hip_status("siren_backward_stored (small)")) return rc;
+    const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 4096);
+    siren::launch_reduce(dim3((unsigned)rblocks), st, partial, plan.splits, P, gparams, 0, 0, 0);
+    return hip_status("siren_backward_stored (reduce)");
+}
+
 // ---- W4s: backward of the fused Laplacian (laplace_mse training) ------------------------------------------
 namespace {
 int check_jet(const siren_cfg* cfg) {

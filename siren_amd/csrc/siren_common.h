@@ -33,7 +33,10 @@ constexpr int MAX_LH_GRAD = 3;    // max hidden layers of the forward+grad kerne
 // only, sin epilogues without cos, output layer folded into a final serial epilogue).
 // MODE_JET (W4): forward-mode Taylor jet for the Laplacian — 4 coordinates x 4 jet streams (value, d/dx_1,
 // d/dx_2, sum_i d2/dx_i2) in the 16 MFMA columns, y / grad / Laplacian in one forward sweep.
-enum { MODE_W1 = 0, MODE_STORE = 1, MODE_FWD = 2, MODE_JET = 3 };
+// MODE_FWDS (W2 split, forward half): MODE_FWD + a_l tiles (wgrad layout) and cos(w z_l) (lane-major) to HBM, so
+// the backward needs no forward recompute. MODE_REV (W2 split, backward half): the L reverse GEMMs only, cos read
+// back from HBM, delta_l tiles stored like MODE_STORE.
+enum { MODE_W1 = 0, MODE_STORE = 1, MODE_FWD = 2, MODE_JET = 3, MODE_FWDS = 4, MODE_REV = 5 };
 // w1_kernel modifier bits (MODE & MODE_BASE is the mode proper): MODE_PROF records per-GEMM s_memtime stamps;
 // MODE_O1S specialises d_out == 1 with the all-ones output cotangent (gy == NULL); MODE_D(k) fixes d_in = k at
 // compile time. Both only remove runtime-uniform branches and selects from the epilogues (whose VALU count is the
@@ -43,7 +46,14 @@ constexpr int MODE_D(int k) { return k << 8; }
 constexpr int mode_din(int mode) { return (mode >> 8) & 7; }
 // MODE_PROF (diagnostics, siren_w1_phase_profile): s_memtime stamps at tile start, after each GEMM and at tile end
 constexpr int PROF_TILES = 4, PROF_EVENTS = 8, PROF_BLOCKS = 256;
-__host__ __device__ constexpr bool forward_only(int mode) { return mode == MODE_FWD || mode == MODE_JET; }
+__host__ __device__ constexpr bool forward_only(int mode) {
+    return mode == MODE_FWD || mode == MODE_JET || mode == MODE_FWDS;
+}
+// lane-major cos(w z_l) buffer of MODE_FWDS / MODE_REV: per (tile, wave) (LH + 1) layers x NB blocks x 64 lanes x f32x4
+// (one coalesced dwordx4 per lane per block): float offset of (tile, wave, layer, block, lane)
+__host__ __device__ constexpr int64_t cos_off(int64_t tile, int wave, int lh, int l, int b, int lane) {
+    return (((tile * WAVES + wave) * (lh + 1) + l) * NB + b) * 256 + lane * 4;
+}
 
 // Small-parameter block (head of the workspace, copied to LDS by every workgroup):
 //   [SM_W0,  +4H)  W0T[k][n] = W_0[n][k]  (k < d_in, zero padded to 4 rows)

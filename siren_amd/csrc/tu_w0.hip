@@ -19,4 +19,17 @@ void launch_w0(dim3 grid, hipStream_t st, const FusedArgs& a) {
 #undef SIREN_L
 }
 
+// MODE_FWDS: W0 + a_l tiles (a.abuf) and lane-major cos (a.dbuf) for the stored-forward W2 split
+void launch_w0s(dim3 grid, hipStream_t st, const FusedArgs& a) {
+#define SIREN_L(LHV)                                                                                             \
+    hipLaunchKernelGGL((w1_kernel<LHV, MODE_FWDS>), grid, dim3(THREADS), 0, st, a.ws, a.x, a.n, (const float*)nullptr, \
+                       a.y, (float*)nullptr, a.d, a.o, a.w0, a.w, a.abuf, a.dbuf, a.n_pad, (int64_t)0)
+    switch (a.lh) {
+        case 1: SIREN_L(1); break;
+        case 2: SIREN_L(2); break;
+        default: SIREN_L(3); break;
+    }
+#undef SIREN_L
+}
+
 }  // namespace siren

@@ -14,6 +14,12 @@ void launch_w1(int mode, dim3 grid, hipStream_t st, const FusedArgs& a) {
             case 2: SIREN_L(2, MODE_STORE); break;
             default: SIREN_L(3, MODE_STORE); break;
         }
+    } else if (mode == MODE_REV) {  // a.abuf = lane-major cos from MODE_FWDS, a.dbuf = delta tiles
+        switch (a.lh) {
+            case 1: SIREN_L(1, MODE_REV); break;
+            case 2: SIREN_L(2, MODE_REV); break;
+            default: SIREN_L(3, MODE_REV); break;
+        }
     } else if (mode == (MODE_W1 | MODE_PROF)) {
         SIREN_L(3, MODE_W1 | MODE_PROF);
     } else if (mode == (MODE_W1 | MODE_O1S | MODE_D(2)) && a.lh == 3) {

@@ -94,17 +94,25 @@ __device__ __forceinline__ void lgkm_wait(f32x4& a, f32x4& b) {
 }
 
 template <int MODE>
-constexpr int npasses() { return forward_only(MODE & MODE_BASE) ? 1 : 2; }
+constexpr int npasses() { return forward_only(MODE & MODE_BASE) || (MODE & MODE_BASE) == MODE_REV ? 1 : 2; }
+// first GEMM of a tile: MODE_REV runs only the reverse GEMMs G = LH .. 2 LH - 1 (its stream pointer starts at the
+// transposed slices, so slice indices are counted from G0)
+template <int MODE, int LH>
+constexpr int gemm0() { return (MODE & MODE_BASE) == MODE_REV ? LH : 0; }
+template <int MODE>
+constexpr bool is_rev() { return (MODE & MODE_BASE) == MODE_REV; }
 
 template <int LH, int MODE>
 struct W1State {
     f32x4 act[NB];     // B operand of the current GEMM (filled one block ahead)
     f32x4 acc[2][NB];  // ping-pong accumulators
-    f32x4 C[forward_only(MODE & MODE_BASE) ? 1 : LH][NB];  // cos(w z_l), l = 0 .. LH-1 (unused in forward-only modes)
+    f32x4 C[forward_only(MODE & MODE_BASE) || (MODE & MODE_BASE) == MODE_REV ? 1 : LH][NB];  // cos(w z_l), l < LH
+                                                                     // (unused in forward-only modes and REV)
     f32x4 pa0, pa1;    // prefetched first operand pair of the next slice
     float xv[MAXD];    // this lane's coordinate
     float gyv[MAXO];   // this lane's output cotangent
     float yp[MAXO];    // partial y over this lane's neurons
+    f32x4 cq[3];       // MODE_REV: cos blocks of the next epilogues, prefetched two slices ahead (slot e % 3)
 };
 
 struct W1Ctx {
@@ -117,8 +125,10 @@ struct W1Ctx {
     // undoes the first layer's scale in gx
     float w0, w, wsd, inv_s0;
     bool seed_ones;
-    float* abuf;  // STORE: lane-adjusted tile base of layer 0; layer l at + l * lstride
-    float* dbuf;
+    float* abuf;  // STORE / FWDS: lane-adjusted tile base of layer 0; layer l at + l * lstride
+    float* dbuf;  // STORE / REV: delta tiles, same layout
+    float* cst;   // FWDS: this lane's cos store base (cos_off(tile, wave, LH, 0, 0, lane))
+    const char* cbase;  // REV: wave-uniform cos base of (tile, wave) (SGPRs), + 16 * lane per lane
     bool more;    // persistent grid: this workgroup runs another coordinate tile after the current one, so the
                   // ring keeps streaming (slices 0..2 of the next tile are issued during the last 3 slices)
     int64_t lstride;
@@ -143,6 +153,17 @@ __device__ __forceinline__ void ring_issue4(const float* __restrict__ stream, fl
     const unsigned dst = lds_addr(ring + (s % W1_NBUF) * SLICE + wave * 1024);
 #pragma unroll
     for (int q = 0; q < 4; ++q) glds_x4(src + q * 1024, lane_off, dst + q * 1024);
+}
+
+// MODE_REV: cos block of epilogue index E (E = (G - LH) NB + b handles block b of reverse GEMM G's epilogue: layer
+// LH for the SEED epilogue G = LH, layer 2 LH - G for DELTA) as a saddr-form global_load_dwordx4 into cq[E % 3].
+// Issued before a ring issue, so the ring's counted s_waitcnt vmcnt(4) one slice later also covers it.
+template <int E, int LH, int MODE>
+__device__ __forceinline__ void cos_issue(W1State<LH, MODE>& st, const W1Ctx& cx) {
+    constexpr int GE = LH + E / NB, BE = E % NB;
+    constexpr int LC = GE == LH ? LH : 2 * LH - GE;
+    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(st.cq[E % 3]) : "v"(16u * cx.lane),
+                 "s"(cx.cbase + (LC * NB + BE) * 1024));
 }
 
 // ---- epilogue parameters (LDS) -------------------------------------------------------------------------
@@ -182,6 +203,8 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
     constexpr int KIND = epi_kind<G, LH>();
     constexpr bool STORE = (MODE & MODE_BASE) == MODE_STORE;
     constexpr bool FWD = forward_only(MODE & MODE_BASE);
+    constexpr bool FWDS = (MODE & MODE_BASE) == MODE_FWDS;
+    constexpr bool REV = is_rev<MODE>();
     if constexpr ((MODE & MODE_BASE) == MODE_JET && KIND == EPI_FIRST) {
         f32x4 z = cx.jcf[0] * ep.v[0];
 #pragma unroll
@@ -207,7 +230,8 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
             cs4[r] = cs;
         }
         if constexpr (!FWD) st.C[0][b] = pin(cs4);
-        if constexpr (STORE) store_block(cx.abuf, b, st.act[b]);
+        if constexpr (STORE || FWDS) store_block(cx.abuf, b, st.act[b]);
+        if constexpr (FWDS) *(f32x4*)(cx.cst + b * 256) = cs4;
     } else if constexpr (KIND == EPI_SINCOS) {
         const f32x4 z = st.acc[(G + 1) & 1][b] + ep.v[0];
         f32x4 cs4;
@@ -219,7 +243,18 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
             cs4[r] = cs;
         }
         if constexpr (!FWD) st.C[G][b] = to_agpr(cs4);
-        if constexpr (STORE) store_block(cx.abuf + G * cx.lstride, b, st.act[b]);
+        if constexpr (STORE || FWDS) store_block(cx.abuf + G * cx.lstride, b, st.act[b]);
+        if constexpr (FWDS) *(f32x4*)(cx.cst + (G * NB + b) * 256) = cs4;
+    } else if constexpr (KIND == EPI_SEED && REV) {
+        // delta_L = (gy Wout) . cos(w z_L) . w with cos from the forward's store
+        const f32x4 cs = st.cq[((G - LH) * NB + b) % 3];
+        f32x4 ga = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < MAXO; ++j)
+            if (j < cx.o && !cx.seed_ones) ga += st.gyv[j] * ep.v[1 + j];
+        if (cx.seed_ones) ga = ep.v[5];
+        st.act[b] = (ga * cs) * cx.wsd;
+        store_block(cx.dbuf + LH * cx.lstride, b, st.act[b]);
     } else if constexpr (KIND == EPI_SEED) {
         const f32x4 z = st.acc[(G + 1) & 1][b] + ep.v[0];
         f32x4 sn, cs;
@@ -245,8 +280,11 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
         if constexpr (STORE) store_block(cx.dbuf + LH * cx.lstride, b, st.act[b]);
     } else {
         constexpr int L = 2 * LH - G;  // delta_L = u_L . cos(w z_L) . w,  1 <= L < LH
-        st.act[b] = (st.acc[(G + 1) & 1][b] * from_agpr(st.C[L][b])) * cx.w;
-        if constexpr (STORE) store_block(cx.dbuf + L * cx.lstride, b, st.act[b]);
+        if constexpr (REV)
+            st.act[b] = (st.acc[(G + 1) & 1][b] * st.cq[((G - LH) * NB + b) % 3]) * cx.w;
+        else
+            st.act[b] = (st.acc[(G + 1) & 1][b] * from_agpr(st.C[L][b])) * cx.w;
+        if constexpr (STORE || REV) store_block(cx.dbuf + L * cx.lstride, b, st.act[b]);
     }
 }
 
@@ -255,7 +293,7 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
 template <int G, int KB, int LH, int MODE>
 __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx) {
     constexpr int NS = npasses<MODE>() * LH * NB;
-    constexpr int S = G * NB + KB;
+    constexpr int S = (G - gemm0<MODE, LH>()) * NB + KB;
     constexpr int SLOT = (S % W1_NBUF) * SLICE * 4;
     constexpr int NSLOT = ((S + 1) % W1_NBUF) * SLICE * 4;
     constexpr int KIND = epi_kind<G, LH>();
@@ -276,6 +314,11 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
                     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
                 else
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if constexpr (is_rev<MODE>()) {
+                    // the cos block issued one slice ago (epilogue S + 1) has landed; prefetch epilogue S + 2's
+                    asm volatile("" : "+v"(st.cq[(S + 1) % 3]));
+                    if constexpr (S + 2 < NS) cos_issue<S + 2, LH, MODE>(st, cx);
+                }
                 __builtin_amdgcn_s_barrier();
                 if (S + 3 < NS || cx.more) {
                     const float* sp = cx.stream;
@@ -351,7 +394,7 @@ __device__ __forceinline__ void prof_mark(const W1Ctx& cx, int ev) {
 
 template <int G, int LH, int MODE>
 __device__ __forceinline__ void w1_run(W1State<LH, MODE>& st, const W1Ctx& cx) {
-    if constexpr (G < npasses<MODE>() * LH) {
+    if constexpr (G < gemm0<MODE, LH>() + npasses<MODE>() * LH) {
         w1_gemm<G, LH, MODE>(st, cx);
         if constexpr ((MODE & MODE_PROF) != 0) prof_mark(cx, G + 1);
         w1_run<G + 1, LH, MODE>(st, cx);
@@ -370,6 +413,8 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
                                                         int64_t n_pad, int64_t ws_bstride) {
     constexpr bool STORE = (MODE & MODE_BASE) == MODE_STORE;
     constexpr bool JET = (MODE & MODE_BASE) == MODE_JET;
+    constexpr bool FWDS = (MODE & MODE_BASE) == MODE_FWDS;  // abuf = a_l tiles, dbuf = lane-major cos buffer
+    constexpr bool REV = is_rev<MODE>();                     // abuf = lane-major cos buffer, dbuf = delta tiles
     constexpr int NS = npasses<MODE>() * LH * NB;
     __shared__ __attribute__((aligned(16))) float lds[W1_NBUF * SLICE + small_floats_ct(LH)];
     W1Ctx cx;
@@ -408,7 +453,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
     cx.abuf = cx.dbuf = nullptr;
     cx.more = false;
     cx.prof = nullptr;
-    cx.stream = ws + small_pad(LH);
+    cx.stream = ws + small_pad(LH) + (REV ? (int64_t)LH * NB * SLICE : 0);
     cx.lstride = n_pad * H;
     const unsigned lds_base = (unsigned)(uintptr_t)((__attribute__((address_space(3))) float*)lds);
     cx.ring_vaddr = lds_base + cx.lane * 16;
@@ -472,10 +517,18 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
 #pragma unroll
             for (int k = 0; k < MAXD; ++k) cx.jcf[k] = cx.ja * st.xv[k] + (js == k + 1 ? 1.f : 0.f);
         }
-        if constexpr (STORE) {
+        if constexpr (STORE || FWDS || REV) {
             const int64_t toff = (tile * WAVES + cx.wave) * (H * 16) + 4 * cx.g * 16 + c;
-            cx.abuf = abuf + toff;
-            cx.dbuf = dbuf + toff;
+            if constexpr (!REV) cx.abuf = abuf + toff;
+            if constexpr (!FWDS) cx.dbuf = dbuf + toff;
+        }
+        if constexpr (FWDS) cx.cst = dbuf + cos_off(tile, cx.wave, LH, 0, 0, cx.lane);
+        if constexpr (REV) {
+            // cos blocks of the first two epilogues (SEED blocks 0, 1); later ones are prefetched by the slices
+            cx.cbase = (const char*)(abuf + cos_off(tile, cx.wave, LH, 0, 0, 0));
+            cos_issue<0, LH, MODE>(st, cx);
+            cos_issue<1, LH, MODE>(st, cx);
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(st.cq[0]), "+v"(st.cq[1])::"memory");
         }
 
         if constexpr ((MODE & MODE_PROF) != 0) {
@@ -485,7 +538,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
                           : nullptr;
             prof_mark(cx, 0);
         }
-        w1_run<0, LH, MODE>(st, cx);
+        w1_run<gemm0<MODE, LH>(), LH, MODE>(st, cx);
 
         if constexpr (JET) {
             // last hidden layer's jet, output layer per stream, then y / grad / Laplacian from the quad's lanes
@@ -516,19 +569,24 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
                 if (js == 3) abuf[coord] = tot;
                 else if (js >= 1 && js <= d && gx != nullptr) gx[coord * d + js - 1] = tot;
             }
-        } else if constexpr ((MODE & MODE_BASE) == MODE_FWD) {
+        } else if constexpr ((MODE & MODE_BASE) == MODE_FWD || FWDS) {
             // last hidden layer: z_L = acc + b_L, a_L = sin(w z_L), y = a_L Wout^T + bout (serial epilogue)
             constexpr int GL = (LH - 1) & 1;
 #pragma unroll
             for (int rb = 0; rb < NB; ++rb) {
                 const int nb = 16 * rb + 4 * cx.g;
                 const f32x4 z = st.acc[GL][rb] + *(const f32x4*)(sm + SM_BIAS + LH * H + nb);
-                f32x4 sn;
+                f32x4 sn, cs4;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     float a, cc;
                     sincos_rev(z[r], a, cc);
                     sn[r] = a;
+                    cs4[r] = cc;
+                }
+                if constexpr (FWDS) {
+                    store_block(cx.abuf + LH * cx.lstride, rb, sn);
+                    *(f32x4*)(cx.cst + (LH * NB + rb) * 256) = cs4;
                 }
 #pragma unroll
                 for (int j = 0; j < MAXO; ++j) {
@@ -557,9 +615,15 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
             // delta_0 = u_0 . cos(w0 z_0) . w0 (u_0 = s W_1^T delta_1 from the scaled pack: cx.w0 = w0 / s);
             // gx = delta_0 W0 (the LDS W0^T carries s0: cx.inv_s0)
             constexpr int GL = (2 * LH - 1) & 1;
+            if constexpr (REV) {
+                const f32x4* c0 = (const f32x4*)(cx.cbase + 16 * cx.lane);
 #pragma unroll
-            for (int rb = 0; rb < NB; ++rb) st.act[rb] = (st.acc[GL][rb] * st.C[0][rb]) * cx.w0;
-            if constexpr (STORE) store_tile(cx.dbuf, st.act);
+                for (int rb = 0; rb < NB; ++rb) st.act[rb] = (st.acc[GL][rb] * c0[rb * 64]) * cx.w0;
+            } else {
+#pragma unroll
+                for (int rb = 0; rb < NB; ++rb) st.act[rb] = (st.acc[GL][rb] * st.C[0][rb]) * cx.w0;
+            }
+            if constexpr (STORE || REV) store_tile(cx.dbuf, st.act);
 #pragma unroll
             for (int k = 0; k < MAXD; ++k) {
                 if (k < d) {

@@ -46,6 +46,10 @@ class SirenEngine:
         # the W4 jet kernel (fused Laplacian): hidden 256, d_in <= 2, linear output, 1..5 hidden layers
         self.laplace_supported = (self.supported and int(hidden) == 256 and int(d_in) <= 2 and 1 <= n_hidden <= 5
                                   and bool(outermost_linear) and omega_first != 0 and omega_hidden != 0)
+        # stored-forward W2 split: training forward keeps a_l / cos, backward is reverse-only (hidden 256)
+        self.stored_supported = (self.supported and int(hidden) == 256 and 1 <= n_hidden <= 3
+                                 and bool(outermost_linear) and omega_first != 0 and omega_hidden != 0
+                                 and not (int(flags) & 1))
         self.second_order_supported = (self.supported and int(hidden) == 256 and 1 <= n_hidden <= 3
                                        and int(d_out) <= 4 and bool(outermost_linear))
 
@@ -245,6 +249,33 @@ class SirenEngine:
         _lib.check(self.lib.siren_backward_batched(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, B, _ptr(gy),
                                                    _ptr(tws), _ptr(gx), _ptr(gp), _stream(x.device)),
                    'siren_backward_batched')
+        return gx, gp
+
+    def forward_store(self, ws, x):
+        """Training forward (stored-forward W2 split): y plus the a_l tiles and cos(w z_l) the reverse-only
+        backward needs, kept in a workspace returned with y."""
+        self._require()
+        x = self._check_x(x)
+        n = x.shape[0]
+        cnt = ctypes.c_int64()
+        _lib.check(self.lib.siren_train_stored_ws_floats(ctypes.byref(self.cfg), n, ctypes.byref(cnt)),
+                   'siren_train_stored_ws_floats')
+        tws = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
+        y = torch.empty(n, self.cfg.d_out, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_forward_store(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(y), _ptr(tws),
+                                                _stream(x.device)), 'siren_forward_store')
+        return y, tws
+
+    def backward_stored(self, ws, x, gy, tws):
+        """W2 backward from forward_store's workspace: reverse sweep only + wgrad. Returns (gx, gparams)."""
+        self._require()
+        x = self._check_x(x)
+        n = x.shape[0]
+        gy = gy.contiguous()
+        gx = torch.empty(n, self.cfg.d_in, dtype=torch.float32, device=x.device)
+        gp = torch.empty(self.param_count, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_backward_stored(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(gy), _ptr(tws),
+                                                  _ptr(gx), _ptr(gp), _stream(x.device)), 'siren_backward_stored')
         return gx, gp
 
     def second_order(self, ws, x, v, want_theta=True, gy=None, u=None, want_ydot=False):

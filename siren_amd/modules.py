@@ -182,7 +182,8 @@ def _fused_apply(engine, jet, coords, weights_biases):
             and torch.is_grad_enabled() and x2d.requires_grad):
         y, _ = SirenJetFunction.apply(engine, x2d, flat)  # J stays alive as the node's second output
     else:
-        y = SirenFunction.apply(engine, jet, x2d, flat)
+        # a graph that will want parameter gradients: the forward keeps a_l / cos for a reverse-only backward
+        y = SirenFunction.apply(engine, jet, x2d, flat, torch.is_grad_enabled() and flat.requires_grad)
     return y.view(*lead, y.shape[-1])
 
 

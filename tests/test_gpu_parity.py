@@ -442,3 +442,51 @@ def test_second_order_losses_use_hip_kernel(cuda, g1, jet, monkeypatch):
     for k, p in m.named_parameters():
         ref = g1['G1_gradients_mse_grad_' + k]
         assert np.max(np.abs(p.grad.cpu().numpy() - ref)) <= 1e-4 * max(np.max(np.abs(ref)), 1e-30) + 1e-12, k
+
+
+# ---------------------------------------------------------------------------------------------------------
+# stored-forward W2 split (siren_forward_store + siren_backward_stored)
+# ---------------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize('n,d,L,o', [(1, 2, 3, 1), (4097, 2, 3, 1), (1000, 3, 3, 3), (777, 4, 2, 2), (300, 1, 1, 4)])
+def test_stored_forward_split_matches_recompute(cuda, n, d, L, o):
+    """The split (forward keeps a_l / cos, reverse-only backward) returns the recompute pipeline's y, gx and
+    theta-grads, and both match fp64 autograd."""
+    layers = random_layers(d, L, o, seed=3 * n + L)
+    eng = engine(d, L, o)
+    assert eng.stored_supported
+    ws = eng.pack(to_dev(O.flatten(layers), cuda))
+    rng = np.random.default_rng(n)
+    x = to_dev(rng.uniform(-1, 1, (n, d)), cuda)
+    gy = to_dev(rng.normal(size=(n, o)), cuda)
+    y_s, tws = eng.forward_store(ws, x)
+    gx_s, gp_s = eng.backward_stored(ws, x, gy, tws)
+    y_r = eng.forward(ws, x)
+    gx_r, gp_r = eng.backward_params(ws, x, gy)
+    assert torch.equal(y_s, y_r)
+    scale_x = max(1., float(gx_r.abs().max()))
+    assert float((gx_s - gx_r).abs().max()) <= 1e-6 * scale_x
+    assert float((gp_s - gp_r).abs().max()) <= 1e-6 * float(gp_r.abs().max())
+    xt = torch.tensor(x.cpu().numpy(), dtype=torch.float64, requires_grad=True)
+    params = [torch.tensor(t, dtype=torch.float64, requires_grad=True) for W, b in layers for t in (W, b)]
+    yt = O.torch_forward(xt, params)
+    g = torch.autograd.grad(yt, [xt] + params, torch.tensor(gy.cpu().numpy(), dtype=torch.float64))
+    rgp = torch.cat([t.reshape(-1) for t in g[1:]]).numpy()
+    assert np.max(np.abs(gp_s.cpu().numpy() - rgp)) <= 1e-4 * np.max(np.abs(rgp))
+    assert np.max(np.abs(gx_s.cpu().numpy() - g[0].numpy())) <= tol_rel(g[0].numpy())
+
+
+def test_training_uses_stored_forward(cuda, g1, monkeypatch):
+    """image_mse training through the modules runs forward_store + backward_stored (not the recompute)."""
+    from siren_amd import loss_functions as Lf
+    from siren_amd.engine import SirenEngine
+    def boom(*a, **k):
+        raise AssertionError('recompute backward used')
+    monkeypatch.setattr(SirenEngine, 'backward_params', boom)
+    m = load_model(g1, cuda, jet=False)
+    out = m({'coords': to_dev(g1['coords'], cuda)})
+    loss = Lf.image_mse(None, out, {'img': to_dev(g1['gt_img'], cuda)})['img_loss']
+    m.zero_grad()
+    loss.backward()
+    for k, p in m.named_parameters():
+        ref = g1['G1_image_mse_grad_' + k]
+        assert np.max(np.abs(p.grad.cpu().numpy() - ref)) <= 1e-4 * max(np.max(np.abs(ref)), 1e-30) + 1e-12, k

@@ -45,6 +45,21 @@ def main():
                            ('W1 forward+vjp_x', lambda: eng.forward_grad(ws, x, gy), 2 * F),
                            ('W2 backward (store+wgrad+small+reduce)', lambda: eng.backward_params(ws, x, gy), 3 * F)):
         report(name, timed(fn), work, a.n)
+    if eng.stored_supported:
+        # stored-forward split: the training forward keeps a_l / cos, the backward is reverse-only; a W2 unit is the
+        # forward (W0 role) + the backward, so compare W0 + W2-backward above with this pair
+        state = {}
+
+        def fwd_store():
+            state['y'], state['tws'] = eng.forward_store(ws, x)
+        fwd_store()
+        t_fs = timed(fwd_store)
+        t_bs = timed(lambda: eng.backward_stored(ws, x, gy, state['tws']))
+        report('W2 split: forward_store', t_fs, F, a.n)
+        report('W2 split: backward_stored (rev+wgrad+...)', t_bs, 2 * F, a.n)
+        report('W2 split: forward_store + backward_stored', t_fs + t_bs, 3 * F, a.n)
+        t_w0, t_w2 = timed(lambda: eng.forward(ws, x)), timed(lambda: eng.backward_params(ws, x, gy))
+        report('W2 recompute: forward + backward_params', t_w0 + t_w2, 3 * F, a.n)
     if eng.laplace_supported:
         # W4 algorithmic unit: (1 + 2d) F; the jet kernel executes 4F (4 MFMA columns/coord)
         report('W4 y+grad+Laplacian (jet, 1 launch)', timed(lambda: eng.forward_laplace(ws, x, True, True)),
