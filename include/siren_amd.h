@@ -211,7 +211,7 @@ int32_t siren_forward_grad_batched(const siren_cfg* cfg, const float* ws, const 
 int32_t siren_backward_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
                                const float* gy, float* tws, float* gx, float* gparams, void* stream);
 
-/* ---- stored-forward W2 split (hidden 256, linear output, 1..3 hidden layers) ----------------------------------
+/* ---- stored-forward W2 split (linear output; hidden 256: 1..3 hidden layers, hidden 512: 1..8) --------------
  * The training forward (model(model_input), training.py:72) keeps what the backward needs, so
  * train_loss.backward() (training.py:96) runs the L reverse GEMMs only instead of recomputing the forward:
  *   siren_forward_store : W0 (y) + a_l tiles and cos(w z_l) of every sine layer into tws

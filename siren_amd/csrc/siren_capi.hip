@@ -292,17 +292,25 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
 
 // ---- stored-forward W2 split: the training forward keeps a_l and cos(w z_l) so the backward is reverse-only ----
 bool stored_ok(const siren_cfg* cfg) {
-    return w1_ok(cfg) && cfg->outermost_linear && cfg->n_hidden <= siren::MAX_LH_GRAD &&
-           (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0;
+    if (!cfg->outermost_linear || (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) != 0) return false;
+    return wide(cfg) || (w1_ok(cfg) && cfg->n_hidden <= siren::MAX_LH_GRAD);
+}
+// stored-split workspace: [a_l tiles][delta_l tiles][partial slabs][hidden 512: cos scratch of L + 1 layers]
+// [hidden 256: lane-major cos of L + 1 layers]
+float* stored_cos(const siren_cfg* cfg, const TrainPlan& plan, float* tws) {
+    return wide(cfg) ? tws + 2 * plan.act_floats + plan.partial_floats : tws + plan.total;
 }
 
 int32_t siren_train_stored_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (!stored_ok(cfg))
-        return fail(SIREN_EUNSUPPORTED, "the stored-forward W2 split covers hidden 256, linear output, 1..3 hidden layers");
+        return fail(SIREN_EUNSUPPORTED, "the stored-forward W2 split needs a linear output layer (hidden 256: 1..3 "
+                                        "hidden layers)");
     if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
     const TrainPlan plan(cfg, n);
-    *count = plan.total + plan.act_floats;  // + the lane-major cos buffer (same size as the a_l tiles)
+    // hidden 256: + the lane-major cos buffer (L + 1 layers, the size of the a_l tiles); hidden 512: the cos
+    // scratch grows from L to L + 1 layers
+    *count = plan.total + (wide(cfg) ? plan.n_pad * cfg->hidden : plan.act_floats);
     return SIREN_OK;
 }
 
@@ -316,10 +324,17 @@ int32_t siren_forward_store(const siren_cfg* cfg, const float* ws, const float* 
     if (ws == nullptr || x == nullptr || y == nullptr || tws == nullptr) return fail(SIREN_EINVAL, "ws/x/y/tws is NULL");
     const TrainPlan plan(cfg, n);
     float* abuf = tws;
-    float* cbuf = tws + plan.total;
+    float* cbuf = stored_cos(cfg, plan, tws);
+    const dim3 grid((unsigned)(plan.n_pad / siren::TILE));
+    if (wide(cfg)) {
+        siren::FusedArgs fa{ws, x, n, nullptr, y, nullptr, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first,
+                            cfg->omega_hidden, 0, abuf, nullptr, plan.n_pad};
+        siren::launch_wide(siren::MODE_FWDS, grid, (hipStream_t)stream, fa, cbuf);
+        return hip_status("siren_forward_store");
+    }
     siren::FusedArgs fa{w1_ws(cfg, ws), x, n, nullptr, y, nullptr, cfg->d_in, cfg->d_out, cfg->n_hidden,
                         cfg->omega_first, cfg->omega_hidden, 0, abuf, cbuf, plan.n_pad};
-    siren::launch_w0s(dim3((unsigned)(plan.n_pad / siren::TILE)), (hipStream_t)stream, fa);
+    siren::launch_w0s(grid, (hipStream_t)stream, fa);
     return hip_status("siren_forward_store");
 }
 
@@ -342,13 +357,20 @@ int32_t siren_backward_stored(const siren_cfg* cfg, const float* ws, const float
     float* abuf = tws;
     float* dbuf = tws + plan.act_floats;
     float* partial = tws + 2 * plan.act_floats;
-    float* cbuf = tws + plan.total;
-    siren::FusedArgs fa{w1_ws(cfg, ws), x, n, gy, nullptr, gx, cfg->d_in, cfg->d_out, cfg->n_hidden,
-                        cfg->omega_first, cfg->omega_hidden, 0, cbuf, dbuf, plan.n_pad};
-    siren::launch_w1(siren::MODE_REV, tile_grid(cfg, plan.n_pad / siren::TILE, 1), st, fa);
+    float* cbuf = stored_cos(cfg, plan, tws);
+    if (wide(cfg)) {
+        siren::FusedArgs fa{ws, x, n, gy, nullptr, gx, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first,
+                            cfg->omega_hidden, 0, nullptr, dbuf, plan.n_pad};
+        siren::launch_wide(siren::MODE_REV, dim3((unsigned)(plan.n_pad / siren::TILE)), st, fa, cbuf);
+    } else {
+        siren::FusedArgs fa{w1_ws(cfg, ws), x, n, gy, nullptr, gx, cfg->d_in, cfg->d_out, cfg->n_hidden,
+                            cfg->omega_first, cfg->omega_hidden, 0, cbuf, dbuf, plan.n_pad};
+        siren::launch_w1(siren::MODE_REV, tile_grid(cfg, plan.n_pad / siren::TILE, 1), st, fa);
+    }
     if (int rc = hip_status("siren_backward_stored (reverse)")) return rc;
-    siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden, 1), st, abuf, dbuf, plan.n_pad, plan.tps,
-                        partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1, cfg->hidden);
+    const unsigned quads = (unsigned)((cfg->hidden / 256) * (cfg->hidden / 256));
+    siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden, quads), st, abuf, dbuf, plan.n_pad,
+                        plan.tps, partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1, cfg->hidden);
     if (int rc = hip_status("siren_backward_stored (wgrad)")) return rc;
     siren::launch_small(dim3((unsigned)plan.splits), st, abuf, dbuf, x, gy, n, plan.n_pad, plan.tps, partial, P,
                         cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden);

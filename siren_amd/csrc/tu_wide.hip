@@ -12,6 +12,10 @@ void launch_wide(int mode, dim3 grid, hipStream_t st, const FusedArgs& a, float*
         SIREN_L(MODE_FWD);
     else if (mode == MODE_STORE)
         SIREN_L(MODE_STORE);
+    else if (mode == MODE_FWDS)
+        SIREN_L(MODE_FWDS);
+    else if (mode == MODE_REV)
+        SIREN_L(MODE_REV);
     else
         SIREN_L(MODE_W1);
 #undef SIREN_L

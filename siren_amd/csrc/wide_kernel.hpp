@@ -16,7 +16,9 @@
 //
 // Modes (siren_common.h): MODE_FWD (W0: y only), MODE_W1 (y and vjp_x), MODE_STORE (W2 backward stage 1:
 // additionally a_l and delta_l of every layer to abuf / dbuf in the [l][tile][neuron][16] layout that
-// wgrad_kernel / small_kernel read with h = 512).
+// wgrad_kernel / small_kernel read with h = 512). Stored-forward W2 split: MODE_FWDS = the forward passes with
+// a_l tiles to abuf and cos(w z_l) of layers 0..L (L + 1 scratch layers) to the scratch; MODE_REV = the seed from
+// the stored cos(w z_L) and the L reverse passes only, delta_l tiles to dbuf.
 #include "siren_common.h"
 #include "siren_params.h"
 
@@ -89,8 +91,11 @@ __global__ __launch_bounds__(THREADS, 1) void wide_kernel(
     const float* __restrict__ ws, const float* __restrict__ x, int64_t n, const float* __restrict__ gy,
     float* __restrict__ y, float* __restrict__ gx, int d, int o, int lh, float w0, float w, int final_sine,
     float* __restrict__ spill, float* __restrict__ abuf, float* __restrict__ dbuf, int64_t n_pad) {
-    constexpr bool GRAD = MODE != MODE_FWD;
-    constexpr bool STORE = MODE == MODE_STORE;
+    constexpr bool FWDS = MODE == MODE_FWDS, REV = MODE == MODE_REV;
+    constexpr bool GRAD = MODE == MODE_W1 || MODE == MODE_STORE || REV;  // runs the reverse passes
+    constexpr bool SPILLC = GRAD || FWDS;                                // forward writes cos to the scratch
+    constexpr bool STORE = MODE == MODE_STORE || FWDS;                   // a_l tiles (STORE, FWDS)
+    constexpr bool DSTORE = MODE == MODE_STORE || REV;                   // delta_l tiles (STORE, REV)
     __shared__ __attribute__((aligned(16))) float lds[WNBUF * WSLICE + WSMALL_MAX];
     const SmallLayout L(WH);
     float* ring = lds;
@@ -99,6 +104,7 @@ __global__ __launch_bounds__(THREADS, 1) void wide_kernel(
     const int g = lane >> 4, c = lane & 15;
     const int npass = (GRAD ? 2 : 1) * lh;
     const int nslices = npass * WNB;
+    const int p0 = REV ? lh : 0;  // REV: reverse passes only (slices from lh * WNB on)
     const float* stream = ws + L.pad(lh);
 
     {
@@ -115,13 +121,30 @@ __global__ __launch_bounds__(THREADS, 1) void wide_kernel(
 #pragma unroll
     for (int k = 0; k < MAXD; ++k) xv[k] = (valid && k < d) ? x[coord * d + k] : 0.f;
     __syncthreads();
-    wring_issue(stream, ring, 0, nslices, wave, lane);
-    wring_issue(stream, ring, 1, nslices, wave, lane);
+    int s = p0 * WNB;
+    wring_issue(stream, ring, s, nslices, wave, lane);
+    wring_issue(stream, ring, s + 1, nslices, wave, lane);
 
     // ---- first layer (K = d_in) on VALU ----------------------------------------------------------------
     f32x4 act[WNB], acc[WNB];
+    if constexpr (REV) {
+        // seed delta_L = (gy Wout) . cos(w z_L) . w from the forward's stored cos
+        float gyv[MAXO];
 #pragma unroll
-    for (int rb = 0; rb < WNB; ++rb) {
+        for (int j = 0; j < MAXO; ++j) gyv[j] = (j < o) ? (gy == nullptr ? 1.f : (valid ? gy[coord * o + j] : 0.f)) : 0.f;
+        const float* cp = sp + (int64_t)lh * lstride;
+#pragma unroll
+        for (int rb = 0; rb < WNB; ++rb) {
+            f32x4 ga = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < MAXO; ++j)
+                if (j < o) ga += gyv[j] * *(const f32x4*)(sm + L.wo + j * WH + 16 * rb + 4 * g);
+            act[rb] = (ga * *(const f32x4*)(cp + rb * 256)) * w;
+        }
+        wstore_tile(dbuf + (int64_t)lh * lstride + toff, act);
+    }
+#pragma unroll
+    for (int rb = 0; rb < (REV ? 0 : WNB); ++rb) {
         const int nb = 16 * rb + 4 * g;
         f32x4 z = *(const f32x4*)(sm + L.bias + nb);
 #pragma unroll
@@ -136,15 +159,14 @@ __global__ __launch_bounds__(THREADS, 1) void wide_kernel(
             cs[r] = cn;
         }
         act[rb] = sn;
-        if (GRAD) *(f32x4*)(sp + rb * 256) = cs;
+        if (SPILLC) *(f32x4*)(sp + rb * 256) = cs;
     }
-    if (STORE) wstore_tile(abuf + toff, act);
+    if (STORE && !REV) wstore_tile(abuf + toff, act);
 
     // ---- 2 L layer passes through one layer body: forward l = 1..L, then reverse l = L..1 ----------------
-    int s = 0;
     float yp[MAXO] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
-    for (int p = 0; p < npass; ++p) {
+    for (int p = p0; p < npass; ++p) {
 #pragma unroll
         for (int ob = 0; ob < WNB; ++ob) acc[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -170,7 +192,7 @@ __global__ __launch_bounds__(THREADS, 1) void wide_kernel(
                     cs[r] = cn;
                 }
                 act[rb] = sn;
-                if (GRAD) *(f32x4*)(sp + (int64_t)l * lstride + rb * 256) = cs;
+                if (SPILLC) *(f32x4*)(sp + (int64_t)l * lstride + rb * 256) = cs;
             }
             if (STORE) wstore_tile(abuf + (int64_t)l * lstride + toff, act);
         } else if (p == lh - 1) {
@@ -188,6 +210,7 @@ __global__ __launch_bounds__(THREADS, 1) void wide_kernel(
                     sn[r] = a;
                     act[rb][r] = cn;
                 }
+                if (FWDS) *(f32x4*)(sp + (int64_t)lh * lstride + rb * 256) = act[rb];
                 if (STORE) {
                     store_block(ap, 0, sn);
                     ap += 256;
@@ -230,7 +253,7 @@ __global__ __launch_bounds__(THREADS, 1) void wide_kernel(
                     if (j < o) ga += gyv[j] * *(const f32x4*)(sm + L.wo + j * WH + 16 * rb + 4 * g);
                 act[rb] = (ga * act[rb]) * w;
             }
-            if (STORE) wstore_tile(dbuf + (int64_t)lh * lstride + toff, act);
+            if (DSTORE) wstore_tile(dbuf + (int64_t)lh * lstride + toff, act);
         } else {
             // reverse pass through W_l (l = 2L - p): delta_{l-1} = (delta_l W_l) . cos(w z_{l-1}) . w_{l-1}
             const int lm = 2 * lh - p - 1;
@@ -238,7 +261,7 @@ __global__ __launch_bounds__(THREADS, 1) void wide_kernel(
             const float* cp = sp + (int64_t)lm * lstride;
 #pragma unroll
             for (int rb = 0; rb < WNB; ++rb) act[rb] = (acc[rb] * *(const f32x4*)(cp + rb * 256)) * wl;
-            if (STORE) wstore_tile(dbuf + (int64_t)lm * lstride + toff, act);
+            if (DSTORE) wstore_tile(dbuf + (int64_t)lm * lstride + toff, act);
         }
     }
 

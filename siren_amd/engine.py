@@ -46,10 +46,10 @@ class SirenEngine:
         # the W4 jet kernel (fused Laplacian): hidden 256, d_in <= 2, linear output, 1..5 hidden layers
         self.laplace_supported = (self.supported and int(hidden) == 256 and int(d_in) <= 2 and 1 <= n_hidden <= 5
                                   and bool(outermost_linear) and omega_first != 0 and omega_hidden != 0)
-        # stored-forward W2 split: training forward keeps a_l / cos, backward is reverse-only (hidden 256)
-        self.stored_supported = (self.supported and int(hidden) == 256 and 1 <= n_hidden <= 3
-                                 and bool(outermost_linear) and omega_first != 0 and omega_hidden != 0
-                                 and not (int(flags) & 1))
+        # stored-forward W2 split: training forward keeps a_l / cos, backward is reverse-only
+        self.stored_supported = (self.supported and bool(outermost_linear) and not (int(flags) & 1) and
+                                 (int(hidden) == 512 or (1 <= n_hidden <= 3 and omega_first != 0
+                                                         and omega_hidden != 0)))
         self.second_order_supported = (self.supported and int(hidden) == 256 and 1 <= n_hidden <= 3
                                        and int(d_out) <= 4 and bool(outermost_linear))
 

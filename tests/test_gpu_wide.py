@@ -137,3 +137,30 @@ def test_module_image_fit_step_wide(cuda, g4):
     for name, p in m.named_parameters():
         ref = g4['G4_image_mse_grad_' + name]
         assert np.max(np.abs(p.grad.cpu().numpy() - ref)) <= 1e-4 * max(1e-6, np.max(np.abs(ref))) + 1e-9, name
+
+
+@pytest.mark.parametrize('n,d,L,o', [(1, 3, 3, 3), (4097, 3, 3, 3), (700, 2, 1, 1), (333, 4, 5, 2)])
+def test_wide_stored_forward_split_matches_recompute(cuda, n, d, L, o):
+    """Hidden 512 stored-forward split (wide_kernel MODE_FWDS / MODE_REV) == the recompute pipeline; vs fp64."""
+    layers = random_layers(d, L, o, seed=5 * n + L)
+    eng = wide_engine(d, L, o)
+    assert eng.stored_supported
+    ws = eng.pack(to_dev(O.flatten(layers), cuda))
+    rng = np.random.default_rng(n + 1)
+    x = to_dev(rng.uniform(-1, 1, (n, d)), cuda)
+    gy = to_dev(rng.normal(size=(n, o)), cuda)
+    y_s, tws = eng.forward_store(ws, x)
+    gx_s, gp_s = eng.backward_stored(ws, x, gy, tws)
+    y_r = eng.forward(ws, x)
+    assert torch.equal(y_s, y_r)
+    if eng.grad_supported:
+        gx_r, gp_r = eng.backward_params(ws, x, gy)
+        assert float((gx_s - gx_r).abs().max()) <= 1e-6 * max(1., float(gx_r.abs().max()))
+        assert float((gp_s - gp_r).abs().max()) <= 1e-6 * float(gp_r.abs().max())
+    xt = torch.tensor(x.cpu().numpy(), dtype=torch.float64, requires_grad=True)
+    params = [torch.tensor(t, dtype=torch.float64, requires_grad=True) for W, b in layers for t in (W, b)]
+    yt = O.torch_forward(xt, params)
+    g = torch.autograd.grad(yt, [xt] + params, torch.tensor(gy.cpu().numpy(), dtype=torch.float64))
+    rgp = torch.cat([t.reshape(-1) for t in g[1:]]).numpy()
+    assert np.max(np.abs(gp_s.cpu().numpy() - rgp)) <= 1e-4 * np.max(np.abs(rgp))
+    assert np.max(np.abs(gx_s.cpu().numpy() - g[0].numpy())) <= tol_rel(g[0].numpy())
