@@ -224,6 +224,16 @@ int32_t siren_forward_store(const siren_cfg* cfg, const float* ws, const float* 
 int32_t siren_backward_stored(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* gy,
                               float* tws, float* gx, float* gparams, void* stream);
 
+/* Stored jet forward for gradient losses (hidden 256): y and J = sum_j dPhi_j/dx (siren_forward_grad's outputs with
+ * gy = ones) as siren_forward_store + a reverse-only sweep from the stored cos, leaving a_l / cos in tws
+ * (siren_train_stored_ws_floats) for siren_second_order_kept. */
+int32_t siren_forward_grad_store(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y,
+                                 float* gx, float* tws, void* stream);
+/* siren_second_order_seeded from a stored forward (kept = siren_forward_grad_store's / siren_forward_store's tws):
+ * the hidden layers run the tangent GEMMs only (the primal a_l and cos come from kept). tws as siren_second_order. */
+int32_t siren_second_order_kept(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
+                                const float* gy, float* kept, float* tws, float* gx, float* gparams, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -114,9 +114,14 @@ class SirenJetFunction(torch.autograd.Function):
     for the gradient terms)."""
 
     @staticmethod
-    def forward(ctx, engine, x, flat):
+    def forward(ctx, engine, x, flat, store=False):
         ws = engine.pack(flat)
-        y, J = engine.forward_grad(ws, x)
+        ctx.tws = None
+        if store and engine.stored_supported and engine.cfg.hidden == 256 and STORED_FORWARD:
+            # training: keep a_l / cos so the backward (seeded W3) skips the primal forward GEMMs
+            y, J, ctx.tws = engine.forward_grad_store(ws, x)
+        else:
+            y, J = engine.forward_grad(ws, x)
         ctx.engine, ctx.ws = engine, ws
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(x, flat, J)
@@ -130,25 +135,28 @@ class SirenJetFunction(torch.autograd.Function):
         need_x = ctx.needs_input_grad[1] and _will_execute(ctx, 0)
         need_p = ctx.needs_input_grad[2] and _will_execute(ctx, 1)
         if (gy is None and gJ is None) or not (need_x or need_p):
-            return None, None, None
+            return None, None, None, None
         gy = gy.contiguous() if gy is not None else None
         gJ = gJ.contiguous() if gJ is not None else None
         gx = gp = None
         if not torch.is_grad_enabled():
             if gJ is None:  # first order only
                 if need_p:
-                    gx, gp = engine.backward_params(ws, x, gy)
+                    if ctx.tws is not None:
+                        gx, gp = engine.backward_stored(ws, x, gy, ctx.tws)
+                    else:
+                        gx, gp = engine.backward_params(ws, x, gy)
                 else:
                     gx = gy * J
             elif engine.second_order_supported:
-                gx, gp = engine.second_order(ws, x, gJ, want_theta=need_p, gy=gy)
+                gx, gp = engine.second_order(ws, x, gJ, want_theta=need_p, gy=gy, kept=ctx.tws)
             else:
                 gx, gp = _torch_path.jacobian_vjp(engine.cfg, x, flat, gJ, create_graph=False)
                 if gy is not None:
                     gx = gx + gy * J
                     if need_p:
                         gp = gp + engine.backward_params(ws, x, gy)[1]
-            return None, (gx if need_x else None), (gp if need_p else None)
+            return None, (gx if need_x else None), (gp if need_p else None), None
         # create_graph=True: differentiable in (x, theta, gy, gJ); J here is this node's own output 1
         if need_x:
             gx = gy * J if gy is not None else None
@@ -164,7 +172,7 @@ class SirenJetFunction(torch.autograd.Function):
             if gJ is not None:
                 _, gpj = _torch_path.jacobian_vjp(engine.cfg, x, flat, gJ, create_graph=True)
                 gp = gpj if gp is None else gp + gpj
-        return None, gx, gp
+        return None, gx, gp, None
 
 
 class SirenHVP(torch.autograd.Function):

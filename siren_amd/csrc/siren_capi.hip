@@ -485,9 +485,9 @@ int32_t siren_second_order_seeded(const siren_cfg* cfg, const float* ws, const f
     return siren_second_order_ex(cfg, ws, x, n, v, nullptr, gy, tws, gx, gparams, nullptr, stream);
 }
 
-int32_t siren_second_order_ex(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
-                              const float* u, const float* gy, float* tws, float* gx, float* gparams, float* ydot,
-                              void* stream) {
+static int32_t second_order_impl(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
+                          const float* u, const float* gy, float* tws, float* gx, float* gparams, float* ydot,
+                          float* kept, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (cfg->n_hidden > siren::MAX_LH_GRAD)
         return fail(SIREN_EUNSUPPORTED, "siren_second_order needs 1 <= num_hidden_layers <= 3");
@@ -510,9 +510,16 @@ int32_t siren_second_order_ex(const siren_cfg* cfg, const float* ws, const float
     float* D = At + plan.buf_floats;
     float* Dt = D + plan.buf_floats;
     float* partial = Dt + plan.buf_floats;
+    const float *kA = nullptr, *kC = nullptr;
+    if (kept != nullptr) {  // the stored jet forward's a_l tiles double as A
+        const TrainPlan tp(cfg, n);
+        kA = kept;
+        kC = stored_cos(cfg, tp, kept);
+        A = kept;
+    }
     const dim3 grid((unsigned)(plan.n_pad / siren::TILE));
     siren::launch_w3(theta, grid, st, ws, x, v, gy, u, ydot, cfg->d_out, n, gx, spill, A, At, D, Dt, plan.n_pad,
-                     cfg->d_in, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden);
+                     cfg->d_in, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, kA, kC);
     if (int rc = hip_status("siren_second_order (w3)")) return rc;
     if (!theta) return SIREN_OK;
     const dim3 wgrid((unsigned)plan.splits, (unsigned)cfg->n_hidden);
@@ -530,6 +537,34 @@ int32_t siren_second_order_ex(const siren_cfg* cfg, const float* ws, const float
     siren::launch_reduce(dim3((unsigned)rblocks), st, partial, plan.splits, P, gparams, plan.splits, off.hidden0,
                          off.wout);
     return hip_status("siren_second_order (reduce)");
+}
+
+int32_t siren_second_order_ex(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
+                              const float* u, const float* gy, float* tws, float* gx, float* gparams, float* ydot,
+                              void* stream) {
+    return second_order_impl(cfg, ws, x, n, v, u, gy, tws, gx, gparams, ydot, nullptr, stream);
+}
+
+int32_t siren_second_order_kept(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
+                                const float* gy, float* kept, float* tws, float* gx, float* gparams, void* stream) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (!stored_ok(cfg) || wide(cfg)) return fail(SIREN_EUNSUPPORTED, "siren_second_order_kept covers hidden 256");
+    if (kept == nullptr) return fail(SIREN_EINVAL, "kept is NULL");
+    return second_order_impl(cfg, ws, x, n, v, nullptr, gy, tws, gx, gparams, nullptr, kept, stream);
+}
+
+int32_t siren_forward_grad_store(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y,
+                                 float* gx, float* tws, void* stream) {
+    if (int rc = siren_forward_store(cfg, ws, x, n, y, tws, stream)) return rc;
+    if (wide(cfg)) return fail(SIREN_EUNSUPPORTED, "siren_forward_grad_store covers hidden 256");
+    if (n == 0) return SIREN_OK;
+    if (gx == nullptr) return fail(SIREN_EINVAL, "gx is NULL");
+    const TrainPlan plan(cfg, n);
+    // dPhi/dx (gy = ones) by the reverse GEMMs from the stored cos; no delta tiles
+    siren::FusedArgs fa{w1_ws(cfg, ws), x, n, nullptr, nullptr, gx, cfg->d_in, cfg->d_out, cfg->n_hidden,
+                        cfg->omega_first, cfg->omega_hidden, 0, stored_cos(cfg, plan, tws), nullptr, plan.n_pad};
+    siren::launch_w1(siren::MODE_REV, tile_grid(cfg, plan.n_pad / siren::TILE, 1), (hipStream_t)stream, fa);
+    return hip_status("siren_forward_grad_store");
 }
 
 // ---- per-step kernels -------------------------------------------------------------------

@@ -129,6 +129,7 @@ struct W1Ctx {
     float* dbuf;  // STORE / REV: delta tiles, same layout
     float* cst;   // FWDS: this lane's cos store base (cos_off(tile, wave, LH, 0, 0, lane))
     const char* cbase;  // REV: wave-uniform cos base of (tile, wave) (SGPRs), + 16 * lane per lane
+    bool dstore;        // REV: store the delta tiles (false: gx only — the stored jet forward's dPhi/dx)
     bool more;    // persistent grid: this workgroup runs another coordinate tile after the current one, so the
                   // ring keeps streaming (slices 0..2 of the next tile are issued during the last 3 slices)
     int64_t lstride;
@@ -254,7 +255,7 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
             if (j < cx.o && !cx.seed_ones) ga += st.gyv[j] * ep.v[1 + j];
         if (cx.seed_ones) ga = ep.v[5];
         st.act[b] = (ga * cs) * cx.wsd;
-        store_block(cx.dbuf + LH * cx.lstride, b, st.act[b]);
+        if (cx.dstore) store_block(cx.dbuf + LH * cx.lstride, b, st.act[b]);
     } else if constexpr (KIND == EPI_SEED) {
         const f32x4 z = st.acc[(G + 1) & 1][b] + ep.v[0];
         f32x4 sn, cs;
@@ -284,7 +285,10 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
             st.act[b] = (st.acc[(G + 1) & 1][b] * st.cq[((G - LH) * NB + b) % 3]) * cx.w;
         else
             st.act[b] = (st.acc[(G + 1) & 1][b] * from_agpr(st.C[L][b])) * cx.w;
-        if constexpr (STORE || REV) store_block(cx.dbuf + L * cx.lstride, b, st.act[b]);
+        if constexpr (STORE) store_block(cx.dbuf + L * cx.lstride, b, st.act[b]);
+        if constexpr (REV) {
+            if (cx.dstore) store_block(cx.dbuf + L * cx.lstride, b, st.act[b]);
+        }
     }
 }
 
@@ -450,6 +454,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
         cx.inv_s0 = two_pi / w0;
     }
     cx.seed_ones = gy == nullptr;
+    cx.dstore = dbuf != nullptr;
     cx.abuf = cx.dbuf = nullptr;
     cx.more = false;
     cx.prof = nullptr;
@@ -623,7 +628,10 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
 #pragma unroll
                 for (int rb = 0; rb < NB; ++rb) st.act[rb] = (st.acc[GL][rb] * st.C[0][rb]) * cx.w0;
             }
-            if constexpr (STORE || REV) store_tile(cx.dbuf, st.act);
+            if constexpr (STORE) store_tile(cx.dbuf, st.act);
+            if constexpr (REV) {
+                if (cx.dstore) store_tile(cx.dbuf, st.act);
+            }
 #pragma unroll
             for (int k = 0; k < MAXD; ++k) {
                 if (k < d) {

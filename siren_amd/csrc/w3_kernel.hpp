@@ -24,6 +24,9 @@
 // (c_l, zd_l, a_l) of every layer go to a per-wave spill area in HBM in the forward sweep and come back in the
 // reverse sweep (coalesced 1 KiB per block; a WG's 768 KiB usually still sits in the 256 MiB Infinity Cache).
 // Same weight stream (packed forward + transposed slices) and 3-slot LDS ring as the W1 kernels.
+// KEPT (sdf training after a stored jet forward, siren_forward_grad_store): a_l (wgrad tile layout, kA) and
+// cos(w z_l) (lane-major, kC) of every layer come from the forward's workspace, so the hidden layers run the
+// tangent GEMMs only (half the forward MFMAs), only zdot is spilled, and kA doubles as the THETA A buffer.
 #pragma once
 #include "ring.hpp"
 #include "siren_common.h"
@@ -65,12 +68,50 @@ __device__ __forceinline__ void layer_mma2(const float* __restrict__ stream, flo
     }
 }
 
+// tangent-only layer GEMM (KEPT): acc = W-slices x B, 16 slices
+__device__ __forceinline__ void layer_mma1(const float* __restrict__ stream, float* ring, int& s, int nslices,
+                                           int wave, int lane, const f32x4 (&bt)[NB], f32x4 (&acct)[NB]) {
+#pragma unroll
+    for (int ob = 0; ob < NB; ++ob) acct[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) {
+        ring_wait(s, nslices);
+        ring_issue(stream, ring, s + 2, nslices, wave, lane);
+        const float* sl = ring + (s % NBUF) * SLICE + lane * 4;
+        f32x4 a0 = *(const f32x4*)(sl), a1 = *(const f32x4*)(sl + 256);
+#pragma unroll
+        for (int ob = 0; ob < NB; ob += 2) {
+            f32x4 n0, n1;
+            if (ob + 2 < NB) {
+                n0 = *(const f32x4*)(sl + (ob + 2) * 256);
+                n1 = *(const f32x4*)(sl + (ob + 3) * 256);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                acct[ob] = mfma4(a0[r], bt[kb][r], acct[ob]);
+                acct[ob + 1] = mfma4(a1[r], bt[kb][r], acct[ob + 1]);
+            }
+            if (ob + 2 < NB) {
+                a0 = n0;
+                a1 = n1;
+            }
+        }
+        ++s;
+    }
+}
+
 // spill slot of (layer l, quantity q in {c, zd, a}, block b) for this lane: 1 KiB per block, lane-contiguous
 __device__ __forceinline__ f32x4* spill_at(float* wave_spill, int l, int q, int b, int lane) {
     return (f32x4*)(wave_spill + ((int64_t)(l * 3 + q) * NB + b) * 256 + lane * 4);
 }
 
-template <int LH, bool THETA>
+// KEPT inputs of (layer l, block rb) for this lane: a_l from the wgrad tile layout (4 strided dwords), cos lane-major
+__device__ __forceinline__ f32x4 kept_a(const float* kA, int64_t lstride, int64_t toff, int l, int rb) {
+    const float* p = kA + l * lstride + toff + rb * 256;
+    return f32x4{p[0], p[16], p[32], p[48]};
+}
+
+template <int LH, bool THETA, bool KEPT = false>
 __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict__ ws, const float* __restrict__ x,
                                                         const float* __restrict__ v, const float* __restrict__ gy,
                                                         const float* __restrict__ u, float* __restrict__ ydot, int o,
@@ -78,7 +119,8 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
                                                         float* __restrict__ spill, float* __restrict__ A,
                                                         float* __restrict__ At, float* __restrict__ D,
                                                         float* __restrict__ Dt, int64_t n_pad, int d, float w0,
-                                                        float w) {
+                                                        float w, const float* __restrict__ kA,
+                                                        const float* __restrict__ kC) {
     __shared__ __attribute__((aligned(16))) float lds[NBUF * SLICE + SMALL_MAX];
     float* ring = lds;
     float* sm = lds + NBUF * SLICE;
@@ -90,6 +132,9 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
     float* wsp = spill + tile * (int64_t)(LH + 1) * 3 * NB * 256;
     const int64_t lstride = n_pad * H;
     const int64_t toff = tile * (H * 16) + 4 * g * 16 + c;
+    auto kept_c = [&](int l, int rb) -> f32x4 {
+        return *(const f32x4*)(kC + cos_off(blockIdx.x, wave, LH, l, rb, lane));
+    };
 
     {
         const int nf4 = (small_floats(LH) + 3) / 4;
@@ -134,11 +179,13 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
         }
         actp[rb] = sn;
         actt[rb] = (w0 * cs) * zd;
-        *spill_at(wsp, 0, 0, rb, lane) = cs;
         *spill_at(wsp, 0, 1, rb, lane) = zd;
-        *spill_at(wsp, 0, 2, rb, lane) = sn;
+        if (!KEPT) {
+            *spill_at(wsp, 0, 0, rb, lane) = cs;
+            *spill_at(wsp, 0, 2, rb, lane) = sn;
+        }
         if (THETA) {
-            store_block(A + toff, rb, actp[rb]);
+            if (!KEPT) store_block(A + toff, rb, actp[rb]);
             store_block(At + toff, rb, actt[rb]);
         }
     }
@@ -147,6 +194,18 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
     int s = 0;
 #pragma unroll 1
     for (int l = 1; l <= LH; ++l) {
+        if constexpr (KEPT) {
+            // primal from the stored forward: tangent GEMM only, zdot_l = W_l adot_{l-1}, adot_l = w cos_l zdot_l
+            layer_mma1(stream, ring, s, nslices, wave, lane, actt, acct);
+#pragma unroll
+            for (int rb = 0; rb < NB; ++rb) {
+                const f32x4 zd = acct[rb];
+                actt[rb] = (w * kept_c(l, rb)) * zd;
+                *spill_at(wsp, l, 1, rb, lane) = zd;
+                if (THETA) store_block(At + l * lstride + toff, rb, actt[rb]);
+            }
+            continue;
+        }
         layer_mma2(stream, ring, s, nslices, wave, lane, actp, actt, accp, acct);
         const float* bl = sm + SM_BIAS + l * H + 4 * g;
 #pragma unroll
@@ -204,9 +263,9 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
             abseed = abseed + gyv[j] * wj;
             if (u != nullptr) adb = adb + uv[j] * wj;
         }
-        const f32x4 cs = *spill_at(wsp, LH, 0, rb, lane);
+        const f32x4 cs = KEPT ? kept_c(LH, rb) : *spill_at(wsp, LH, 0, rb, lane);
         const f32x4 zd = *spill_at(wsp, LH, 1, rb, lane);
-        const f32x4 sn = *spill_at(wsp, LH, 2, rb, lane);
+        const f32x4 sn = KEPT ? kept_a(kA, lstride, toff, LH, rb) : *spill_at(wsp, LH, 2, rb, lane);
         actt[rb] = (w * cs) * adb;
         actp[rb] = (w * cs) * abseed - (w * w) * sn * zd * adb;
         if (THETA) {
@@ -220,9 +279,9 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
         const float wl = (l == 1) ? w0 : w;
 #pragma unroll
         for (int rb = 0; rb < NB; ++rb) {
-            const f32x4 cs = *spill_at(wsp, l - 1, 0, rb, lane);
+            const f32x4 cs = KEPT ? kept_c(l - 1, rb) : *spill_at(wsp, l - 1, 0, rb, lane);
             const f32x4 zd = *spill_at(wsp, l - 1, 1, rb, lane);
-            const f32x4 sn = *spill_at(wsp, l - 1, 2, rb, lane);
+            const f32x4 sn = KEPT ? kept_a(kA, lstride, toff, l - 1, rb) : *spill_at(wsp, l - 1, 2, rb, lane);
             const f32x4 wc = wl * cs;
             actt[rb] = wc * acct[rb];
             actp[rb] = wc * accp[rb] - (wl * wl) * sn * zd * acct[rb];

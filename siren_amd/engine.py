@@ -266,6 +266,21 @@ class SirenEngine:
                                                 _stream(x.device)), 'siren_forward_store')
         return y, tws
 
+    def forward_grad_store(self, ws, x):
+        """Stored jet forward (hidden 256): (y, J = dPhi/dx, tws) with a_l / cos kept in tws for second_order(kept=)."""
+        self._require()
+        x = self._check_x(x)
+        n = x.shape[0]
+        cnt = ctypes.c_int64()
+        _lib.check(self.lib.siren_train_stored_ws_floats(ctypes.byref(self.cfg), n, ctypes.byref(cnt)),
+                   'siren_train_stored_ws_floats')
+        tws = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
+        y = torch.empty(n, self.cfg.d_out, dtype=torch.float32, device=x.device)
+        gx = torch.empty(n, self.cfg.d_in, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_forward_grad_store(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(y), _ptr(gx),
+                                                     _ptr(tws), _stream(x.device)), 'siren_forward_grad_store')
+        return y, gx, tws
+
     def backward_stored(self, ws, x, gy, tws):
         """W2 backward from forward_store's workspace: reverse sweep only + wgrad. Returns (gx, gparams)."""
         self._require()
@@ -278,7 +293,7 @@ class SirenEngine:
                                                   _ptr(gx), _ptr(gp), _stream(x.device)), 'siren_backward_stored')
         return gx, gp
 
-    def second_order(self, ws, x, v, want_theta=True, gy=None, u=None, want_ydot=False):
+    def second_order(self, ws, x, v, want_theta=True, gy=None, u=None, want_ydot=False, kept=None):
         """W3: the backward of the vjp node gx = J^T u (u (n, d_out), None = ones, i.e. diff_operators.gradient's
         dPhi/dx) given its cotangent v (n, d_in): H v and d/dtheta of F = sum <v, J^T u> (+ sum gy . y with a
         first-order seed gy (n, d_out)) in ONE sweep (siren_second_order_ex). Returns (gx, gparams or None), plus
@@ -304,6 +319,12 @@ class SirenEngine:
         gx = torch.empty(n, self.cfg.d_in, dtype=torch.float32, device=x.device)
         gp = torch.empty(self.param_count, dtype=torch.float32, device=x.device) if want_theta else None
         ydot = torch.empty(n, o, dtype=torch.float32, device=x.device) if want_ydot else None
+        if kept is not None and u is None and not want_ydot:
+            # stored forward (forward_grad_store / forward_store): tangent-only hidden GEMMs
+            _lib.check(self.lib.siren_second_order_kept(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(v), _ptr(gy),
+                                                        _ptr(kept), _ptr(tws), _ptr(gx), _ptr(gp), _stream(x.device)),
+                       'siren_second_order_kept')
+            return gx, gp
         _lib.check(self.lib.siren_second_order_ex(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(v), _ptr(u),
                                                   _ptr(gy), _ptr(tws), _ptr(gx), _ptr(gp), _ptr(ydot),
                                                   _stream(x.device)), 'siren_second_order_ex')

@@ -180,7 +180,7 @@ def _fused_apply(engine, jet, coords, weights_biases):
         x2d = coords.view(coords.shape)
     if (jet is not None and jet.active and engine.cfg.d_out == 1 and engine.grad_supported
             and torch.is_grad_enabled() and x2d.requires_grad):
-        y, _ = SirenJetFunction.apply(engine, x2d, flat)  # J stays alive as the node's second output
+        y, _ = SirenJetFunction.apply(engine, x2d, flat, flat.requires_grad)  # J: the node's second output
     else:
         # a graph that will want parameter gradients: the forward keeps a_l / cos for a reverse-only backward
         y = SirenFunction.apply(engine, jet, x2d, flat, torch.is_grad_enabled() and flat.requires_grad)

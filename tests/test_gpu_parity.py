@@ -490,3 +490,30 @@ def test_training_uses_stored_forward(cuda, g1, monkeypatch):
     for k, p in m.named_parameters():
         ref = g1['G1_image_mse_grad_' + k]
         assert np.max(np.abs(p.grad.cpu().numpy() - ref)) <= 1e-4 * max(np.max(np.abs(ref)), 1e-30) + 1e-12, k
+
+
+@pytest.mark.parametrize('n,d,L', [(1, 3, 3), (4097, 3, 3), (1000, 2, 2), (333, 1, 1)])
+def test_kept_w3_matches_recompute(cuda, n, d, L):
+    """Stored jet forward (y, J from forward_grad_store) + seeded W3 from the kept a_l / cos == the recompute
+    kernels (forward_grad + siren_second_order_seeded), and the fp64 reference."""
+    layers = random_layers(d, L, 1, seed=11 * n + d)
+    eng = engine(d, L, 1)
+    ws = eng.pack(to_dev(O.flatten(layers), cuda))
+    rng = np.random.default_rng(n + 3)
+    x = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    v = rng.normal(size=(n, d)).astype(np.float32)
+    gy = rng.normal(size=(n, 1)).astype(np.float32)
+    X, V, GY = to_dev(x, cuda), to_dev(v, cuda), to_dev(gy, cuda)
+    y_k, J_k, kept = eng.forward_grad_store(ws, X)
+    y_r, J_r = eng.forward_grad(ws, X)
+    assert float((y_k - y_r).abs().max()) <= 1e-6  # W0 vs W1 body: different y summation order
+    assert float((J_k - J_r).abs().max()) <= 1e-6 * max(1., float(J_r.abs().max()))
+    for theta in (False, True):
+        gx_k, gp_k = eng.second_order(ws, X, V, want_theta=theta, gy=GY, kept=kept)
+        gx_r, gp_r = eng.second_order(ws, X, V, want_theta=theta, gy=GY)
+        assert float((gx_k - gx_r).abs().max()) <= 1e-5 * max(1., float(gx_r.abs().max()))
+        if theta:
+            assert float((gp_k - gp_r).abs().max()) <= 1e-5 * float(gp_r.abs().max())
+    rgx, rgp = torch_seeded_ref(x, layers, v, gy)
+    assert np.max(np.abs(gx_k.cpu().numpy() - rgx)) <= tol_rel(rgx)
+    assert np.max(np.abs(gp_k.cpu().numpy() - rgp)) <= 1e-4 * np.max(np.abs(rgp))

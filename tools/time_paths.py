@@ -69,6 +69,22 @@ def main():
         for name, fn, work in (('W3 H v (x only)', lambda: eng.second_order(ws, x, v, want_theta=False), 4 * F),
                                ('W3 H v + theta-grad', lambda: eng.second_order(ws, x, v, want_theta=True), 6 * F)):
             report(name, timed(fn), work, a.n)
+        if eng.stored_supported and a.o == 1:
+            # sdf step kernels: jet forward (y, J) + seeded W3 with theta-grads, recompute vs stored forward
+            gy1 = torch.randn(a.n, 1, device='cuda')
+            st = {}
+
+            def fwd_keep():
+                st['y'], st['J'], st['k'] = eng.forward_grad_store(ws, x)
+            fwd_keep()
+            t_fk = timed(fwd_keep)
+            t_bk = timed(lambda: eng.second_order(ws, x, v, want_theta=True, gy=gy1, kept=st['k']))
+            t_fr = timed(lambda: eng.forward_grad(ws, x))
+            t_br = timed(lambda: eng.second_order(ws, x, v, want_theta=True, gy=gy1))
+            report('sdf kernels, stored: fwd_grad_store', t_fk, 2 * F, a.n)
+            report('sdf kernels, stored: W3 kept + theta', t_bk, 6 * F, a.n)
+            report('sdf kernels, stored: total (8F)', t_fk + t_bk, 8 * F, a.n)
+            report('sdf kernels, recompute: total (8F)', t_fr + t_br, 8 * F, a.n)
 
 
 def report(name, ms, work, n):
