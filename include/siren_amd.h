@@ -234,6 +234,14 @@ int32_t siren_forward_grad_store(const siren_cfg* cfg, const float* ws, const fl
 int32_t siren_second_order_kept(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
                                 const float* gy, float* kept, float* tws, float* gx, float* gparams, void* stream);
 
+/* Split W4 / W4s (laplace_mse training): siren_forward_laplace's outputs (y / gx / lap, y and gx nullable) from the
+ * forward jet sweep that also keeps the a-jets and z-jets in tws (siren_laplace_backward_ws_floats), then
+ * siren_laplace_backward's outputs from the seed + reverse sweep over those stores (no forward recompute). */
+int32_t siren_forward_laplace_store(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y,
+                                    float* gx, float* lap, float* tws, void* stream);
+int32_t siren_laplace_backward_stored(const siren_cfg* cfg, const float* ws, const float* x, int64_t n,
+                                      const float* glap, float* tws, float* gx, float* gparams, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -275,8 +275,12 @@ class SirenLaplace(torch.autograd.Function):
     differentiable backward (create_graph over it, a fourth derivative) recomputes with device torch ops."""
 
     @staticmethod
-    def forward(ctx, engine, ws, x, flat):
-        _, _, lap = engine.forward_laplace(ws, x)
+    def forward(ctx, engine, ws, x, flat, store=False):
+        ctx.tws = None
+        if store and STORED_FORWARD:  # training: keep the jet stores, the backward is reverse-only
+            lap, ctx.tws = engine.forward_laplace_store(ws, x)
+        else:
+            _, _, lap = engine.forward_laplace(ws, x)
         ctx.engine, ctx.ws = engine, ws
         ctx.save_for_backward(x, flat)
         return lap
@@ -288,13 +292,16 @@ class SirenLaplace(torch.autograd.Function):
         need_x = ctx.needs_input_grad[2] and _will_execute(ctx, 1)
         need_p = ctx.needs_input_grad[3] and _will_execute(ctx, 2)
         if not (need_x or need_p):
-            return None, None, None, None
+            return None, None, None, None, None
         if not torch.is_grad_enabled():
-            gx, gp = ctx.engine.laplace_backward(ctx.ws, x, glap)
-            return None, None, (gx if need_x else None), (gp if need_p else None)
+            if ctx.tws is not None:
+                gx, gp = ctx.engine.laplace_backward_stored(ctx.ws, x, glap, ctx.tws)
+            else:
+                gx, gp = ctx.engine.laplace_backward(ctx.ws, x, glap)
+            return None, None, (gx if need_x else None), (gp if need_p else None), None
         gx, gp = _torch_path.laplace_vjp(ctx.engine.cfg, x, flat, glap.contiguous(),
                                          create_graph=torch.is_grad_enabled())
-        return None, None, (gx if need_x else None), (gp if need_p else None)
+        return None, None, (gx if need_x else None), (gp if need_p else None), None
 
 
 _VIEW_NODES = ('ViewBackward0', 'ReshapeAliasBackward0', 'UnsafeViewBackward0')
@@ -334,5 +341,5 @@ def fused_laplace(y, x):
     if node is None or not node.engine.laplace_supported:
         return None
     xs, flat = node.saved_tensors[:2]
-    lap = SirenLaplace.apply(node.engine, node.ws, xs, flat)
+    lap = SirenLaplace.apply(node.engine, node.ws, xs, flat, torch.is_grad_enabled() and flat.requires_grad)
     return lap.view(*y.shape[:-1], 1)

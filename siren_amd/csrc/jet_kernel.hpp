@@ -16,6 +16,9 @@
 // jet_store_kernel: forward jet (stores a-jets to abuf and z-jets to a lane-major scratch), seed
 // u_L,second = (sum_j Wout_j) glap, then the reverse sweep storing zb-jets to dbuf; one layer body for all 2L
 // GEMM passes (runtime loop), 3-slot ring of 16 KiB slices (ring.hpp). Tiles are 16 columns = 4 coordinates.
+// Split (laplace_mse training, SirenLaplace with a stored forward): PHASE JET_FWD runs the forward passes only —
+// stores as above, plus the outputs y / grad / Laplacian from the last a-jet (the W4 forward's results) — and
+// PHASE JET_REV the seed + reverse passes only from the stored z-jets; JET_BOTH is the single-launch form.
 #include "ring.hpp"
 #include "siren_common.h"
 #include "siren_params.h"
@@ -48,16 +51,21 @@ struct LaneBlocks {  // lane-major scratch: block rb of this lane at p + rb * 25
     }
 };
 
+enum { JET_BOTH = 0, JET_FWD = 1, JET_REV = 2 };
+
+// JET_FWD: glap is unused and the outputs go to y (n, o) / gx (n, d) / lap (n) (each nullable)
+template <int PHASE>
 __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
     const float* __restrict__ ws, const float* __restrict__ x, int64_t n, const float* __restrict__ glap,
     float* __restrict__ gx, int d, int o, int lh, float w0, float w, float* __restrict__ spill,
-    float* __restrict__ abuf, float* __restrict__ dbuf, int64_t n_pad) {
+    float* __restrict__ abuf, float* __restrict__ dbuf, int64_t n_pad, float* __restrict__ y,
+    float* __restrict__ lap) {
     __shared__ __attribute__((aligned(16))) float lds[NBUF * SLICE + SMALL_MAX];
     float* ring = lds;
     float* sm = lds + NBUF * SLICE;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane >> 4, c = lane & 15, js = c & 3;
-    const int nslices = 2 * lh * NB;
+    const int nslices = (PHASE == JET_FWD ? 1 : 2) * lh * NB;  // JET_FWD never issues the reverse slices
     const float* stream = ws + small_pad(lh);
     {
         const int nf4 = (small_floats(lh) + 3) / 4;
@@ -79,14 +87,25 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
     const float kb0 = js == 0 ? 0.f : w0, kg0 = js == 3 ? w0 * w0 : 0.f;
     const float kb = js == 0 ? 0.f : w, kg = js == 3 ? w * w : 0.f;
     const float m12 = (js == 1 || js == 2) ? 1.f : 0.f;
-    const float gl = (valid && js == 3) ? glap[coord] : 0.f;
+    const float gl = (PHASE != JET_FWD && valid && js == 3) ? glap[coord] : 0.f;
     __syncthreads();
-    ring_issue(stream, ring, 0, nslices, wave, lane);
-    ring_issue(stream, ring, 1, nslices, wave, lane);
+    const int p0 = PHASE == JET_REV ? lh : 0, p1 = PHASE == JET_FWD ? lh : 2 * lh;
+    int s = p0 * NB;
+    ring_issue(stream, ring, s, nslices, wave, lane);
+    ring_issue(stream, ring, s + 1, nslices, wave, lane);
 
     // ---- first layer: z_0 jet (VALU, K = d_in) ---------------------------------------------------------------
     f32x4 act[NB], acc[NB];
-    {
+    if (PHASE == JET_REV) {
+        // seed from the stored z_L jet (the JET_FWD launch's scratch)
+        LaneBlocks zl{sp + (int64_t)lh * lstride};
+#pragma unroll
+        for (int rb = 0; rb < NB; ++rb) {
+            const f32x4 u = gl * *(const f32x4*)(sm + SM_SEED + 16 * rb + 4 * g);
+            act[rb] = jet_sin_adjoint(u, zl.next_load(), w, val, m12);
+        }
+        jstore_tile(dbuf + (int64_t)lh * lstride + toff, act);
+    } else {
         LaneBlocks zs{sp};
 #pragma unroll
         for (int rb = 0; rb < NB; ++rb) {
@@ -98,12 +117,11 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
             zs.next_store(z);
             act[rb] = jet_sin(z, w0, val, kb0, kg0);
         }
+        jstore_tile(abuf + toff, act);
     }
-    jstore_tile(abuf + toff, act);
 
-    int s = 0;
 #pragma unroll 1
-    for (int p = 0; p < 2 * lh; ++p) {
+    for (int p = p0; p < p1; ++p) {
 #pragma unroll
         for (int ob = 0; ob < NB; ++ob) acc[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -137,7 +155,32 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
                 act[rb] = jet_sin(z, w, val, kb, kg);
             }
             jstore_tile(abuf + (int64_t)l * lstride + toff, act);
-            if (l == lh) {
+            if (PHASE == JET_FWD && l == lh) {
+                // outputs per stream (the W4 forward's): y_j (value), sum_j dy_j/dx_k (tangent k), sum_j Lap y_j
+                float tot = 0.f;
+#pragma unroll
+                for (int j = 0; j < MAXO; ++j) {
+                    if (j < o) {
+                        float pj = 0.f;
+#pragma unroll
+                        for (int rb = 0; rb < NB; ++rb) {
+                            const f32x4 wj = *(const f32x4*)(sm + SM_WO + j * H + 16 * rb + 4 * g);
+                            pj += wj[0] * act[rb][0] + wj[1] * act[rb][1] + wj[2] * act[rb][2] + wj[3] * act[rb][3];
+                        }
+                        const float vj = sum_groups(pj) + val * sm[SM_BOUT + j];
+                        if (y != nullptr && valid && g == 0 && js == 0) y[coord * o + j] = vj;
+                        tot += vj;
+                    }
+                }
+                if (valid && g == 0) {
+                    if (js == 3) {
+                        if (lap != nullptr) lap[coord] = tot;
+                    } else if (js >= 1 && js <= d && gx != nullptr) {
+                        gx[coord * d + js - 1] = tot;
+                    }
+                }
+            }
+            if (PHASE == JET_BOTH && l == lh) {
                 // seed: u_L (cotangent of the a_L jet) = (sum_j Wout_j) glap on the second-order stream only,
                 // then zb_L = adjoint of the last sine layer
                 LaneBlocks zl{zp};
@@ -161,6 +204,7 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
         }
     }
 
+    if (PHASE == JET_FWD) return;
     // ---- gx = W0^T zb_0 (value stream) -----------------------------------------------------------------------
 #pragma unroll
     for (int k = 0; k < MAXD; ++k) {

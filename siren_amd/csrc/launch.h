@@ -38,6 +38,9 @@ void launch_w4(dim3 grid, hipStream_t st, const float* ws, const float* x, int64
 void launch_jet_store(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* glap,
                       float* gx, int d, int o, int lh, float w0, float w, float* spill, float* abuf, float* dbuf,
                       int64_t n_pad);
+void launch_jet_phase(int phase, dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n,
+                      const float* glap, float* gx, int d, int o, int lh, float w0, float w, float* spill, float* abuf,
+                      float* dbuf, int64_t n_pad, float* y, float* lap);
 void launch_small_jet(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x,
                       const float* glap, int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d,
                       int o, int lh);

@@ -449,6 +449,56 @@ int32_t siren_laplace_backward(const siren_cfg* cfg, const float* ws, const floa
     return hip_status("siren_laplace_backward (reduce)");
 }
 
+// ---- split W4 / W4s for laplace_mse training: the forward jet keeps its stores, the backward is reverse-only ----
+int32_t siren_forward_laplace_store(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y,
+                                    float* gx, float* lap, float* tws, void* stream) {
+    if (int rc = check_jet(cfg)) return rc;
+    if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    if (n == 0) return SIREN_OK;
+    if (ws == nullptr || x == nullptr || lap == nullptr || tws == nullptr) return fail(SIREN_EINVAL, "ws/x/lap/tws is NULL");
+    const JetPlan plan(cfg, n);
+    float* abuf = tws;
+    float* dbuf = abuf + plan.buf_floats;
+    float* spill = dbuf + plan.buf_floats;
+    siren::launch_jet_phase(1, dim3((unsigned)(plan.n_pad / 16)), (hipStream_t)stream, ws, x, n, nullptr, gx,
+                            cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, spill, abuf,
+                            dbuf, plan.n_pad, y, lap);
+    return hip_status("siren_forward_laplace_store");
+}
+
+int32_t siren_laplace_backward_stored(const siren_cfg* cfg, const float* ws, const float* x, int64_t n,
+                                      const float* glap, float* tws, float* gx, float* gparams, void* stream) {
+    if (int rc = check_jet(cfg)) return rc;
+    if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    if (ws == nullptr || tws == nullptr || gx == nullptr || gparams == nullptr ||
+        (n > 0 && (x == nullptr || glap == nullptr)))
+        return fail(SIREN_EINVAL, "ws/x/glap/tws/gx/gparams is NULL");
+    const JetPlan plan(cfg, n);
+    const hipStream_t st = (hipStream_t)stream;
+    const int64_t P = param_count(cfg);
+    if (n == 0) {
+        (void)hipMemsetAsync(gparams, 0, P * sizeof(float), st);
+        return hip_status("siren_laplace_backward_stored");
+    }
+    float* abuf = tws;
+    float* dbuf = abuf + plan.buf_floats;
+    float* spill = dbuf + plan.buf_floats;
+    float* partial = spill + plan.buf_floats;
+    siren::launch_jet_phase(2, dim3((unsigned)(plan.n_pad / 16)), st, ws, x, n, glap, gx, cfg->d_in, cfg->d_out,
+                            cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, spill, abuf, dbuf, plan.n_pad, nullptr,
+                            nullptr);
+    if (int rc = hip_status("siren_laplace_backward_stored (jet reverse)")) return rc;
+    siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden), st, abuf, dbuf, plan.cols, plan.tps,
+                        partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1, siren::H, 1);
+    if (int rc = hip_status("siren_laplace_backward_stored (wgrad)")) return rc;
+    siren::launch_small_jet(dim3((unsigned)plan.splits), st, abuf, dbuf, x, glap, n, plan.n_pad, plan.tps, partial,
+                            P, cfg->d_in, cfg->d_out, cfg->n_hidden);
+    if (int rc = hip_status("siren_laplace_backward_stored (small)")) return rc;
+    const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 4096);
+    siren::launch_reduce(dim3((unsigned)rblocks), st, partial, plan.splits, P, gparams, 0, 0, 0);
+    return hip_status("siren_laplace_backward_stored (reduce)");
+}
+
 // ---- W3: second-order adjoint (Hessian-vector product + mixed theta gradient), d_out == 1 ---------------
 namespace {
 struct W3Plan {

@@ -7,8 +7,20 @@ namespace siren {
 void launch_jet_store(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* glap,
                       float* gx, int d, int o, int lh, float w0, float w, float* spill, float* abuf, float* dbuf,
                       int64_t n_pad) {
-    hipLaunchKernelGGL(jet_store_kernel, grid, dim3(THREADS), 0, st, ws, x, n, glap, gx, d, o, lh, w0, w, spill, abuf,
-                       dbuf, n_pad);
+    hipLaunchKernelGGL(jet_store_kernel<JET_BOTH>, grid, dim3(THREADS), 0, st, ws, x, n, glap, gx, d, o, lh, w0, w,
+                       spill, abuf, dbuf, n_pad, (float*)nullptr, (float*)nullptr);
+}
+
+// split form: phase 1 = forward jet with stores and outputs (y / gx / lap), phase 2 = seed + reverse from the stores
+void launch_jet_phase(int phase, dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n,
+                      const float* glap, float* gx, int d, int o, int lh, float w0, float w, float* spill, float* abuf,
+                      float* dbuf, int64_t n_pad, float* y, float* lap) {
+    if (phase == JET_FWD)
+        hipLaunchKernelGGL(jet_store_kernel<JET_FWD>, grid, dim3(THREADS), 0, st, ws, x, n, glap, gx, d, o, lh, w0, w,
+                           spill, abuf, dbuf, n_pad, y, lap);
+    else
+        hipLaunchKernelGGL(jet_store_kernel<JET_REV>, grid, dim3(THREADS), 0, st, ws, x, n, glap, gx, d, o, lh, w0, w,
+                           spill, abuf, dbuf, n_pad, y, lap);
 }
 
 

@@ -160,6 +160,35 @@ class SirenEngine:
                    'siren_laplace_backward')
         return gx, gp
 
+    def forward_laplace_store(self, ws, x):
+        """Split W4 (laplace_mse training forward): the Laplacian (n, 1) + the jet stores, kept in a workspace for
+        laplace_backward_stored. Returns (lap, tws)."""
+        self._require()
+        x = self._check_x(x)
+        n = x.shape[0]
+        cnt = ctypes.c_int64()
+        _lib.check(self.lib.siren_laplace_backward_ws_floats(ctypes.byref(self.cfg), n, ctypes.byref(cnt)),
+                   'siren_laplace_backward_ws_floats')
+        tws = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
+        lap = torch.empty(n, 1, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_forward_laplace_store(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, None, None,
+                                                        _ptr(lap), _ptr(tws), _stream(x.device)),
+                   'siren_forward_laplace_store')
+        return lap, tws
+
+    def laplace_backward_stored(self, ws, x, glap, tws):
+        """Split W4s: (gx, gparams) from forward_laplace_store's workspace (reverse-only jet sweep)."""
+        self._require()
+        x = self._check_x(x)
+        n = x.shape[0]
+        glap = glap.reshape(-1).contiguous()
+        gx = torch.empty(n, self.cfg.d_in, dtype=torch.float32, device=x.device)
+        gp = torch.empty(self.param_count, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_laplace_backward_stored(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(glap),
+                                                          _ptr(tws), _ptr(gx), _ptr(gp), _stream(x.device)),
+                   'siren_laplace_backward_stored')
+        return gx, gp
+
     # ------------------------------------------------------------------------------------------------------
     def backward_params(self, ws, x, gy):
         """W2 backward: (gx, gparams) for one coordinate batch, gparams flat in parameter order.

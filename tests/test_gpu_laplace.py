@@ -111,8 +111,10 @@ def test_diff_operators_laplace_takes_the_fused_path(cuda, g2, monkeypatch):
     m = SingleBVPNet(verbose=False).to(cuda)
     m.load_state_dict({k[2:]: torch.tensor(v) for k, v in g2.items() if k.startswith('w_')})
     calls = []
-    real = SirenEngine.forward_laplace
+    real, real_s = SirenEngine.forward_laplace, SirenEngine.forward_laplace_store  # (training: the split form)
     monkeypatch.setattr(SirenEngine, 'forward_laplace', lambda self, *a, **k: calls.append(1) or real(self, *a, **k))
+    monkeypatch.setattr(SirenEngine, 'forward_laplace_store',
+                        lambda self, *a, **k: calls.append(2) or real_s(self, *a, **k))
     coords = (torch.rand(1, 3000, 2, generator=torch.Generator().manual_seed(3)) * 2 - 1).to(cuda)
     out = m({'coords': coords})
     lap = D.laplace(out['model_out'], out['model_in'])
@@ -178,3 +180,26 @@ def test_laplace_mse_step_runs_on_hip_kernels(cuda, g1, monkeypatch):
     for k, p in m.named_parameters():
         ref = g1['G1_laplace_mse_grad_' + k]
         assert np.max(np.abs(p.grad.cpu().numpy() - ref)) <= 1e-4 * np.max(np.abs(ref)) + 1e-12, k
+
+
+@pytest.mark.parametrize('n,d,L', [(1, 2, 3), (4097, 2, 3), (1000, 1, 2), (333, 2, 5)])
+def test_split_laplace_forward_backward_matches(cuda, n, d, L):
+    """Split W4 / W4s (forward jet keeps its stores, reverse-only backward) == the single-launch kernels."""
+    from siren_amd.engine import SirenEngine
+    rng = np.random.default_rng(n + L)
+    dims = [d] + [256] * (L + 1) + [1]
+    layers = []
+    for i, (fi, fo) in enumerate(zip(dims[:-1], dims[1:])):
+        bound = 1. / fi if i == 0 else np.sqrt(6. / fi) / 30.
+        layers.append((rng.uniform(-bound, bound, (fo, fi)).astype(np.float32),
+                       (rng.uniform(-1, 1, fo) / np.sqrt(fi)).astype(np.float32)))
+    eng = SirenEngine(d, 256, L, 1)
+    ws = eng.pack(torch.tensor(O.flatten(layers), device=cuda))
+    x = torch.tensor(rng.uniform(-1, 1, (n, d)).astype(np.float32), device=cuda)
+    glap = torch.tensor(rng.normal(size=(n, 1)).astype(np.float32), device=cuda)
+    lap_s, tws = eng.forward_laplace_store(ws, x)
+    _, _, lap_r = eng.forward_laplace(ws, x)
+    assert float((lap_s - lap_r).abs().max()) <= 1e-5 * max(1., float(lap_r.abs().max()))
+    gx_s, gp_s = eng.laplace_backward_stored(ws, x, glap, tws)
+    gx_r, gp_r = eng.laplace_backward(ws, x, glap)
+    assert torch.equal(gx_s, gx_r) and torch.equal(gp_s, gp_r)

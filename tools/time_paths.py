@@ -64,6 +64,17 @@ def main():
         # W4 algorithmic unit: (1 + 2d) F; the jet kernel executes 4F (4 MFMA columns/coord)
         report('W4 y+grad+Laplacian (jet, 1 launch)', timed(lambda: eng.forward_laplace(ws, x, True, True)),
                (1 + 2 * d) * F, a.n)
+        # laplace_mse training kernels (W4s unit 3 (1 + 2d) F): W4 + W4s recompute vs the split pair
+        gl = torch.randn(a.n, 1, device='cuda')
+        t_r = timed(lambda: eng.forward_laplace(ws, x)) + timed(lambda: eng.laplace_backward(ws, x, gl))
+        jst = {}
+
+        def lfs():
+            jst['lap'], jst['tws'] = eng.forward_laplace_store(ws, x)
+        lfs()
+        t_s = timed(lfs) + timed(lambda: eng.laplace_backward_stored(ws, x, gl, jst['tws']))
+        report('W4s train kernels, recompute (W4 + W4s)', t_r, 3 * (1 + 2 * d) * F, a.n)
+        report('W4s train kernels, split (store + reverse)', t_s, 3 * (1 + 2 * d) * F, a.n)
     if eng.second_order_supported:
         v = torch.randn(a.n, a.d, device='cuda')
         for name, fn, work in (('W3 H v (x only)', lambda: eng.second_order(ws, x, v, want_theta=False), 4 * F),
