@@ -71,6 +71,14 @@ class FusedAdam:
         self._bind_grads()
 
     @torch.no_grad()
+    def allreduce_grad(self, world):
+        """Data parallel: average the flat gradient bucket over ranks with ONE all-reduce (RCCL over xGMI)."""
+        import torch.distributed as dist
+        self._gather_grads()
+        dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)
+        self.grad.div_(world)
+
+    @torch.no_grad()
     def step(self):
         self._gather_grads()
         self.step_count += 1

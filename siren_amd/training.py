@@ -90,7 +90,10 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
             if not use_lbfgs:
                 optim.zero_grad()
                 train_loss.backward()
-                distributed.allreduce_gradients(list(model.parameters()), world)
+                if fused_adam and world > 1:
+                    optim.allreduce_grad(world)  # the bucket itself is the all-reduce buffer: no gather / scatter
+                else:
+                    distributed.allreduce_gradients(list(model.parameters()), world)
                 if clip_grad and not fused_adam:
                     max_norm = 1. if isinstance(clip_grad, bool) else clip_grad
                     torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
