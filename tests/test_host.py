@@ -150,3 +150,37 @@ def test_hypernetwork_predicts_reference_weights(g7):
     assert list(params.keys()) == ['net.net.%d.0.%s' % (i, k) for i in range(5) for k in ('weight', 'bias')]
     for k, v in params.items():
         assert np.array_equal(v.numpy(), g7['p_' + k]), k
+
+
+def test_new_entry_points_validate_before_any_device_work(lib):
+    """Argument validation of the split / batched / per-step entry points happens on the host (no HIP call):
+    NULL buffers, negative sizes and unsupported networks come back as status codes with siren_last_error text."""
+    from siren_amd import _lib
+    P = ctypes.c_void_p
+    cfg = _lib.SirenCfg(2, 256, 3, 1, 30., 30., 1, 0)
+    cnt = ctypes.c_int64()
+    assert lib.siren_train_stored_ws_floats(ctypes.byref(cfg), 1000, ctypes.byref(cnt)) == 0 and cnt.value > 0
+    lin0 = _lib.SirenCfg(2, 256, 3, 1, 30., 30., 0, 0)  # notebook Siren with a final sine: no stored split
+    assert lib.siren_train_stored_ws_floats(ctypes.byref(lin0), 10, ctypes.byref(cnt)) == _lib.SIREN_EUNSUPPORTED
+    assert lib.siren_last_error()
+    assert lib.siren_forward_store(ctypes.byref(cfg), None, None, 0, None, None, None) == 0
+    assert lib.siren_forward_store(ctypes.byref(cfg), None, None, 5, None, None, None) == _lib.SIREN_EINVAL
+    assert lib.siren_backward_stored(ctypes.byref(cfg), None, None, 5, None, None, None, None, None) == \
+        _lib.SIREN_EINVAL
+    assert lib.siren_forward_laplace_store(ctypes.byref(cfg), None, None, -1, None, None, None, None, None) == \
+        _lib.SIREN_EINVAL
+    assert lib.siren_second_order_kept(ctypes.byref(cfg), None, None, 5, None, None, None, None, None, None,
+                                       None) == _lib.SIREN_EINVAL
+    assert lib.siren_forward_batched(ctypes.byref(cfg), None, None, 10, 70000, None, None) == _lib.SIREN_EINVAL
+    assert lib.siren_forward_batched(ctypes.byref(cfg), None, None, 10, 0, None, None) == 0
+    assert lib.siren_pack_batched(ctypes.byref(cfg), None, 3, None, None) == _lib.SIREN_EINVAL
+    assert lib.siren_sample_sdf(None, None, 0, 10, 0, 0, None, None, None, None) == _lib.SIREN_EINVAL
+    assert lib.siren_sample_sdf(None, None, 5, 0, 0, 0, None, None, None, None) == 0
+    assert lib.siren_adam_step(None, None, None, None, 10, 1e-3, .9, .999, 1e-8, 0, 0., None, None) == \
+        _lib.SIREN_EINVAL  # step must be >= 1
+    assert lib.siren_adam_step(P(4), P(16), P(16), P(16), 10, 1e-3, .9, .999, 1e-8, 1, 0., None, None) == \
+        _lib.SIREN_EINVAL  # 16-byte alignment
+    assert lib.siren_adam_scratch_floats(ctypes.byref(cnt)) == 0 and cnt.value > 1024
+    wide = _lib.SirenCfg(3, 512, 3, 3, 30., 30., 1, 0)
+    assert lib.siren_second_order_ex(ctypes.byref(wide), None, None, 1, None, None, None, None, None, None, None,
+                                     None) == _lib.SIREN_EUNSUPPORTED
