@@ -206,8 +206,10 @@ int32_t siren_forward_batched(const siren_cfg* cfg, const float* ws, const float
  * persistent grid is split across the elements); gy (B, n, d_out) nullable = ones. */
 int32_t siren_forward_grad_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
                                    const float* gy, float* y, float* gx, void* stream);
-/* W2 per element (the hypernetwork needs each element's theta-gradient): siren_backward on the stream, element by
- * element, sharing tws (siren_train_ws_floats(cfg, n)). gx nullable. */
+/* W2 per element (the hypernetwork needs each element's theta-gradient). Hidden 256 with elements below two CU
+ * rounds of tiles: ONE grouped launch per stage (fused store, wgrad, edge layers, slab reduction; grid over the
+ * elements); otherwise siren_backward element by element. tws: siren_train_batched_ws_floats(cfg, n, batch). */
+int32_t siren_train_batched_ws_floats(const siren_cfg* cfg, int64_t n, int64_t batch, int64_t* count);
 int32_t siren_backward_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
                                const float* gy, float* tws, float* gx, float* gparams, void* stream);
 

@@ -54,6 +54,7 @@ _SIGS = {
     'siren_second_order_kept': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P],
     'siren_forward_laplace_store': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P],
     'siren_laplace_backward_stored': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P],
+    'siren_train_batched_ws_floats': [_CFG, _I64, _I64, ctypes.POINTER(_I64)],
     'siren_pack_batched': [_CFG, _P, _I64, _P, _P],
     'siren_forward_batched': [_CFG, _P, _P, _I64, _I64, _P, _P],
     'siren_forward_grad_batched': [_CFG, _P, _P, _I64, _I64, _P, _P, _P, _P],

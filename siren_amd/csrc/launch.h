@@ -55,12 +55,15 @@ void launch_small_w3(dim3 grid, hipStream_t st, const float* At, const float* D,
                      const float* x, const float* v, const float* gy, const float* u, int64_t n, int64_t n_pad, int64_t tps,
                      float* partial, int64_t P, int d, int o, int lh);
 // tu_train.hip
+// bstride_act / bstride_part: grouped W2 over batched weights (grid.z of wgrad, grid.y of small / reduce = element)
 void launch_wgrad(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, int64_t n_pad, int64_t tps,
-                  float* partial, int64_t P, int d, int o, int lh, int with_bias, int h, int jet_bias = 0);
+                  float* partial, int64_t P, int d, int o, int lh, int with_bias, int h, int jet_bias = 0,
+                  int64_t bstride_act = 0, int64_t bstride_part = 0);
 void launch_small(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* gy,
-                  int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d, int o, int lh, int h);
+                  int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d, int o, int lh, int h,
+                  int64_t bstride_act = 0, int64_t bstride_part = 0);
 void launch_reduce(dim3 grid, hipStream_t st, const float* partial, int64_t S, int64_t P, float* gp, int64_t S2,
-                   int64_t lo, int64_t hi);
+                   int64_t lo, int64_t hi, int64_t bstride_part = 0);
 
 constexpr int STEP_BLOCKS = 1024;  // partial sums of the clip-norm pass (4 workgroups per CU)
 // tu_step.hip: device point-cloud sampling (dataio.py:420-442), clip_grad_norm_ + Adam over the flat bucket

@@ -108,10 +108,12 @@ int64_t wgrad_splits(const siren_cfg* cfg) {
 // of the wide kernel (layers 0..L-1).
 struct TrainPlan {
     int64_t n_pad, tiles, splits, tps, act_floats, partial_floats, spill_floats, total;
-    TrainPlan(const siren_cfg* cfg, int64_t n) {
+    // batch > 1: a grouped W2 over that many elements shares the CU rounds (fewer splits per element, so the
+    // per-split slabs stay a small fraction of the traffic)
+    TrainPlan(const siren_cfg* cfg, int64_t n, int64_t batch = 1) {
         n_pad = (n + siren::TILE - 1) / siren::TILE * siren::TILE;
         tiles = n_pad / 16;
-        const int64_t want = wgrad_splits(cfg);
+        const int64_t want = std::max<int64_t>(1, wgrad_splits(cfg) / std::max<int64_t>(1, batch));
         splits = tiles < want ? tiles : want;
         if (splits < 1) splits = 1;
         tps = (tiles + splits - 1) / splits;
@@ -719,14 +721,57 @@ int32_t siren_forward_grad_batched(const siren_cfg* cfg, const float* ws, const 
     return hip_status("siren_forward_grad_batched");
 }
 
+// grouped W2 (hidden 256, elements below ~2 CU rounds of tiles): ONE STORE launch (grid.y = element), one wgrad
+// launch (grid.z = element), one edge launch and one reduction over all elements; workspace per element =
+// siren_train_ws_floats(cfg, n) (siren_train_batched_ws_floats)
+bool grouped_w2(const siren_cfg* cfg, int64_t n) {
+    return grouped_ok(cfg) && cfg->n_hidden <= siren::MAX_LH_GRAD && (n + siren::TILE - 1) / siren::TILE < 2 * cu_count();
+}
+
+int32_t siren_train_batched_ws_floats(const siren_cfg* cfg, int64_t n, int64_t batch, int64_t* count) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (count == nullptr || n < 0 || batch < 0) return fail(SIREN_EINVAL, "count is NULL or n / batch < 0");
+    const bool grouped = grouped_w2(cfg, n);
+    const TrainPlan plan(cfg, n, grouped ? batch : 1);
+    *count = grouped ? batch * plan.total : plan.total;
+    return SIREN_OK;
+}
+
 int32_t siren_backward_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
                                const float* gy, float* tws, float* gx, float* gparams, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
-    if (n < 0 || batch < 0) return fail(SIREN_EINVAL, "need n >= 0 and batch >= 0");
-    if (batch > 0 && (ws == nullptr || gy == nullptr || gparams == nullptr || (n > 0 && x == nullptr)))
-        return fail(SIREN_EINVAL, "ws/x/gy/gparams is NULL");
+    if (n < 0 || batch < 0 || batch > 65535) return fail(SIREN_EINVAL, "need n >= 0 and 0 <= batch <= 65535");
+    if (batch > 0 && (ws == nullptr || gy == nullptr || gparams == nullptr || tws == nullptr || gx == nullptr ||
+                      (n > 0 && x == nullptr)))
+        return fail(SIREN_EINVAL, "ws/x/gy/tws/gx/gparams is NULL");
     const int64_t W = ws_floats(cfg), P = param_count(cfg);
     const int d = cfg->d_in, o = cfg->d_out;
+    if (batch > 0 && n > 0 && grouped_w2(cfg, n)) {
+        const TrainPlan plan(cfg, n, batch);
+        const hipStream_t st = (hipStream_t)stream;
+        // [a tiles of every element][delta tiles of every element][partial slabs of every element]: element b's
+        // tiles at + b * act_floats (the STORE kernel's grid.y offset), its slabs at + b * partial_floats
+        const int64_t bact = plan.act_floats, bpart = plan.partial_floats;
+        float* abuf = tws;
+        float* dbuf = tws + batch * bact;
+        float* partial = tws + 2 * batch * bact;
+        siren::FusedArgs fa{w1_ws(cfg, ws), x, n, gy, nullptr, gx, d, o, cfg->n_hidden, cfg->omega_first,
+                            cfg->omega_hidden, 0, abuf, dbuf, plan.n_pad, W};
+        const int64_t tiles = plan.n_pad / siren::TILE;
+        const int64_t per = std::max<int64_t>(1, ((int64_t)cu_count() + batch - 1) / batch);
+        siren::launch_w1(siren::MODE_STORE, dim3((unsigned)std::min(tiles, per), (unsigned)batch), st, fa);
+        if (int rc = hip_status("siren_backward_batched (grouped store)")) return rc;
+        siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden, (unsigned)batch), st, abuf, dbuf,
+                            plan.n_pad, plan.tps, partial, P, d, o, cfg->n_hidden, 1, cfg->hidden, 0, bact, bpart);
+        if (int rc = hip_status("siren_backward_batched (grouped wgrad)")) return rc;
+        siren::launch_small(dim3((unsigned)plan.splits, (unsigned)batch), st, abuf, dbuf, x, gy, n, plan.n_pad,
+                            plan.tps, partial, P, d, o, cfg->n_hidden, cfg->hidden, bact, bpart);
+        if (int rc = hip_status("siren_backward_batched (grouped small)")) return rc;
+        const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 1024);
+        siren::launch_reduce(dim3((unsigned)rblocks, (unsigned)batch), st, partial, plan.splits, P, gparams, 0, 0, 0,
+                             bpart);
+        return hip_status("siren_backward_batched (grouped reduce)");
+    }
     for (int64_t b = 0; b < batch; ++b)
         if (int rc = siren_backward(cfg, ws + b * W, x + b * n * d, n, gy + b * n * o, tws, nullptr,
                                     gx ? gx + b * n * d : nullptr, gparams + b * P, stream))

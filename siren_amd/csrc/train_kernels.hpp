@@ -39,11 +39,17 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
                                                           const float* __restrict__ dbuf, int64_t n_pad,
                                                           int64_t tps, float* __restrict__ partial, int64_t P,
                                                           int d, int o, int lh, int with_bias, int h,
-                                                          int jet_bias = 0) {
+                                                          int jet_bias = 0, int64_t bstride_act = 0,
+                                                          int64_t bstride_part = 0) {
     __shared__ __attribute__((aligned(16))) float ring[WG_NBUF * WG_SLOT];
     const ParamOffsets off(d, o, lh, h);
     const int s = blockIdx.x, l = blockIdx.y + 1;
-    const int qn = h / 256, qr = blockIdx.z / qn, qc = blockIdx.z % qn;
+    // grid.z = batch element x (h/256)^2 quadrants (grouped W2 over batched weights: per-element tiles / slabs)
+    const int qn = h / 256, qz = blockIdx.z % (qn * qn), bz = blockIdx.z / (qn * qn);
+    const int qr = qz / qn, qc = qz % qn;
+    abuf += bz * bstride_act;
+    dbuf += bz * bstride_act;
+    partial += bz * bstride_part;
     const int64_t tstride = (int64_t)h * 16;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane >> 4, i = lane & 15;
@@ -129,7 +135,8 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
                                                        const float* __restrict__ sgy, const float* __restrict__ su,
                                                        int64_t n, int64_t ntiles,
                                                        int64_t tps, float* __restrict__ partial, int64_t P, int d,
-                                                       int o, int lh, int h) {
+                                                       int o, int lh, int h, int64_t bstride_act = 0,
+                                                       int64_t bstride_part = 0) {
     // per-column scalars of one chunk: [col][0..3] = x (d_in <= 4), [col][4..7] = gy / v / glap, [col][8..11] = the
     // first-order seed gy (n, o) of a seeded W3 (sgy != nullptr: rows r3 = a_L add gy^T a_L to dWout, sum gy to
     // dbout), [col][12..15] = W3's output weighting u (n, o) (ones when su == nullptr)
@@ -141,6 +148,14 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
     const ParamOffsets off(d, o, lh, h);
     const int s = blockIdx.x;
     const int64_t t0 = (int64_t)s * tps, t1 = t0 + tps < ntiles ? t0 + tps : ntiles;
+    if (gridDim.y > 1) {  // grouped W2 (EDGE_W2 over batched weights): grid.y = batch element
+        const int64_t b = blockIdx.y;
+        r0 += b * bstride_act;
+        r1 += b * bstride_act;
+        x += b * n * d;
+        sc += b * n * o;
+        partial += b * bstride_part;
+    }
     const int64_t tstride = (int64_t)h * 16;
     const int ns = KIND == EDGE_W2 ? o : (KIND == EDGE_W3 ? d : 1);  // scalars per coordinate besides x
     float* out = partial + (int64_t)s * P;
@@ -245,7 +260,9 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
 // gp[i] = sum over the partial slabs; indices in [lo, hi) (the hidden layers' W/b) sum S + S2 slabs, the others
 // (first and output layer, written by the small kernels into the first S slabs only) sum S.
 __global__ void reduce_kernel(const float* __restrict__ partial, int64_t S, int64_t P, float* __restrict__ gp,
-                              int64_t S2 = 0, int64_t lo = 0, int64_t hi = 0) {
+                              int64_t S2 = 0, int64_t lo = 0, int64_t hi = 0, int64_t bstride_part = 0) {
+    partial += (int64_t)blockIdx.y * bstride_part;  // grouped: grid.y = batch element, gp rows of P
+    gp += (int64_t)blockIdx.y * P;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < P; idx += (int64_t)gridDim.x * blockDim.x) {
         float acc = 0.f;
         const int64_t ns = (idx >= lo && idx < hi) ? S + S2 : S;

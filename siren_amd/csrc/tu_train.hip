@@ -5,16 +5,18 @@
 namespace siren {
 
 void launch_wgrad(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, int64_t n_pad, int64_t tps,
-                  float* partial, int64_t P, int d, int o, int lh, int with_bias, int h, int jet_bias) {
+                  float* partial, int64_t P, int d, int o, int lh, int with_bias, int h, int jet_bias,
+                  int64_t bstride_act, int64_t bstride_part) {
     hipLaunchKernelGGL(wgrad_kernel, grid, dim3(THREADS), 0, st, abuf, dbuf, n_pad, tps, partial, P, d, o, lh,
-                       with_bias, h, jet_bias);
+                       with_bias, h, jet_bias, bstride_act, bstride_part);
 }
 
 void launch_small(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* gy,
-                  int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d, int o, int lh, int h) {
+                  int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d, int o, int lh, int h,
+                  int64_t bstride_act, int64_t bstride_part) {
     hipLaunchKernelGGL(edge_kernel<EDGE_W2>, grid, dim3(THREADS), 0, st, dbuf, abuf + (int64_t)lh * n_pad * h,
                        (const float*)nullptr, (const float*)nullptr, x, gy, (const float*)nullptr, (const float*)nullptr, n,
-                       n_pad / 16, tps, partial, P, d, o, lh, h);
+                       n_pad / 16, tps, partial, P, d, o, lh, h, bstride_act, bstride_part);
 }
 
 void launch_small_w3(dim3 grid, hipStream_t st, const float* At, const float* D, const float* Dt, const float* AL,
@@ -34,8 +36,8 @@ void launch_small_jet(dim3 grid, hipStream_t st, const float* abuf, const float*
 }
 
 void launch_reduce(dim3 grid, hipStream_t st, const float* partial, int64_t S, int64_t P, float* gp, int64_t S2,
-                   int64_t lo, int64_t hi) {
-    hipLaunchKernelGGL(reduce_kernel, grid, dim3(256), 0, st, partial, S, P, gp, S2, lo, hi);
+                   int64_t lo, int64_t hi, int64_t bstride_part) {
+    hipLaunchKernelGGL(reduce_kernel, grid, dim3(256), 0, st, partial, S, P, gp, S2, lo, hi, bstride_part);
 }
 
 }  // namespace siren

@@ -444,6 +444,10 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
         if (y != nullptr) y += b * n * o;
         if (gx != nullptr) gx += b * n * d;
         if (gy != nullptr) gy += b * n * o;
+        if constexpr ((MODE & MODE_BASE) == MODE_STORE) {  // grouped W2: per-element a / delta tiles
+            abuf += b * (LH + 1) * n_pad * H;
+            dbuf += b * (LH + 1) * n_pad * H;
+        }
     }
     {
         constexpr float two_pi = 6.28318530717958648f;

@@ -270,8 +270,8 @@ class SirenEngine:
         B, n = x.shape[:2]
         gy = gy.contiguous()
         cnt = ctypes.c_int64()
-        _lib.check(self.lib.siren_train_ws_floats(ctypes.byref(self.cfg), n, ctypes.byref(cnt)),
-                   'siren_train_ws_floats')
+        _lib.check(self.lib.siren_train_batched_ws_floats(ctypes.byref(self.cfg), n, B, ctypes.byref(cnt)),
+                   'siren_train_batched_ws_floats')
         tws = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
         gx = torch.empty_like(x)
         gp = torch.empty(B, self.param_count, dtype=torch.float32, device=x.device)

@@ -54,7 +54,9 @@ def test_grouped_launch_equals_per_element(cuda, B, n, d, L, o, H):
             y1, gx = eng.forward_grad(ws, x[b], gy[b])
             assert torch.equal(y1, y1b[b]) and torch.equal(gx, gxb[b])
             gx2, gp2 = eng.backward_params(ws, x[b], gy[b])
-            assert torch.equal(gp2, gpp[b]) and torch.equal(gx2, gxp[b])
+            # the grouped W2 uses fewer split-K slabs per element: same sums, different order
+            assert torch.equal(gx2, gxp[b])
+            assert float((gp2 - gpp[b]).abs().max()) <= 1e-5 * float(gp2.abs().max())
 
 
 def test_hypo_params_forward_gradient_and_theta_grads_vs_reference(cuda, g7):

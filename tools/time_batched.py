@@ -35,7 +35,10 @@ def main():
     x = torch.rand(a.B, a.n, 2, device='cuda') * 2 - 1
     wsb = eng.pack_batched(flat)
     F = 394752
+    gy = torch.randn(a.B, a.n, 1, device='cuda')
     for name, grouped, single, flop in (
+            ('W2 backward', lambda: eng.backward_params_batched(wsb, x, gy),
+             lambda b: eng.backward_params(wsb[b], x[b], gy[b]), 3 * F),  # store (fwd + rev) + wgrad
             ('W0 forward', lambda: eng.forward_batched(wsb, x), lambda b: eng.forward(wsb[b], x[b]), F),
             ('W1 fwd+grad', lambda: eng.forward_grad_batched(wsb, x), lambda b: eng.forward_grad(wsb[b], x[b]), 2 * F)):
         tg = timed(grouped)
