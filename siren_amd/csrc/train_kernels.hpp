@@ -264,10 +264,18 @@ __global__ void reduce_kernel(const float* __restrict__ partial, int64_t S, int6
     partial += (int64_t)blockIdx.y * bstride_part;  // grouped: grid.y = batch element, gp rows of P
     gp += (int64_t)blockIdx.y * P;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < P; idx += (int64_t)gridDim.x * blockDim.x) {
-        float acc = 0.f;
         const int64_t ns = (idx >= lo && idx < hi) ? S + S2 : S;
-        for (int64_t s = 0; s < ns; ++s) acc += partial[s * P + idx];
-        gp[idx] = acc;
+        // 8 independent partial sums keep 8 slab loads in flight per thread (one dependent chain was
+        // latency-bound); the combine order is fixed, so the result stays deterministic
+        float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        const float* col = partial + idx;
+        int64_t s = 0;
+        for (; s + 8 <= ns; s += 8) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) a[q] += col[(s + q) * P];
+        }
+        for (; s < ns; ++s) a[0] += col[s * P];
+        gp[idx] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     }
 }
 
