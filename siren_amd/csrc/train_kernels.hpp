@@ -185,7 +185,7 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
             }
             __syncthreads();
             if (t < h) {
-#pragma unroll 2
+#pragma unroll(KIND == EDGE_JET ? 8 : 2)
                 for (int i = 0; i < nt; ++i) {
                     const int64_t tile = c0 + i;
                     const f32x4* a = (const f32x4*)(r0 + tile * tstride + t * 16);
