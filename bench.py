@@ -127,6 +127,16 @@ def train_step_rate(device, n=1 << 18, steps=5):
     return n * steps / (time.perf_counter() - t0) / 1e6
 
 
+def reference_laplace(y, x):
+    """diff_operators.laplace as the reference writes it (diff_operators.py:27-43), restated: gradient with
+    create_graph, then divergence = one create_graph autograd.grad per input dimension."""
+    grad = torch.autograd.grad(y, [x], grad_outputs=torch.ones_like(y), create_graph=True)[0]
+    div = 0.
+    for i in range(grad.shape[-1]):
+        div += torch.autograd.grad(grad[..., i], x, torch.ones_like(grad[..., i]), create_graph=True)[0][..., i:i + 1]
+    return div
+
+
 def config_rates(device, steps=5):
     """Secondary per-config rates (BASELINE.json configs[2..4]), one GPU, drop-in API end to end (model ->
     loss_functions -> backward -> Adam), inputs resident on the device. Mcoords/s per GPU."""
@@ -233,6 +243,14 @@ def config_rates(device, steps=5):
     n = grid.shape[1]
     lap_gt = torch.sin(4 * grid[..., :1])
     res['poisson_512sq_laplace_mse_train_mcoords_s'] = rate(m, grid, lambda o: LF.laplace_mse(o, {'laplace': lap_gt}), n)
+    # the same loss through the reference's own op sequence (diff_operators.py:27-43: gradient, then one create_graph
+    # autograd.grad per input dimension) instead of siren_amd's fused laplace(): d Hessian-vector-product nodes
+    # whose backward is the third-order mixed-jet kernel (siren_hvp_backward)
+    torch.manual_seed(0)
+    m = SingleBVPNet(verbose=False).to(device)
+    res['poisson_512sq_reference_recipe_laplace_mse_train_mcoords_s'] = rate(
+        m, grid, lambda o: {'laplace_loss': ((reference_laplace(o['model_out'], o['model_in']) - lap_gt) ** 2).mean()},
+        n)
     eng = SirenEngine(2, 256, 3, 1)
     ws = eng.pack(seed0_params(device))
     x2 = grid[0].contiguous()

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define SIREN_ABI_VERSION 1
+#define SIREN_ABI_VERSION 2
 
 enum {
     SIREN_OK = 0,
@@ -89,10 +89,11 @@ int32_t siren_forward(const siren_cfg* cfg, const float* ws, const float* x, int
 /* W1 (forward + coordinate vector-Jacobian product) in ONE launch:
  *   y  = Phi(x)                       (skipped when y == NULL)
  *   gx = sum_j gy_j * dPhi_j/dx       (gy == NULL means gy = ones: diff_operators.gradient, d.o.py:39-43)
- * hidden 256: n_hidden must be 1..3 (cos(w z_l) of every layer stays in registers); hidden 512: 1..8 (cos is
- * spilled to a stream-ordered scratch allocation, hipMallocAsync/hipFreeAsync on `stream`). */
+ * hidden 256: n_hidden must be 1..3 (cos(w z_l) of every layer stays in registers; tws may be NULL); hidden 512:
+ * 1..8 (cos is spilled to the caller's workspace tws, siren_forward_grad_ws_floats(cfg, n) floats). */
+int32_t siren_forward_grad_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count);
 int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x, int64_t n,
-                           const float* gy, float* y, float* gx, void* stream);
+                           const float* gy, float* y, float* gx, float* tws, void* stream);
 
 /* W4 (the fused Laplacian) in ONE launch, forward-mode Taylor jet:
  *   y   (n, d_out)  = Phi(x)                       (skipped when y == NULL)
@@ -165,6 +166,22 @@ int32_t siren_second_order_ex(const siren_cfg* cfg, const float* ws, const float
                               const float* u, const float* gy, float* tws, float* gx, float* gparams, float* ydot,
                               void* stream);
 
+/* Third-order adjoint: the backward of the Hessian-vector-product node h = sum_j u_j H_j(x) v (the node that
+ * diff_operators.divergence(gradient(y, x), x) records per input dimension, diff_operators.py:27-36, and that the
+ * second jacobian() of helmholtz_pml / wave_pml records, loss_functions.py:112-211). With g (n, d_in) the cotangent
+ * of h, S = sum_c <g_c, h_c> = sum_c sum_j u_cj D2 Phi_j(x_c)[v_c, g_c]:
+ *   gx (n, d_in)          = dS/dx
+ *   gparams (param_count) = dS/dtheta                       (skipped when NULL)
+ *   gv (n, d_in)          = dS/dv = sum_j u_j H_j g           (skipped when NULL)
+ *   gu (n, d_out)         = dS/du_j = g^T H_j v              (skipped when NULL)
+ * v (n, d_in), u (n, d_out) (NULL = ones). One forward-mode jet along (v, g) + its reverse (4 coordinates x 4 streams
+ * per MFMA tile), then the split-K MFMA weight-gradient over 4n columns and a deterministic slab reduction. Hidden
+ * 256, linear output, 1..5 hidden layers, d_in / d_out <= 4. tws: siren_hvp_backward_ws_floats(cfg, n) floats. */
+int32_t siren_hvp_backward_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count);
+int32_t siren_hvp_backward(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
+                           const float* u, const float* g, float* tws, float* gx, float* gparams, float* gv,
+                           float* gu, void* stream);
+
 /* Diagnostics: the W1 kernel (hidden 256, 3 hidden layers) with s_memtime stamps. stamps receives
  * 256 workgroups x 4 tiles x 4 waves x 8 events (uint64; event 0 tile start, 1..6 after GEMM 0..5, 7 tile end);
  * unrecorded entries are left untouched. y / gx as siren_forward_grad with gy = ones. */
@@ -203,9 +220,10 @@ int32_t siren_pack_batched(const siren_cfg* cfg, const float* params, int64_t ba
 int32_t siren_forward_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
                               float* y, void* stream);
 /* W1 (y, J^T gy) for every element in ONE grouped launch (hidden 256, linear output, 1..3 hidden layers; the
- * persistent grid is split across the elements); gy (B, n, d_out) nullable = ones. */
+ * persistent grid is split across the elements); gy (B, n, d_out) nullable = ones. tws: the per-element workspace of
+ * siren_forward_grad (siren_forward_grad_ws_floats(cfg, n); reused element after element, NULL at hidden 256). */
 int32_t siren_forward_grad_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
-                                   const float* gy, float* y, float* gx, void* stream);
+                                   const float* gy, float* y, float* gx, float* tws, void* stream);
 /* W2 per element (the hypernetwork needs each element's theta-gradient). Hidden 256 with elements below two CU
  * rounds of tiles: ONE grouped launch per stage (fused store, wgrad, edge layers, slab reduction; grid over the
  * elements); otherwise siren_backward element by element. tws: siren_train_batched_ws_floats(cfg, n, batch). */

@@ -177,21 +177,35 @@ class SirenJetFunction(torch.autograd.Function):
 
 class SirenHVP(torch.autograd.Function):
     """d/dx <v, J(x)^T u> = sum_j u_j H_j(x) v as a graph node (u (n, d_out), None = ones: H v for d_out == 1):
-    forward = W3 kernel (x part only, siren_second_order_ex); its own backward (a third derivative: laplace_mse
-    through an unfused divergence, helmholtz_pml / wave_pml training) is recomputed with device torch ops."""
+    forward = W3 kernel (x part only, siren_second_order_ex). Its backward is a third derivative — laplace_mse through
+    the reference's divergence(gradient()) (diff_operators.py:27-36, one such node per input dimension) and the
+    helmholtz_pml / wave_pml training backward (loss_functions.py:112-211) — and runs on the mixed-jet kernel
+    (siren_hvp_backward: d/d(x, theta, v, u) of <g, h> in one forward+reverse jet sweep + MFMA wgrad). Only a
+    differentiable backward (create_graph over it, a fourth derivative) recomputes with device torch ops."""
 
     @staticmethod
     def forward(ctx, engine, ws, x, flat, v, u=None):
         gx, _ = engine.second_order(ws, x, v.contiguous(), want_theta=False, u=u)
-        ctx.engine = engine
+        ctx.engine, ctx.ws = engine, ws
         ctx.save_for_backward(x, flat, v, u)
         return gx
 
     @staticmethod
     def backward(ctx, g):
         x, flat, v, u = ctx.saved_tensors
-        rx, rp, rv, ru = _torch_path.hvp_vjp(ctx.engine.cfg, x, flat, v, g, create_graph=torch.is_grad_enabled(),
-                                             u=u)
+        eng = ctx.engine
+        if eng.hvp_backward_supported and not torch.is_grad_enabled():
+            # tensor inputs in order: ws (0), x (1), flat (2), v (3), u (4, when given)
+            need_x = ctx.needs_input_grad[2] and _will_execute(ctx, 1)
+            need_p = ctx.needs_input_grad[3] and _will_execute(ctx, 2)
+            need_v = ctx.needs_input_grad[4] and _will_execute(ctx, 3)
+            need_u = u is not None and ctx.needs_input_grad[5] and _will_execute(ctx, 4)
+            if not (need_x or need_p or need_v or need_u):
+                return None, None, None, None, None, None
+            gx, gp, gv, gu = eng.hvp_backward(ctx.ws, x, v, g.contiguous(), u, want_theta=need_p, want_v=need_v,
+                                              want_u=need_u)
+            return None, None, (gx if need_x else None), gp, gv, gu
+        rx, rp, rv, ru = _torch_path.hvp_vjp(eng.cfg, x, flat, v, g, create_graph=torch.is_grad_enabled(), u=u)
         return None, None, rx, rp, rv, ru
 
 

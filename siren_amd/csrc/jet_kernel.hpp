@@ -19,6 +19,16 @@
 // Split (laplace_mse training, SirenLaplace with a stored forward): PHASE JET_FWD runs the forward passes only —
 // stores as above, plus the outputs y / grad / Laplacian from the last a-jet (the W4 forward's results) — and
 // PHASE JET_REV the seed + reverse passes only from the stored z-jets; JET_BOTH is the single-launch form.
+//
+// MIX = true: the third-order adjoint (the backward of a Hessian-vector-product node h = sum_j u_j H_j(x) v, i.e.
+// SirenHVP: laplace_mse through the reference's unfused divergence(gradient()), diff_operators.py:27-36, and the
+// second jacobian() of helmholtz_pml / wave_pml, loss_functions.py:112-211). With g the cotangent of h,
+//   S = sum_c <g_c, h_c> = sum_c sum_j u_j D2 y_j(x_c)[v_c, g_c]
+// is the mixed second derivative of the network along two per-coordinate tangents, so the same 4-stream jet carries
+// it: stream 0 value, stream 1 along v, stream 2 along g, stream 3 the mixed second order (jet_sin<true>). Its
+// reverse gives every cotangent of the node at once:
+//   gx = W0^T zb_0,value   gv = W0^T zb_0,v   gu_j = D2 y_j[v, g] (the forward's last jet)   dtheta as for W4s
+// with the first layer's tangents W0 v / W0 g (per coordinate) and the output seed sum_j u_j Wout_j.
 #include "ring.hpp"
 #include "siren_common.h"
 #include "siren_params.h"
@@ -54,12 +64,16 @@ struct LaneBlocks {  // lane-major scratch: block rb of this lane at p + rb * 25
 enum { JET_BOTH = 0, JET_FWD = 1, JET_REV = 2 };
 
 // JET_FWD: glap is unused and the outputs go to y (n, o) / gx (n, d) / lap (n) (each nullable)
-template <int PHASE>
+// MIX: tv / tg (n, d) the tangents v / g, tu (n, o) the output weighting (NULL = ones); gv (n, d) and gu (n, o)
+// nullable outputs; glap unused (JET_BOTH only)
+template <int PHASE, bool MIX = false>
 __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
     const float* __restrict__ ws, const float* __restrict__ x, int64_t n, const float* __restrict__ glap,
     float* __restrict__ gx, int d, int o, int lh, float w0, float w, float* __restrict__ spill,
     float* __restrict__ abuf, float* __restrict__ dbuf, int64_t n_pad, float* __restrict__ y,
-    float* __restrict__ lap) {
+    float* __restrict__ lap, const float* __restrict__ tv, const float* __restrict__ tg,
+    const float* __restrict__ tu, float* __restrict__ gv, float* __restrict__ gu) {
+    static_assert(!MIX || PHASE == JET_BOTH, "the mixed jet runs as one launch");
     __shared__ __attribute__((aligned(16))) float lds[NBUF * SLICE + SMALL_MAX];
     float* ring = lds;
     float* sm = lds + NBUF * SLICE;
@@ -81,13 +95,21 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
 #pragma unroll
     for (int k = 0; k < MAXD; ++k) xv[k] = (valid && k < d) ? x[coord * d + k] : 0.f;
     const float val = js == 0 ? 1.f : 0.f;
-    float jcf[MAXD];
+    float jcf[MAXD];  // first-layer coefficients of W0[:, k] per stream
 #pragma unroll
-    for (int k = 0; k < MAXD; ++k) jcf[k] = val * xv[k] + (js == k + 1 ? 1.f : 0.f);
+    for (int k = 0; k < MAXD; ++k) {
+        if constexpr (MIX) {
+            const float* tp = js == 1 ? tv : tg;
+            jcf[k] = (valid && k < d && (js == 1 || js == 2)) ? tp[coord * d + k] : val * xv[k];
+        } else {
+            jcf[k] = val * xv[k] + (js == k + 1 ? 1.f : 0.f);
+        }
+    }
     const float kb0 = js == 0 ? 0.f : w0, kg0 = js == 3 ? w0 * w0 : 0.f;
     const float kb = js == 0 ? 0.f : w, kg = js == 3 ? w * w : 0.f;
     const float m12 = (js == 1 || js == 2) ? 1.f : 0.f;
-    const float gl = (PHASE != JET_FWD && valid && js == 3) ? glap[coord] : 0.f;
+    const float gl = (PHASE != JET_FWD && valid && js == 3) ? (MIX ? 1.f : glap[coord]) : 0.f;
+    const bool s1 = js == 1;
     __syncthreads();
     const int p0 = PHASE == JET_REV ? lh : 0, p1 = PHASE == JET_FWD ? lh : 2 * lh;
     int s = p0 * NB;
@@ -102,7 +124,7 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
 #pragma unroll
         for (int rb = 0; rb < NB; ++rb) {
             const f32x4 u = gl * *(const f32x4*)(sm + SM_SEED + 16 * rb + 4 * g);
-            act[rb] = jet_sin_adjoint(u, zl.next_load(), w, val, m12);
+            act[rb] = jet_sin_adjoint<MIX>(u, zl.next_load(), w, val, m12, s1);
         }
         jstore_tile(dbuf + (int64_t)lh * lstride + toff, act);
     } else {
@@ -115,7 +137,7 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
             for (int k = 0; k < MAXD; ++k)
                 if (k < d) z += jcf[k] * *(const f32x4*)(sm + SM_W0 + k * H + nb);
             zs.next_store(z);
-            act[rb] = jet_sin(z, w0, val, kb0, kg0);
+            act[rb] = jet_sin<MIX>(z, w0, val, kb0, kg0);
         }
         jstore_tile(abuf + toff, act);
     }
@@ -152,7 +174,7 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
             for (int rb = 0; rb < NB; ++rb) {
                 const f32x4 z = acc[rb] + val * *(const f32x4*)(bl + 16 * rb);
                 zs.next_store(z);
-                act[rb] = jet_sin(z, w, val, kb, kg);
+                act[rb] = jet_sin<MIX>(z, w, val, kb, kg);
             }
             jstore_tile(abuf + (int64_t)l * lstride + toff, act);
             if (PHASE == JET_FWD && l == lh) {
@@ -180,15 +202,42 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
                     }
                 }
             }
+            if (MIX && gu != nullptr && l == lh) {
+                // gu_j = D2 y_j[v, g] = Wout_j . a_L,second (stream 3 lanes; the bias only enters stream 0)
+#pragma unroll
+                for (int j = 0; j < MAXO; ++j) {
+                    if (j < o) {
+                        float pj = 0.f;
+#pragma unroll
+                        for (int rb = 0; rb < NB; ++rb) {
+                            const f32x4 wj = *(const f32x4*)(sm + SM_WO + j * H + 16 * rb + 4 * g);
+                            pj += wj[0] * act[rb][0] + wj[1] * act[rb][1] + wj[2] * act[rb][2] + wj[3] * act[rb][3];
+                        }
+                        pj = sum_groups(pj);
+                        if (valid && g == 0 && js == 3) gu[coord * o + j] = pj;
+                    }
+                }
+            }
             if (PHASE == JET_BOTH && l == lh) {
-                // seed: u_L (cotangent of the a_L jet) = (sum_j Wout_j) glap on the second-order stream only,
-                // then zb_L = adjoint of the last sine layer
+                // seed: u_L (cotangent of the a_L jet) = (sum_j Wout_j) glap on the second-order stream only
+                // (MIX: sum_j u_j Wout_j), then zb_L = adjoint of the last sine layer
                 LaneBlocks zl{zp};
+                float uw[MAXO];  // MIX: this coordinate's output weighting (the seed is sum_j u_j Wout_j)
+#pragma unroll
+                for (int j = 0; j < MAXO; ++j)
+                    uw[j] = (MIX && j < o) ? (tu != nullptr ? (valid ? tu[coord * o + j] : 0.f) : 1.f) : 0.f;
 #pragma unroll
                 for (int rb = 0; rb < NB; ++rb) {
-                    const f32x4 u = gl * *(const f32x4*)(sm + SM_SEED + 16 * rb + 4 * g);
-                    act[rb] = jet_sin_adjoint(u, zl.next_load(), w, val, m12);
+                    f32x4 sd;
+                    if constexpr (MIX) {  // WoT rows j >= o are zero padded: branch-free sum over all 4
+                        const float* wo = sm + SM_WO + 16 * rb + 4 * g;
+                        sd = uw[0] * *(const f32x4*)wo + uw[1] * *(const f32x4*)(wo + H) +
+                             uw[2] * *(const f32x4*)(wo + 2 * H) + uw[3] * *(const f32x4*)(wo + 3 * H);
+                    } else {
+                        sd = *(const f32x4*)(sm + SM_SEED + 16 * rb + 4 * g);
                     }
+                    act[rb] = jet_sin_adjoint<MIX>(gl * sd, zl.next_load(), w, val, m12, s1);
+                }
                 jstore_tile(dbuf + (int64_t)lh * lstride + toff, act);
             }
         } else {
@@ -198,14 +247,14 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
             const float wl = lm == 0 ? w0 : w;
 #pragma unroll
             for (int rb = 0; rb < NB; ++rb) {
-                act[rb] = jet_sin_adjoint(acc[rb], zl.next_load(), wl, val, m12);
+                act[rb] = jet_sin_adjoint<MIX>(acc[rb], zl.next_load(), wl, val, m12, s1);
             }
             jstore_tile(dbuf + (int64_t)lm * lstride + toff, act);
         }
     }
 
     if (PHASE == JET_FWD) return;
-    // ---- gx = W0^T zb_0 (value stream) -----------------------------------------------------------------------
+    // ---- gx = W0^T zb_0 (value stream); MIX: gv = W0^T zb_0 (stream 1, the cotangent of v) ----------------------
 #pragma unroll
     for (int k = 0; k < MAXD; ++k) {
         if (k < d) {
@@ -217,6 +266,7 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
             }
             q = sum_groups(q);
             if (valid && g == 0 && js == 0) gx[coord * d + k] = q;
+            if (MIX && gv != nullptr && valid && g == 0 && js == 1) gv[coord * d + k] = q;
         }
     }
 }

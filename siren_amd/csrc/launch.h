@@ -44,6 +44,13 @@ void launch_jet_phase(int phase, dim3 grid, hipStream_t st, const float* ws, con
 void launch_small_jet(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x,
                       const float* glap, int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d,
                       int o, int lh);
+// tu_jet.hip: the third-order adjoint (mixed jet along per-coordinate tangents v, g; output weighting u nullable)
+void launch_jet_mix(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* v,
+                    const float* g, const float* u, float* gx, float* gv, float* gu, int d, int o, int lh, float w0,
+                    float w, float* spill, float* abuf, float* dbuf, int64_t n_pad);
+void launch_small_mix(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* v,
+                      const float* g, const float* u, int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P,
+                      int d, int o, int lh);
 // tu_wide.hip: hidden width 512 (mode as siren_common.h MODE_*); spill = cos scratch for MODE_W1 / MODE_STORE
 void launch_wide(int mode, dim3 grid, hipStream_t st, const FusedArgs& a, float* spill);
 // tu_w3.hip (launch_small_w3 lives in tu_train.hip with the other edge-layer reductions)

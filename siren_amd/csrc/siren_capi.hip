@@ -116,8 +116,8 @@ struct TrainPlan {
         const int64_t want = std::max<int64_t>(1, wgrad_splits(cfg) / std::max<int64_t>(1, batch));
         splits = tiles < want ? tiles : want;
         if (splits < 1) splits = 1;
-        tps = (tiles + splits - 1) / splits;
-        splits = (tiles + tps - 1) / tps;
+        tps = std::max<int64_t>(1, (tiles + splits - 1) / splits);  // n == 0: no tiles, one empty split
+        splits = std::max<int64_t>(1, (tiles + tps - 1) / tps);
         if (splits < 1) splits = 1;
         act_floats = (int64_t)(cfg->n_hidden + 1) * n_pad * cfg->hidden;
         partial_floats = splits * param_count(cfg);
@@ -177,8 +177,18 @@ int32_t siren_forward(const siren_cfg* cfg, const float* ws, const float* x, int
     return hip_status("siren_forward");
 }
 
+// hidden 512: the cos(w z_l) scratch of layers 0..L-1 (lane-major, n padded to whole tiles); hidden 256 keeps cos in
+// registers and needs none
+int32_t siren_forward_grad_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
+    const int64_t n_pad = (n + siren::TILE - 1) / siren::TILE * siren::TILE;
+    *count = wide(cfg) ? (int64_t)cfg->n_hidden * n_pad * cfg->hidden : 0;
+    return SIREN_OK;
+}
+
 int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* gy,
-                           float* y, float* gx, void* stream) {
+                           float* y, float* gx, float* tws, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (cfg->n_hidden > siren::MAX_LH_GRAD && !wide(cfg))
         return fail(SIREN_EUNSUPPORTED, "siren_forward_grad needs 1 <= num_hidden_layers <= 3 at hidden 256");
@@ -192,15 +202,10 @@ int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x
     siren::FusedArgs fa{ws, x, n, gy, y, gx, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first,
                         cfg->omega_hidden, fs, nullptr, nullptr, 0};
     if (wide(cfg)) {
-        // cos scratch of layers 0..L-1 from the stream-ordered pool (this entry point has no workspace argument)
-        const int64_t n_pad = blocks * siren::TILE;
-        float* spill = nullptr;
-        const size_t bytes = (size_t)cfg->n_hidden * n_pad * cfg->hidden * sizeof(float);
-        if (hipMallocAsync((void**)&spill, bytes, (hipStream_t)stream) != hipSuccess)
-            return fail(SIREN_EHIP, "siren_forward_grad: hipMallocAsync of the hidden-512 cos scratch failed");
-        fa.n_pad = n_pad;  // per-layer scratch stride
-        siren::launch_wide(siren::MODE_W1, grid, (hipStream_t)stream, fa, spill);
-        (void)hipFreeAsync(spill, (hipStream_t)stream);
+        // cos scratch of layers 0..L-1 in the caller's workspace (siren_forward_grad_ws_floats)
+        if (tws == nullptr) return fail(SIREN_EINVAL, "siren_forward_grad at hidden 512 needs tws (siren_forward_grad_ws_floats)");
+        fa.n_pad = blocks * siren::TILE;  // per-layer scratch stride
+        siren::launch_wide(siren::MODE_W1, grid, (hipStream_t)stream, fa, tws);
     } else if ((cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) != 0 || fs || !w1_ok(cfg)) {
         siren::launch_legacy_grad(false, grid, (hipStream_t)stream, fa);
     } else {
@@ -402,8 +407,8 @@ struct JetPlan {
         const int64_t want = wgrad_splits(cfg);
         splits = tiles < want ? tiles : want;
         if (splits < 1) splits = 1;
-        tps = (tiles + splits - 1) / splits;
-        splits = (tiles + tps - 1) / tps;
+        tps = std::max<int64_t>(1, (tiles + splits - 1) / splits);  // n == 0: no tiles, one empty split
+        splits = std::max<int64_t>(1, (tiles + tps - 1) / tps);
         if (splits < 1) splits = 1;
         buf_floats = (int64_t)(cfg->n_hidden + 1) * cols * siren::H;
         partial_floats = splits * param_count(cfg);
@@ -499,6 +504,56 @@ int32_t siren_laplace_backward_stored(const siren_cfg* cfg, const float* ws, con
     const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 4096);
     siren::launch_reduce(dim3((unsigned)rblocks), st, partial, plan.splits, P, gparams, 0, 0, 0);
     return hip_status("siren_laplace_backward_stored (reduce)");
+}
+
+// ---- third-order adjoint: the backward of a Hessian-vector-product node (jet_kernel.hpp MIX) -----------------
+namespace {
+int check_mix(const siren_cfg* cfg) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (wide(cfg) || !cfg->outermost_linear || cfg->n_hidden > 5)
+        return fail(SIREN_EUNSUPPORTED, "siren_hvp_backward covers hidden 256, linear output, 1..5 hidden layers");
+    return SIREN_OK;
+}
+}  // namespace
+
+int32_t siren_hvp_backward_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count) {
+    if (int rc = check_mix(cfg)) return rc;
+    if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
+    *count = JetPlan(cfg, n).total;
+    return SIREN_OK;
+}
+
+int32_t siren_hvp_backward(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
+                           const float* u, const float* g, float* tws, float* gx, float* gparams, float* gv,
+                           float* gu, void* stream) {
+    if (int rc = check_mix(cfg)) return rc;
+    if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    const JetPlan plan(cfg, n);
+    const hipStream_t st = (hipStream_t)stream;
+    const int64_t P = param_count(cfg);
+    if (n == 0) {  // empty batch: zero parameter gradient, nothing else to write (buffers may be empty / NULL)
+        if (gparams != nullptr) (void)hipMemsetAsync(gparams, 0, P * sizeof(float), st);
+        return hip_status("siren_hvp_backward");
+    }
+    if (ws == nullptr || tws == nullptr || gx == nullptr || x == nullptr || v == nullptr || g == nullptr)
+        return fail(SIREN_EINVAL, "ws/x/v/g/tws/gx is NULL");
+    float* abuf = tws;
+    float* dbuf = abuf + plan.buf_floats;
+    float* spill = dbuf + plan.buf_floats;
+    float* partial = spill + plan.buf_floats;
+    siren::launch_jet_mix(dim3((unsigned)(plan.n_pad / 16)), st, ws, x, n, v, g, u, gx, gv, gu, cfg->d_in, cfg->d_out,
+                          cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, spill, abuf, dbuf, plan.n_pad);
+    if (int rc = hip_status("siren_hvp_backward (mixed jet)")) return rc;
+    if (gparams == nullptr) return SIREN_OK;
+    siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden), st, abuf, dbuf, plan.cols, plan.tps,
+                        partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1, siren::H, 1);
+    if (int rc = hip_status("siren_hvp_backward (wgrad)")) return rc;
+    siren::launch_small_mix(dim3((unsigned)plan.splits), st, abuf, dbuf, x, v, g, u, n, plan.n_pad, plan.tps, partial,
+                            P, cfg->d_in, cfg->d_out, cfg->n_hidden);
+    if (int rc = hip_status("siren_hvp_backward (small)")) return rc;
+    const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 4096);
+    siren::launch_reduce(dim3((unsigned)rblocks), st, partial, plan.splits, P, gparams, 0, 0, 0);
+    return hip_status("siren_hvp_backward (reduce)");
 }
 
 // ---- W3: second-order adjoint (Hessian-vector product + mixed theta gradient), d_out == 1 ---------------
@@ -696,7 +751,7 @@ int32_t siren_forward_batched(const siren_cfg* cfg, const float* ws, const float
 }
 
 int32_t siren_forward_grad_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
-                                   const float* gy, float* y, float* gx, void* stream) {
+                                   const float* gy, float* y, float* gx, float* tws, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (n < 0 || batch < 0 || batch > 65535) return fail(SIREN_EINVAL, "need n >= 0 and 0 <= batch <= 65535");
     if (n == 0 || batch == 0) return SIREN_OK;
@@ -707,7 +762,7 @@ int32_t siren_forward_grad_batched(const siren_cfg* cfg, const float* ws, const 
     if (!(grouped_ok(cfg) && cfg->n_hidden <= siren::MAX_LH_GRAD) || blocks >= 2 * cus) {
         for (int64_t b = 0; b < batch; ++b)
             if (int rc = siren_forward_grad(cfg, ws + b * W, x + b * n * d, n, gy ? gy + b * n * o : nullptr,
-                                            y ? y + b * n * o : nullptr, gx + b * n * d, stream))
+                                            y ? y + b * n * o : nullptr, gx + b * n * d, tws, stream))
                 return rc;
         return SIREN_OK;
     }

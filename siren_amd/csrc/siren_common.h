@@ -155,6 +155,9 @@ __device__ __forceinline__ float quad_bcast(float v) {  // value of quad lane SE
 // the jet of z (this lane's stream) -> the jet of sin(w z):
 //   a = sin(w z0), a_i = w cos(w z0) z_i, a_3 = w cos(w z0) z_3 - w^2 sin(w z0) (z_1^2 + z_2^2)
 // with per-lane coefficients ka = [s == 0], kb = w [s != 0], kg = w^2 [s == 3].
+// MIX: the mixed second-order jet of two independent tangents (stream 1 along v, stream 2 along g, stream 3 the
+// mixed second derivative D2[v, g]; the third-order adjoint of jet_kernel.hpp): a_3 = w cos z_3 - w^2 sin z_1 z_2.
+template <bool MIX = false>
 __device__ __forceinline__ f32x4 jet_sin(const f32x4& z, float w, float ka, float kb, float kg) {
     f32x4 out;
 #pragma unroll
@@ -162,7 +165,7 @@ __device__ __forceinline__ f32x4 jet_sin(const f32x4& z, float w, float ka, floa
         const float z0 = quad_bcast<0>(z[r]), t1 = quad_bcast<1>(z[r]), t2 = quad_bcast<2>(z[r]);
         float sn, cs;
         sincos_fast(w * z0, sn, cs);
-        const float q2 = __builtin_fmaf(t1, t1, t2 * t2);
+        const float q2 = MIX ? t1 * t2 : __builtin_fmaf(t1, t1, t2 * t2);
         out[r] = __builtin_fmaf(ka, sn, __builtin_fmaf(kb * cs, z[r], -(kg * sn) * q2));
     }
     return out;
@@ -188,7 +191,11 @@ __device__ __forceinline__ f32x4 jet_sin_rev(const f32x4& z, float ka, float kb,
 //   zb_3 = w c u_3
 //   zb_i = w c u_i - 2 w^2 s z_i u_3
 //   zb_0 = w c u_0 - w^2 s (u_1 z_1 + u_2 z_2) - u_3 (w^2 s z_3 + w^3 c (z_1^2 + z_2^2))
-__device__ __forceinline__ f32x4 jet_sin_adjoint(const f32x4& u, const f32x4& z, float w, float m0, float m12) {
+// MIX (a_3 = w c z_3 - w^2 s z_1 z_2): zb_1 = w c u_1 - w^2 s z_2 u_3, zb_2 = w c u_2 - w^2 s z_1 u_3 (s1 = [s == 1]
+// picks the other tangent), zb_0's last term u_3 (w^2 s z_3 + w^3 c z_1 z_2).
+template <bool MIX = false>
+__device__ __forceinline__ f32x4 jet_sin_adjoint(const f32x4& u, const f32x4& z, float w, float m0, float m12,
+                                                 bool s1 = false) {
     f32x4 out;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -198,9 +205,10 @@ __device__ __forceinline__ f32x4 jet_sin_adjoint(const f32x4& u, const f32x4& z,
         float sn, cs;
         sincos_fast(w * z0, sn, cs);
         const float wc = w * cs, w2s = w * w * sn;
-        const float t12 = (2.f * w2s) * (z[r] * u3);
+        const float t12 = MIX ? w2s * ((s1 ? z2 : z1) * u3) : (2.f * w2s) * (z[r] * u3);
+        const float q2 = MIX ? z1 * z2 : __builtin_fmaf(z1, z1, z2 * z2);
         const float t0 = __builtin_fmaf(w2s, __builtin_fmaf(u1, z1, u2 * z2),
-                                        u3 * __builtin_fmaf(w2s, z3, (w * w * wc) * __builtin_fmaf(z1, z1, z2 * z2)));
+                                        u3 * __builtin_fmaf(w2s, z3, (w * w * wc) * q2));
         out[r] = __builtin_fmaf(wc, u[r], -__builtin_fmaf(m12, t12, m0 * t0));
     }
     return out;

@@ -125,7 +125,10 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
 //             (+ with a first-order seed gy, rows a_L: dWout += gy^T a_L, dbout = sum gy)
 //   EDGE_JET: rows zb_0 jet, a_L jet (16 columns = 4 coordinates x 4 streams, scalars per coordinate):
 //             dW0[:, k] = sum zb_0,value x_k + zb_0,tangent k, db0 = sum zb_0,value, dWout = sum glap a_L,second
-enum { EDGE_W2 = 0, EDGE_W3 = 1, EDGE_JET = 2 };
+//   EDGE_MIX: the mixed jet (third-order adjoint, jet_kernel.hpp MIX): rows as EDGE_JET, scalars x, v (sc), g (sgy)
+//             (n, d) and u (su, (n, o), NULL = ones): dW0[:, k] = sum zb_0,value x_k + zb_0,v v_k + zb_0,g g_k,
+//             db0 = sum zb_0,value, dWout_j = sum u_j a_L,second, dbout = 0
+enum { EDGE_W2 = 0, EDGE_W3 = 1, EDGE_JET = 2, EDGE_MIX = 3 };
 constexpr int EDGE_CHUNK = 16;  // tiles per LDS staging chunk
 
 template <int KIND>
@@ -140,8 +143,9 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
     // per-column scalars of one chunk: [col][0..3] = x (d_in <= 4), [col][4..7] = gy / v / glap, [col][8..11] = the
     // first-order seed gy (n, o) of a seeded W3 (sgy != nullptr: rows r3 = a_L add gy^T a_L to dWout, sum gy to
     // dbout), [col][12..15] = W3's output weighting u (n, o) (ones when su == nullptr)
-    constexpr int CPT = KIND == EDGE_JET ? 4 : 16;  // coordinates per tile
-    constexpr int NSC = KIND == EDGE_W3 ? 16 : 9;
+    constexpr bool JETK = KIND == EDGE_JET || KIND == EDGE_MIX;
+    constexpr int CPT = JETK ? 4 : 16;  // coordinates per tile
+    constexpr int NSC = (KIND == EDGE_W3 || KIND == EDGE_MIX) ? 16 : 9;
     __shared__ __attribute__((aligned(16))) float scal[EDGE_CHUNK * CPT][NSC];
     const bool seeded = KIND == EDGE_W3 && sgy != nullptr;
     const bool weighted = KIND == EDGE_W3 && su != nullptr;
@@ -157,7 +161,7 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
         partial += b * bstride_part;
     }
     const int64_t tstride = (int64_t)h * 16;
-    const int ns = KIND == EDGE_W2 ? o : (KIND == EDGE_W3 ? d : 1);  // scalars per coordinate besides x
+    const int ns = KIND == EDGE_W2 ? o : ((KIND == EDGE_W3 || KIND == EDGE_MIX) ? d : 1);  // scalars besides x
     float* out = partial + (int64_t)s * P;
     for (int tb = 0; tb < h; tb += THREADS) {
         const int t = tb + threadIdx.x;
@@ -179,13 +183,19 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
                         scal[e][8 + j] = (ok && seeded && j < o) ? sgy[cd * o + j] : 0.f;
                         scal[e][12 + j] = weighted ? ((ok && j < o) ? su[cd * o + j] : 0.f) : 1.f;
                     }
+                } else if constexpr (KIND == EDGE_MIX) {
+#pragma unroll
+                    for (int k = 0; k < MAXD; ++k) scal[e][8 + k] = (ok && k < d) ? sgy[cd * d + k] : 0.f;
+#pragma unroll
+                    for (int j = 0; j < MAXO; ++j)
+                        scal[e][12 + j] = (ok && j < o) ? (su != nullptr ? su[cd * o + j] : 1.f) : 0.f;
                 } else {
                     scal[e][8] = 0.f;
                 }
             }
             __syncthreads();
             if (t < h) {
-#pragma unroll(KIND == EDGE_JET ? 8 : 2)
+#pragma unroll(JETK ? 8 : 2)
                 for (int i = 0; i < nt; ++i) {
                     const int64_t tile = c0 + i;
                     const f32x4* a = (const f32x4*)(r0 + tile * tstride + t * 16);
@@ -207,6 +217,14 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
                             gw0[0] += av[q][0] * sv[0] + av[q][1];
                             gw0[1] += av[q][0] * sv[1] + av[q][2];
                             gwo[0] += sv[4] * bv[q][3];
+                        } else if constexpr (KIND == EDGE_MIX) {
+                            const float* sv = scal[i * 4 + q];
+                            gb0 += av[q][0];
+#pragma unroll
+                            for (int k = 0; k < MAXD; ++k)
+                                gw0[k] += av[q][0] * sv[k] + av[q][1] * sv[4 + k] + av[q][2] * sv[8 + k];
+#pragma unroll
+                            for (int j = 0; j < MAXO; ++j) gwo[j] += sv[12 + j] * bv[q][3];
                         } else {
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
@@ -249,6 +267,11 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
                     if (j < o) out[off.wout + (int64_t)j * h + t] = gwo[j];
                     if (j < o && t == j) out[off.bout + t] = gbj[j];
                 }
+            } else if constexpr (KIND == EDGE_MIX) {
+#pragma unroll
+                for (int j = 0; j < MAXO; ++j)
+                    if (j < o) out[off.wout + (int64_t)j * h + t] = gwo[j];
+                if (t < o) out[off.bout + t] = 0.f;
             } else {
                 for (int j = 0; j < o; ++j) out[off.wout + (int64_t)j * h + t] = gwo[0];
                 if (t < o) out[off.bout + t] = 0.f;

@@ -4,11 +4,14 @@
 
 namespace siren {
 
+#define NOF ((const float*)nullptr)
+#define NUL ((float*)nullptr)
+
 void launch_jet_store(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* glap,
                       float* gx, int d, int o, int lh, float w0, float w, float* spill, float* abuf, float* dbuf,
                       int64_t n_pad) {
     hipLaunchKernelGGL(jet_store_kernel<JET_BOTH>, grid, dim3(THREADS), 0, st, ws, x, n, glap, gx, d, o, lh, w0, w,
-                       spill, abuf, dbuf, n_pad, (float*)nullptr, (float*)nullptr);
+                       spill, abuf, dbuf, n_pad, (float*)nullptr, (float*)nullptr, NOF, NOF, NOF, NUL, NUL);
 }
 
 // split form: phase 1 = forward jet with stores and outputs (y / gx / lap), phase 2 = seed + reverse from the stores
@@ -17,11 +20,18 @@ void launch_jet_phase(int phase, dim3 grid, hipStream_t st, const float* ws, con
                       float* dbuf, int64_t n_pad, float* y, float* lap) {
     if (phase == JET_FWD)
         hipLaunchKernelGGL(jet_store_kernel<JET_FWD>, grid, dim3(THREADS), 0, st, ws, x, n, glap, gx, d, o, lh, w0, w,
-                           spill, abuf, dbuf, n_pad, y, lap);
+                           spill, abuf, dbuf, n_pad, y, lap, NOF, NOF, NOF, NUL, NUL);
     else
         hipLaunchKernelGGL(jet_store_kernel<JET_REV>, grid, dim3(THREADS), 0, st, ws, x, n, glap, gx, d, o, lh, w0, w,
-                           spill, abuf, dbuf, n_pad, y, lap);
+                           spill, abuf, dbuf, n_pad, y, lap, NOF, NOF, NOF, NUL, NUL);
 }
 
+// third-order adjoint (backward of a Hessian-vector-product node): the mixed jet along (v, g), one launch
+void launch_jet_mix(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* v,
+                    const float* g, const float* u, float* gx, float* gv, float* gu, int d, int o, int lh, float w0,
+                    float w, float* spill, float* abuf, float* dbuf, int64_t n_pad) {
+    hipLaunchKernelGGL((jet_store_kernel<JET_BOTH, true>), grid, dim3(THREADS), 0, st, ws, x, n, NOF, gx, d, o, lh, w0,
+                       w, spill, abuf, dbuf, n_pad, NUL, NUL, v, g, u, gv, gu);
+}
 
 }  // namespace siren

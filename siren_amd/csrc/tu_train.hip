@@ -35,6 +35,14 @@ void launch_small_jet(dim3 grid, hipStream_t st, const float* abuf, const float*
                        partial, P, d, o, lh, H);
 }
 
+void launch_small_mix(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* v,
+                      const float* g, const float* u, int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P,
+                      int d, int o, int lh) {
+    hipLaunchKernelGGL(edge_kernel<EDGE_MIX>, grid, dim3(THREADS), 0, st, dbuf, abuf + (int64_t)lh * 4 * n_pad * H,
+                       (const float*)nullptr, (const float*)nullptr, x, v, g, u, n, n_pad / 4, tps, partial, P, d, o,
+                       lh, H);
+}
+
 void launch_reduce(dim3 grid, hipStream_t st, const float* partial, int64_t S, int64_t P, float* gp, int64_t S2,
                    int64_t lo, int64_t hi, int64_t bstride_part) {
     hipLaunchKernelGGL(reduce_kernel, grid, dim3(256), 0, st, partial, S, P, gp, S2, lo, hi, bstride_part);

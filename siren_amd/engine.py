@@ -52,6 +52,9 @@ class SirenEngine:
                                                          and omega_hidden != 0)))
         self.second_order_supported = (self.supported and int(hidden) == 256 and 1 <= n_hidden <= 3
                                        and int(d_out) <= 4 and bool(outermost_linear))
+        # the third-order adjoint (mixed jet, siren_hvp_backward): hidden 256, linear output, 1..5 hidden layers
+        self.hvp_backward_supported = (self.supported and int(hidden) == 256 and 1 <= n_hidden <= 5
+                                       and bool(outermost_linear))
 
     # ------------------------------------------------------------------------------------------------------
     def _require(self):
@@ -117,9 +120,44 @@ class SirenEngine:
         if want_y:
             y = out_y if out_y is not None else torch.empty(n, self.cfg.d_out, dtype=torch.float32, device=x.device)
         gx = out_gx if out_gx is not None else torch.empty(n, self.cfg.d_in, dtype=torch.float32, device=x.device)
+        tws = self._fg_workspace(n, x.device)
         _lib.check(self.lib.siren_forward_grad(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(gy), _ptr(y),
-                                               _ptr(gx), _stream(x.device)), 'siren_forward_grad')
+                                               _ptr(gx), _ptr(tws), _stream(x.device)), 'siren_forward_grad')
         return y, gx
+
+    def _fg_workspace(self, n, device):
+        """siren_forward_grad's caller-owned scratch (hidden 512: the cos spill; hidden 256: none)."""
+        cnt = ctypes.c_int64()
+        _lib.check(self.lib.siren_forward_grad_ws_floats(ctypes.byref(self.cfg), n, ctypes.byref(cnt)),
+                   'siren_forward_grad_ws_floats')
+        return torch.empty(cnt.value, dtype=torch.float32, device=device) if cnt.value > 0 else None
+
+    def hvp_backward(self, ws, x, v, g, u=None, want_theta=True, want_v=False, want_u=False):
+        """Third-order adjoint: the backward of the Hessian-vector-product node h = sum_j u_j H_j(x) v given its
+        cotangent g (siren_hvp_backward). Returns (gx, gparams | None, gv | None, gu | None) = d/d(x, theta, v, u)
+        of sum_c <g_c, h_c>."""
+        self._require()
+        if not self.hvp_backward_supported:
+            raise _lib.SirenUnsupported('siren_hvp_backward covers hidden 256, linear output, 1..5 hidden layers')
+        x = self._check_x(x)
+        n, d, o = x.shape[0], self.cfg.d_in, self.cfg.d_out
+        for name, t, w in (('v', v, d), ('g', g, d), ('u', u, o)):
+            if t is not None and (t.numel() != n * w or t.dtype != torch.float32 or t.device != x.device):
+                raise ValueError('%s must be fp32 with %d values on %s' % (name, n * w, x.device))
+        v, g = v.contiguous(), g.contiguous()
+        u = u.contiguous() if u is not None else None
+        cnt = ctypes.c_int64()
+        _lib.check(self.lib.siren_hvp_backward_ws_floats(ctypes.byref(self.cfg), n, ctypes.byref(cnt)),
+                   'siren_hvp_backward_ws_floats')
+        tws = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
+        gx = torch.empty(n, d, dtype=torch.float32, device=x.device)
+        gp = torch.empty(self.param_count, dtype=torch.float32, device=x.device) if want_theta else None
+        gv = torch.empty(n, d, dtype=torch.float32, device=x.device) if want_v else None
+        gu = torch.empty(n, o, dtype=torch.float32, device=x.device) if want_u else None
+        _lib.check(self.lib.siren_hvp_backward(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(v), _ptr(u), _ptr(g),
+                                               _ptr(tws), _ptr(gx), _ptr(gp), _ptr(gv), _ptr(gu), _stream(x.device)),
+                   'siren_hvp_backward')
+        return gx, gp, gv, gu
 
     def forward_laplace(self, ws, x, want_y=False, want_gx=False):
         """W4 in one launch: (y | None, sum_j grad y_j | None, sum_j Laplacian y_j (n, 1)) — what
@@ -256,8 +294,9 @@ class SirenEngine:
                 raise ValueError('gy must be (%d, %d, %d)' % (B, n, self.cfg.d_out))
         y = torch.empty(B, n, self.cfg.d_out, dtype=torch.float32, device=x.device) if want_y else None
         gx = torch.empty_like(x)
+        tws = self._fg_workspace(n, x.device)
         _lib.check(self.lib.siren_forward_grad_batched(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, B, _ptr(gy),
-                                                       _ptr(y), _ptr(gx), _stream(x.device)),
+                                                       _ptr(y), _ptr(gx), _ptr(tws), _stream(x.device)),
                    'siren_forward_grad_batched')
         return y, gx
 

@@ -1,0 +1,166 @@
+"""Third-order adjoint on the HIP kernels: the backward of the Hessian-vector-product node (siren_hvp_backward, the
+mixed jet of jet_kernel.hpp) against fp64 autograd, and the reference's own laplace_mse recipe —
+laplace = divergence(gradient(y, x)) with one create_graph autograd.grad per input dimension
+(/root/reference/diff_operators.py:27-43, loss_functions.py:104-109) — trained end to end with every device-torch
+recompute of siren_amd._torch_path forbidden, against the reference's G1 / G2 laplace_mse theta-gradients.
+Needs an MI355X.
+
+Tolerances: derivatives abs <= 1e-4 * max(1, max|ref|) (gx, gv, gu), theta-grads abs <= 1e-4 *
+max|ref|, all against fp64 references.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import siren_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def tol_rel(ref, rel=1e-4):
+    return rel * max(1., float(np.max(np.abs(ref))))
+
+
+def to_dev(a, dev):
+    return torch.tensor(np.asarray(a, np.float32), device=dev)
+
+
+def random_layers(d, L, o, seed=0, w=30.):
+    rng = np.random.default_rng(seed)
+    dims = [d] + [256] * (L + 1) + [o]
+    layers = []
+    for i, (fi, fo) in enumerate(zip(dims[:-1], dims[1:])):
+        bound = 1. / fi if i == 0 else np.sqrt(6. / fi) / w
+        layers.append((rng.uniform(-bound, bound, (fo, fi)).astype(np.float32),
+                       (rng.uniform(-1, 1, fo) / np.sqrt(fi)).astype(np.float32)))
+    return layers
+
+
+def hvp_vjp_ref(x, layers, v, g, u):
+    """fp64 autograd of S = sum <g, sum_j u_j H_j v>: returns dS/dx, dS/dtheta, dS/dv, dS/du."""
+    xt = torch.tensor(x, dtype=torch.float64, requires_grad=True)
+    params = [torch.tensor(t, dtype=torch.float64, requires_grad=True) for W, b in layers for t in (W, b)]
+    vt = torch.tensor(v, dtype=torch.float64, requires_grad=True)
+    y = O.torch_forward(xt, params)
+    ut = (torch.ones_like(y) if u is None else torch.tensor(u, dtype=torch.float64)).requires_grad_(True)
+    Ju = torch.autograd.grad(y, xt, ut, create_graph=True)[0]
+    hv = torch.autograd.grad(Ju, xt, vt, create_graph=True)[0]
+    S = (hv * torch.tensor(g, dtype=torch.float64)).sum()
+    grads = torch.autograd.grad(S, [xt, vt, ut] + params, allow_unused=True)
+    gp = torch.cat([(torch.zeros_like(p) if gg is None else gg).reshape(-1) for gg, p in zip(grads[3:], params)])
+    return grads[0].numpy(), gp.numpy(), grads[1].numpy(), grads[2].numpy()
+
+
+@pytest.mark.parametrize('n,d,L,o,weighted', [(1, 2, 3, 1, False), (15, 2, 3, 1, False), (4097, 2, 3, 1, False),
+                                               (1000, 3, 3, 1, True), (333, 3, 2, 3, True), (700, 4, 1, 2, True),
+                                               (2048, 2, 3, 2, True), (300, 1, 5, 1, False), (65, 2, 4, 4, True)])
+def test_hvp_backward_vs_fp64(cuda, n, d, L, o, weighted):
+    from siren_amd.engine import SirenEngine
+    layers = random_layers(d, L, o, seed=7 * n + L + o)
+    eng = SirenEngine(d, 256, L, o)
+    ws = eng.pack(to_dev(O.flatten(layers), cuda))
+    rng = np.random.default_rng(n + d)
+    x = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    v = rng.normal(size=(n, d)).astype(np.float32)
+    g = (rng.normal(size=(n, d)) / n).astype(np.float32)
+    u = rng.normal(size=(n, o)).astype(np.float32) if weighted else None
+    gx, gp, gv, gu = eng.hvp_backward(ws, to_dev(x, cuda), to_dev(v, cuda), to_dev(g, cuda),
+                                      to_dev(u, cuda) if weighted else None, want_theta=True, want_v=True,
+                                      want_u=True)
+    rgx, rgp, rgv, rgu = hvp_vjp_ref(x, layers, v, g, u)
+    assert np.max(np.abs(gp.cpu().numpy() - rgp)) <= 1e-4 * np.max(np.abs(rgp))
+    assert np.max(np.abs(gx.cpu().numpy() - rgx)) <= 1e-4 * max(1e-6, np.max(np.abs(rgx)))
+    assert np.max(np.abs(gv.cpu().numpy() - rgv)) <= 1e-4 * max(1e-6, np.max(np.abs(rgv)))
+    assert np.max(np.abs(gu.cpu().numpy() - rgu)) <= 1e-4 * max(1e-6, np.max(np.abs(rgu)))
+    # the optional outputs do not change the others (x only request: no theta / v / u work)
+    gx2, none_p, none_v, none_u = eng.hvp_backward(ws, to_dev(x, cuda), to_dev(v, cuda), to_dev(g, cuda),
+                                                   to_dev(u, cuda) if weighted else None, want_theta=False)
+    assert none_p is None and none_v is None and none_u is None and torch.equal(gx, gx2)
+
+
+def test_hvp_backward_n0_and_determinism(cuda):
+    from siren_amd.engine import SirenEngine
+    from siren_amd import dataio
+    layers = random_layers(2, 3, 1, seed=3)
+    eng = SirenEngine(2, 256, 3, 1)
+    ws = eng.pack(to_dev(O.flatten(layers), cuda))
+    z = torch.empty(0, 2, device=cuda)
+    gx, gp, _, _ = eng.hvp_backward(ws, z, z, z)
+    assert gx.shape == (0, 2) and float(gp.abs().max()) == 0.
+    x = dataio.get_mgrid(512).to(cuda)  # config-5 size
+    v = torch.zeros_like(x)
+    v[:, 0] = 1.
+    g = torch.randn_like(x) / x.shape[0]
+    a = eng.hvp_backward(ws, x, v, g)
+    b = eng.hvp_backward(ws, x, v, g)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    c = eng.hvp_backward(ws, x, v, 2. * g)  # linear in the cotangent
+    assert torch.allclose(c[1], 2. * a[1], rtol=0, atol=1e-5 * float(a[1].abs().max()))
+    idx = torch.randperm(x.shape[0], generator=torch.Generator().manual_seed(0))[:512]
+    rgx, _, _, _ = hvp_vjp_ref(x[idx].cpu().numpy(), layers, v[idx].cpu().numpy(), g[idx].cpu().numpy(), None)
+    assert np.max(np.abs(a[0][idx].cpu().numpy() - rgx)) <= 1e-4 * max(1e-6, np.max(np.abs(rgx)))
+
+
+def _forbid_torch_path(monkeypatch):
+    from siren_amd import _torch_path
+
+    def boom(*a, **k):
+        raise AssertionError('device-torch recompute used')
+    for name in ('vjp_params', 'jacobian_vjp', 'vjp_vjp', 'hvp_vjp', 'laplace_vjp', 'laplacian', 'forward'):
+        monkeypatch.setattr(_torch_path, name, boom)
+
+
+def reference_laplace(y, x):
+    """The reference's op sequence (diff_operators.py:27-43): gradient with create_graph, then one create_graph
+    autograd.grad per input dimension — NOT siren_amd.diff_operators.laplace's fused interception."""
+    grad = torch.autograd.grad(y, [x], grad_outputs=torch.ones_like(y), create_graph=True)[0]
+    div = 0.
+    for i in range(grad.shape[-1]):
+        div += torch.autograd.grad(grad[..., i], x, torch.ones_like(grad[..., i]), create_graph=True)[0][..., i:i + 1]
+    return div
+
+
+@pytest.mark.parametrize('name', ['g1', 'g2'])
+def test_reference_recipe_laplace_mse_trains_on_kernels(cuda, g1, name, request, monkeypatch):
+    """laplace_mse with the untouched recipe: gradient -> per-dimension divergence -> backward(), twice (the first
+    pass records SirenVJP nodes, the second runs with jet mode switched on: SirenJetFunction), every _torch_path
+    function forbidden; theta-grads vs the reference's fp64 laplace_mse gradients."""
+    from siren_amd.modules import SingleBVPNet
+    fx = request.getfixturevalue(name)
+    tag = name.upper()
+    _forbid_torch_path(monkeypatch)
+    m = SingleBVPNet(verbose=False).to(cuda)
+    m.load_state_dict({k[2:]: torch.tensor(v) for k, v in fx.items() if k.startswith('w_')})
+    gt = to_dev(g1['gt_laplace'], cuda)
+    for _ in range(2):
+        m.zero_grad()
+        out = m({'coords': to_dev(g1['coords'], cuda)})
+        lap = reference_laplace(out['model_out'], out['model_in'])
+        loss = torch.mean((lap - gt) ** 2)  # loss_functions.py:104-109
+        loss.backward()
+        rl = fx[tag + '_laplace_f64']
+        assert np.max(np.abs(lap.detach().cpu().numpy() - rl)) <= tol_rel(rl)
+        for k, p in m.named_parameters():
+            ref = fx[tag + '_laplace_mse_grad_' + k]
+            assert np.max(np.abs(p.grad.cpu().numpy() - ref)) <= 1e-4 * np.max(np.abs(ref)) + 1e-12, k
+
+
+def test_reference_recipe_laplace_mse_matches_fused(cuda, g2):
+    """The two HIP routes to the same loss gradient agree: the reference recipe (d HVP nodes -> d mixed jets) and
+    the fused W4 / W4s node."""
+    from siren_amd import loss_functions as LF
+    from siren_amd.modules import SingleBVPNet
+    coords = (torch.rand(1, 5000, 2, generator=torch.Generator().manual_seed(4)) * 2 - 1).to(cuda)
+    gt = torch.sin(3 * coords[..., :1]) * 1e3
+    grads = []
+    for fused in (False, True):
+        m = SingleBVPNet(verbose=False).to(cuda)
+        m.load_state_dict({k[2:]: torch.tensor(v) for k, v in g2.items() if k.startswith('w_')})
+        out = m({'coords': coords})
+        if fused:
+            loss = LF.laplace_mse(out, {'laplace': gt})['laplace_loss']
+        else:
+            loss = torch.mean((reference_laplace(out['model_out'], out['model_in']) - gt) ** 2)
+        loss.backward()
+        grads.append(torch.cat([p.grad.reshape(-1) for p in m.parameters()]))
+    assert float((grads[0] - grads[1]).abs().max()) <= 2e-5 * float(grads[1].abs().max())

@@ -94,9 +94,11 @@ def _no_second_order_fallback(monkeypatch):
     from siren_amd import _torch_path
 
     def boom(*a, **k):
-        raise AssertionError('device-torch recompute used on a second-order path')
-    monkeypatch.setattr(_torch_path, 'vjp_vjp', boom)
-    monkeypatch.setattr(_torch_path, 'jacobian_vjp', boom)
+        raise AssertionError('device-torch recompute used on a second- or third-order path')
+    # hvp_vjp: the PML losses' training backward through the second jacobian() (a third derivative) runs on the
+    # mixed-jet kernel (siren_hvp_backward)
+    for name in ('vjp_vjp', 'jacobian_vjp', 'hvp_vjp', 'vjp_params', 'laplace_vjp'):
+        monkeypatch.setattr(_torch_path, name, boom)
 
 
 def test_jacobian_hessian_vector_output_vs_reference(cuda, g6, monkeypatch):
@@ -119,7 +121,7 @@ def test_jacobian_hessian_vector_output_vs_reference(cuda, g6, monkeypatch):
 @pytest.mark.parametrize('tag,d,o,jet', [('H', 2, 2, 'auto'), ('W', 3, 1, False), ('W', 3, 1, True)])
 def test_pml_training_theta_grads_vs_reference(cuda, g6, manifest, monkeypatch, tag, d, o, jet):
     """helmholtz_pml / wave_pml training step: loss terms and theta-grads vs the reference's fp64 golden; the
-    second-order sweeps run on W3 (the vjp-of-vjp torch recompute is forbidden here)."""
+    second-order sweeps run on W3 and the third-order ones on the mixed jet (every torch recompute is forbidden)."""
     from siren_amd import loss_functions as LF
     _no_second_order_fallback(monkeypatch)
     case = pml_case(g6, tag)

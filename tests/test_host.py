@@ -184,3 +184,32 @@ def test_new_entry_points_validate_before_any_device_work(lib):
     wide = _lib.SirenCfg(3, 512, 3, 3, 30., 30., 1, 0)
     assert lib.siren_second_order_ex(ctypes.byref(wide), None, None, 1, None, None, None, None, None, None, None,
                                      None) == _lib.SIREN_EUNSUPPORTED
+
+
+def test_workspace_queries_at_zero_coords_and_caller_owned_scratch(lib):
+    """Every workspace query answers for n = 0 (the split-K plans used to divide by a zero tile count), and the
+    hidden-512 W1 takes its cos scratch from the caller (siren_forward_grad_ws_floats; no allocation inside the
+    library, SURVEY.md §8b ownership)."""
+    from siren_amd import _lib
+    cnt = ctypes.c_int64()
+    cfg = _lib.SirenCfg(2, 256, 3, 1, 30., 30., 1, 0)
+    wide = _lib.SirenCfg(3, 512, 3, 3, 30., 30., 1, 0)
+    for c in (cfg, wide):
+        assert lib.siren_train_ws_floats(ctypes.byref(c), 0, ctypes.byref(cnt)) == 0
+        assert lib.siren_train_stored_ws_floats(ctypes.byref(c), 0, ctypes.byref(cnt)) == 0
+        assert lib.siren_forward_grad_ws_floats(ctypes.byref(c), 0, ctypes.byref(cnt)) == 0 and cnt.value == 0
+    for q in ('siren_laplace_backward_ws_floats', 'siren_hvp_backward_ws_floats'):
+        assert getattr(lib, q)(ctypes.byref(cfg), 0, ctypes.byref(cnt)) == 0
+    assert lib.siren_second_order_ws_floats(ctypes.byref(cfg), 0, 1, ctypes.byref(cnt)) == 0
+    assert lib.siren_forward_grad_ws_floats(ctypes.byref(cfg), 4096, ctypes.byref(cnt)) == 0 and cnt.value == 0
+    assert lib.siren_forward_grad_ws_floats(ctypes.byref(wide), 4096, ctypes.byref(cnt)) == 0
+    assert cnt.value == 3 * 4096 * 512
+    # hidden 512 without the workspace: refused on the host, before any launch
+    P = ctypes.c_void_p
+    assert lib.siren_forward_grad(ctypes.byref(wide), P(64), P(64), 10, None, None, P(64), None, None) == \
+        _lib.SIREN_EINVAL
+    assert b'tws' in lib.siren_last_error()
+    # the third-order adjoint validates like the others
+    assert lib.siren_hvp_backward(ctypes.byref(cfg), None, None, 5, None, None, None, None, None, None, None, None,
+                                  None) == _lib.SIREN_EINVAL
+    assert lib.siren_hvp_backward_ws_floats(ctypes.byref(wide), 5, ctypes.byref(cnt)) == _lib.SIREN_EUNSUPPORTED
