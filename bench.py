@@ -12,11 +12,20 @@ timed on the host cores (cpu_baseline), a short W2 training-step rate, the PSNR 
 against the reference's (tests/golden manifest), and per-config training / inference rates for the other
 BASELINE configs (sdf = W3, 5x512 video = W2 at hidden 512, Poisson 512^2 = W4/W4s), all on the same JSON line.
 
-python bench.py [--gpus N] [--steps K] [--warmup W] [--n COORDS] [--no-cpu] [--no-extra]
+Data-parallel training legs (every N, all ranks): BASELINE configs[2] (sdf, 5x256 d3, 2^19
+coordinates per GPU resampled on the device every step, clip + Adam) and configs[3] (video, 5x512 d3 o3, 2^20
+coordinates per GPU sampled from a 64x512x512 grid every step) with FusedAdam's ONE count-weighted all-reduce of
+the flat gradient bucket over RCCL; the all-reduce is also timed alone.
+
+python bench.py [--gpus N] [--steps K] [--warmup W] [--n COORDS] [--no-cpu] [--no-extra] [--no-dp]
+With --gpus N > 1 outside torchrun, bench.py relaunches itself under torch.distributed.run (one process per GPU)
+as a child process before touching the GPU.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -43,8 +52,34 @@ def seed0_params(device):
     return torch.cat([p.detach().reshape(-1) for p in net.parameters()]).to(device)
 
 
-def cpu_baseline(seconds=15.):
-    """The oracle's torch restatement (reference op sequence + autograd gradient) on the host cores."""
+def _host_cpu():
+    """CPU model name and physical core count of this host (/proc/cpuinfo), for the cpu_baseline record."""
+    model, cores = None, set()
+    try:
+        phys = core = None
+        for line in open('/proc/cpuinfo'):
+            k, _, v = line.partition(':')
+            k, v = k.strip(), v.strip()
+            if k == 'model name' and model is None:
+                model = v
+            elif k == 'physical id':
+                phys = v
+            elif k == 'core id':
+                core = v
+            elif not k and phys is not None:
+                cores.add((phys, core))
+                phys = core = None
+        if phys is not None:
+            cores.add((phys, core))
+    except OSError:
+        pass
+    return model, len(cores) or None
+
+
+def cpu_baseline(sizes=(1 << 16, 1 << 18, 1 << 20), seconds=4.):
+    """The oracle's torch restatement (reference op sequence + autograd gradient, i.e. the reference's CPU path) on
+    the host cores at N = 2^16, 2^18, 2^20: at least one full pass and ~`seconds` of passes per
+    size. value = the N = 2^20 rate (the headline workload's size)."""
     from oracle import siren_oracle as O
     torch.manual_seed(0)
     dims = [D_IN] + [H] * (LH + 1) + [D_OUT]
@@ -52,22 +87,28 @@ def cpu_baseline(seconds=15.):
     for i, (fi, fo) in enumerate(zip(dims[:-1], dims[1:])):
         bound = 1. / fi if i == 0 else np.sqrt(6. / fi) / 30.
         params += [((torch.rand(fo, fi) * 2 - 1) * bound), ((torch.rand(fo) * 2 - 1) / np.sqrt(fi))]
-    n = 1 << 15
-    x0 = torch.rand(1, n, D_IN) * 2 - 1
-    done, t0 = 0, time.perf_counter()
-    while True:
-        x = x0.clone().requires_grad_(True)
-        y = O.torch_forward(x, params)
-        g = O.torch_gradient(y, x)
-        _ = float(g.detach().sum())
-        done += n
-        el = time.perf_counter() - t0
-        if el > seconds:
-            break
-    return {'value': round(done / el / 1e6, 4), 'unit': 'Mcoords/s', 'cores': torch.get_num_threads(),
-            'kind': 'port',
-            'sample': '%d x %d coords (5x256 d2 o1, fwd + autograd gradient, torch CPU fp32, %.1f s)'
-                      % (done // n, n, el)}
+    rates, total = {}, 0.
+    for n in sizes:
+        x0 = torch.rand(1, n, D_IN) * 2 - 1
+        done, t0 = 0, time.perf_counter()
+        while True:
+            x = x0.clone().requires_grad_(True)
+            y = O.torch_forward(x, params)
+            g = O.torch_gradient(y, x)
+            _ = float(g.detach().sum())
+            done += n
+            el = time.perf_counter() - t0
+            if el > seconds:
+                break
+        rates['n_2e%d' % (n.bit_length() - 1)] = round(done / el / 1e6, 4)
+        total += el
+    model, phys = _host_cpu()
+    return {'value': rates['n_2e%d' % (sizes[-1].bit_length() - 1)], 'unit': 'Mcoords/s',
+            'cores': torch.get_num_threads(), 'kind': 'port', 'rates_by_n': rates, 'cpu_model': model,
+            'host_physical_cores': phys,
+            'sample': 'N = %s coords, >= %.0f s each (%.1f s total): 5x256 d2 o1 fwd + autograd gradient, torch CPU '
+                      'fp32 on %d threads' % ('/'.join('2^%d' % (n.bit_length() - 1) for n in sizes), seconds, total,
+                                               torch.get_num_threads())}
 
 
 def kernel_roofline(eng, ws, x, reps=10):
@@ -229,13 +270,7 @@ def config_rates(device, steps=5):
         eng_b.forward_grad_batched(wsb, xb)
     torch.cuda.synchronize()
     res['hypernet_b32x4096_grouped_w1_mcoords_s'] = round(32 * 4096 * steps / (time.perf_counter() - t0) / 1e6, 3)
-    # configs[3]: video fit, 5x512 d3 o3 image_mse (W2 at hidden 512), 2^18 coords per GPU
-    torch.manual_seed(0)
-    m = SingleBVPNet(in_features=3, out_features=3, hidden_features=512, verbose=False).to(device)
-    n = 1 << 18
-    x = torch.rand(1, n, 3, device=device) * 2 - 1
-    gt = 0.5 + 0.5 * torch.sin(3 * x + torch.tensor([0., 1., 2.], device=device))
-    res['video_5x512_d3o3_train_mcoords_s'] = rate(m, x, lambda o: LF.image_mse(None, o, {'img': gt}), n)
+    # configs[3] (video, 5x512 d3 o3, 2^20 coordinates per GPU sampled from a 64x512x512 volume): dp_train
     # configs[4]: Poisson on a 512^2 grid: laplace_mse training (W4 + W4s) and W4 inference (y, grad, Laplacian)
     torch.manual_seed(0)
     m = SingleBVPNet(verbose=False).to(device)
@@ -261,6 +296,101 @@ def config_rates(device, steps=5):
         eng.forward_laplace(ws, x2, True, True)
     torch.cuda.synchronize()
     res['poisson_512sq_w4_y_grad_laplacian_mcoords_s'] = round(n * steps / (time.perf_counter() - t0) / 1e6, 3)
+    return res
+
+
+def dp_train_rates(device, world, rank, steps=5, warmup=2):
+    """Data-parallel training steps at every N (weak scaling: a fixed per-GPU batch), the reference's loop semantics
+    (training.py:72-104: forward, loss means, backward, all-reduce, clip, Adam) with FusedAdam's single count-
+    weighted all-reduce of the flat gradient bucket. Returns {config: {...}}; rates are whole-job Mcoords/s from the
+    max over ranks of the timed region."""
+    import torch.distributed as dist
+    from siren_amd.modules import SingleBVPNet
+    from siren_amd import loss_functions as LF
+    from siren_amd import dataio
+    from siren_amd.optim import FusedAdam
+    from siren_amd import distributed as sd
+    res = {}
+
+    def timed(step_fn, n_local, opt):
+        for i in range(warmup):
+            step_fn(i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step_fn(warmup + i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        ar_us = None
+        if world > 1:
+            t = torch.tensor([el], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+            # the bucket all-reduce alone (same size and backend), HIP events on the current stream
+            st = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            for _ in range(3):
+                dist.all_reduce(opt.bucket)
+            torch.cuda.synchronize()
+            e0.record(st)
+            for _ in range(20):
+                dist.all_reduce(opt.bucket)
+            e1.record(st)
+            torch.cuda.synchronize()
+            ar_us = round(e0.elapsed_time(e1) / 20 * 1e3, 2)
+        return {'mcoords_s': round(world * n_local * steps / el / 1e6, 3), 'ms_per_step': round(el / steps * 1e3, 3),
+                'coords_per_gpu': n_local, 'allreduce_us': ar_us, 'bucket_bytes': int(opt.bucket.numel() * 4),
+                'steps': steps}
+
+    # configs[2]: sdf, 5x256 d3, 2^18 on + 2^18 off surface per GPU, device PointCloud resampled every step,
+    # clip_grad=True (train_sdf.py:57-60)
+    g = torch.Generator().manual_seed(0)
+    d = torch.randn(1 << 20, 3, generator=g, dtype=torch.float64)
+    d = d / d.norm(dim=-1, keepdim=True)
+    pcd = dataio.PointCloud(points=torch.cat([d * 0.5, d], 1).numpy(), on_surface_points=1 << 18, device=device)
+    torch.manual_seed(0)
+    m = SingleBVPNet(in_features=3, verbose=False).to(device)
+    sd.broadcast_parameters(m)
+    opt = FusedAdam(m.parameters(), lr=1e-4, max_norm=1.)
+
+    def sdf_step(i):
+        inp, gt = pcd.sample(i * world + rank)  # each rank its own draw
+        out = m({'coords': inp['coords'][None]})
+        total = sum(v.mean() for v in LF.sdf(out, {k: v[None] for k, v in gt.items()}).values())
+        opt.zero_grad()
+        total.backward()
+        if world > 1:
+            opt.allreduce_grad(world, inp['coords'].shape[0])
+        opt.step()
+    res['sdf_5x256_d3'] = timed(sdf_step, 1 << 19, opt)
+    del m, opt, pcd
+    # configs[3]: video, 5x512 d3 o3 (image_mse), 2^20 coordinates per GPU sampled every step from the 64x512x512
+    # grid of a synthetic video (dataio.py:655-673 Implicit3DWrapper, sample_fraction < 1: randint rows)
+    mgrid = dataio.get_mgrid((64, 512, 512), dim=3).to(device)
+    vid = dataio.synthetic_video(mgrid)
+    torch.manual_seed(0)
+    m = SingleBVPNet(in_features=3, out_features=3, hidden_features=512, verbose=False).to(device)
+    sd.broadcast_parameters(m)
+    opt = FusedAdam(m.parameters(), lr=1e-4)
+    gen = torch.Generator(device=device).manual_seed(100 + rank)
+    nv = 1 << 20
+
+    def video_step(i):
+        idx = torch.randint(0, mgrid.shape[0], (nv,), device=device, generator=gen)
+        out = m({'coords': mgrid[idx][None]})
+        total = LF.image_mse(None, out, {'img': vid[idx][None]})['img_loss'].mean()
+        opt.zero_grad()
+        total.backward()
+        if world > 1:
+            opt.allreduce_grad(world, nv)
+        opt.step()
+    res['video_5x512_d3o3'] = timed(video_step, nv, opt)
+    del m, opt, mgrid, vid
+    torch.cuda.empty_cache()
     return res
 
 
@@ -294,15 +424,30 @@ def main():
     ap.add_argument('--n', type=int, default=1 << 20, help='coordinates per GPU per step')
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--no-extra', action='store_true')
+    ap.add_argument('--no-dp', action='store_true', help='skip the data-parallel training legs')
     args = ap.parse_args()
+
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        # one process per GPU: relaunch under torchrun as a CHILD process, before anything touches the GPU
+        s = socket.socket()
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+        s.close()
+        cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(args.gpus),
+               '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # one GPU per rank over RCCL ("nccl"); SIREN_DIST_BACKEND=gloo with more ranks than GPUs is a rehearsal mode
+    # (ranks share devices round-robin) for checking the multi-rank code path on a 1-GPU box
+    ndev = max(1, torch.cuda.device_count())
+    dev_idx = local if local < ndev else local % ndev
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl')
-    device = torch.device('cuda', local)
+        torch.cuda.set_device(dev_idx)
+        dist.init_process_group(os.environ.get('SIREN_DIST_BACKEND', 'nccl'))
+    device = torch.device('cuda', dev_idx)
 
     import __graft_entry__
     __graft_entry__.build()
@@ -338,6 +483,9 @@ def main():
 
     ws = eng.pack(flat)
     kms, achieved = kernel_roofline(eng, ws, x)
+    n_ranks = dist.get_world_size() if world > 1 else 1  # ranks the process group (RCCL) initialised
+    del y, gx, ws
+    dp = None if args.no_dp else dp_train_rates(device, n_ranks, rank)
     extra = {}
     if rank == 0 and not args.no_extra:
         extra['w2_image_mse_train_mcoords_s'] = round(train_step_rate(device), 3)
@@ -346,24 +494,25 @@ def main():
         extra['psnr_db'] = {'value': round(p, 3), 'reference_cpu': REF_PSNR_DB, 'steps': 300,
                             'fit_seconds': round(secs, 2)}
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and n_ranks == 1 and not args.no_cpu:
         cpu = cpu_baseline()
 
     if rank == 0:
         traffic = pmc_traffic(args.n)
         line = {
             'metric': 'Mcoords/sec fwd+∇ (5×256 SIREN) at 1/2/4/8 MI355X; PSNR vs ref',
-            'value': round(value, 3), 'unit': 'Mcoords/s', 'n_gpus': world, 'steps': args.steps,
+            'value': round(value, 3), 'unit': 'Mcoords/s', 'n_gpus': n_ranks, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(el / args.steps * 1e3, 4), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
             'config': {'workload': 'W1 fused fwd+grad, SingleBVPNet 5x256 (d_in 2, 3 hidden, out 1, w0 30), '
                                    'N=%d random coords per GPU per step' % args.n,
-                       'coords_per_gpu': args.n, 'parallelism': 'dp%d' % world},
+                       'coords_per_gpu': args.n, 'parallelism': 'dp%d' % n_ranks},
             'roofline': {'bound': 'mfma', 'achieved': round(achieved, 3), 'peak': PEAK_FP32_MFMA_TFLOPS,
                          'unit': 'TFLOP/s', 'frac': round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
                          'traffic': traffic, 'kernel_ms': round(kms, 4),
                          'flop_per_coord': W1_FLOP},
             'cpu_baseline': cpu,
+            'dp_train': dp,
         }
         line.update(extra)
         print(json.dumps(line), flush=True)

@@ -32,11 +32,13 @@ def init(backend=None):
 
 
 def shard(n, world, rank, align=64):
-    """[start, stop) of rank's share of n coordinates; shares are multiples of `align` except the last."""
-    per = -(-n // world)
-    per = -(-per // align) * align
-    start = min(rank * per, n)
-    return start, min(start + per, n)
+    """[start, stop) of rank's share of n coordinates: boundaries at the multiples of `align` (the kernels' coordinate
+    tile) nearest below the even split, the last rank ending at n, so the shares differ by less than `align` (ranks
+    may be empty when n < world * align). Unequal shares are made exact by allreduce_gradients(count=...), which
+    weights each rank's mean-loss gradient by its coordinate count."""
+    def bound(r):
+        return n if r >= world else (r * n // world) // align * align
+    return bound(rank), bound(rank + 1)
 
 
 def broadcast_parameters(module, src=0):
@@ -51,17 +53,34 @@ def broadcast_parameters(module, src=0):
             off += p.numel()
 
 
-def allreduce_gradients(params, world=None):
-    """Average .grad of `params` over ranks with ONE all-reduce of a flat bucket (in place)."""
+def allreduce_gradients(params, world=None, count=None):
+    """Reduce .grad of `params` over ranks with ONE all-reduce of a flat bucket (in place).
+
+    count=None: plain average (equal shards). count = this rank's coordinate count: the bucket carries count * grad
+    plus the count itself, so the result is sum_r n_r g_r / sum_r n_r — the full-batch gradient of a mean-over-
+    coordinates loss for any split, including empty shards (count 0 contributes nothing; its NaN mean-loss gradient
+    must not have been back-propagated, see training.train)."""
     if not (dist.is_available() and dist.is_initialized()):
         return
     world = world or dist.get_world_size()
-    params = [p for p in params if p.grad is not None]
+    if count is not None:  # every rank sends the full bucket, an empty shard's (unset) grads as zeros
+        params = list(params)
+        for p in params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+    else:
+        params = [p for p in params if p.grad is not None]
     if not params:
         return
-    flat = torch.cat([p.grad.reshape(-1) for p in params])
+    flat = torch.cat([p.grad.reshape(-1) for p in params] +
+                     ([p.grad.new_full((1,), float(count))] if count is not None else []))
+    if count is not None:
+        flat[:-1].mul_(float(count))
     dist.all_reduce(flat, op=dist.ReduceOp.SUM)
-    flat.div_(world)
+    if count is not None:
+        flat = flat[:-1].div_(flat[-1:].clamp_min(1.))
+    else:
+        flat.div_(world)
     off = 0
     for p in params:
         n = p.numel()

@@ -29,7 +29,9 @@ class FusedAdam:
         self.lr, self.betas, self.eps, self.max_norm = float(lr), tuple(betas), float(eps), max_norm
         n = sum(p.numel() for p in self.params)
         self.flat = torch.empty(n, device=dev)
-        self.grad = torch.zeros(n, device=dev)
+        # the gradient bucket + one slot for the coordinate count of a count-weighted all-reduce (allreduce_grad)
+        self.bucket = torch.zeros(n + 1, device=dev)
+        self.grad = self.bucket[:n]
         self.exp_avg = torch.zeros(n, device=dev)
         self.exp_avg_sq = torch.zeros(n, device=dev)
         cnt = ctypes.c_int64()
@@ -71,12 +73,21 @@ class FusedAdam:
         self._bind_grads()
 
     @torch.no_grad()
-    def allreduce_grad(self, world):
-        """Data parallel: average the flat gradient bucket over ranks with ONE all-reduce (RCCL over xGMI)."""
+    def allreduce_grad(self, world, count=None):
+        """Data parallel: reduce the flat gradient bucket over ranks with ONE all-reduce (RCCL over xGMI), in place.
+        count=None averages (equal shards); count = this rank's coordinate count weights the ranks' mean-loss
+        gradients by their shares (sum_r n_r g_r / sum_r n_r, distributed.allreduce_gradients), the count riding
+        in the bucket's last slot so it stays one collective and no host sync."""
         import torch.distributed as dist
         self._gather_grads()
-        dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)
-        self.grad.div_(world)
+        if count is None:
+            dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)
+            self.grad.div_(world)
+            return
+        self.grad.mul_(float(count))
+        self.bucket[-1] = float(count)
+        dist.all_reduce(self.bucket, op=dist.ReduceOp.SUM)
+        self.grad.div_(self.bucket[-1:].clamp_min(1.))
 
     @torch.no_grad()
     def step(self):

@@ -32,6 +32,12 @@ def _writer(summaries_dir):
         return _NullWriter()
 
 
+def _coord_count(model_input):
+    """Coordinates in this rank's batch (B * N of model_input['coords'] (B, N, d))."""
+    c = model_input['coords']
+    return c.numel() // max(1, c.shape[-1])
+
+
 def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_checkpoint, model_dir, loss_fn,
           summary_fn=None, val_dataloader=None, double_precision=False, clip_grad=False, use_lbfgs=False,
           loss_schedules=None, device='cuda', log=print, writer=None, fused_adam=False):
@@ -76,8 +82,10 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
                 def closure():
                     optim.zero_grad()
                     _, loss = step_losses(model_input, gt, total_steps)
-                    loss.backward()
-                    distributed.allreduce_gradients(list(model.parameters()), world)
+                    count = _coord_count(model_input) if world > 1 else None
+                    if count != 0:
+                        loss.backward()
+                    distributed.allreduce_gradients(list(model.parameters()), world, count)
                     return loss
                 optim.step(closure)
             model_output, train_loss = step_losses(model_input, gt, total_steps)
@@ -89,11 +97,15 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
                     summary_fn(model, model_input, gt, model_output, writer, total_steps)
             if not use_lbfgs:
                 optim.zero_grad()
-                train_loss.backward()
+                # under DP each rank's mean-loss gradient is weighted by its coordinate count in the reduction (exact
+                # full-batch gradient for unequal shards); an empty shard contributes zeros, never its NaN mean
+                count = _coord_count(model_input) if world > 1 else None
+                if count != 0:
+                    train_loss.backward()
                 if fused_adam and world > 1:
-                    optim.allreduce_grad(world)  # the bucket itself is the all-reduce buffer: no gather / scatter
+                    optim.allreduce_grad(world, count)  # the bucket itself is the all-reduce buffer: no gather / scatter
                 else:
-                    distributed.allreduce_gradients(list(model.parameters()), world)
+                    distributed.allreduce_gradients(list(model.parameters()), world, count)
                 if clip_grad and not fused_adam:
                     max_norm = 1. if isinstance(clip_grad, bool) else clip_grad
                     torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
