@@ -270,6 +270,15 @@ def config_rates(device, steps=5):
         eng_b.forward_grad_batched(wsb, xb)
     torch.cuda.synchronize()
     res['hypernet_b32x4096_grouped_w1_mcoords_s'] = round(32 * 4096 * steps / (time.perf_counter() - t0) / 1e6, 3)
+    gyb = torch.randn(32, 4096, 1, device=device)
+    eng_b.backward_params_batched(wsb, xb, gyb)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng_b.backward_params_batched(wsb, xb, gyb)
+    torch.cuda.synchronize()
+    res['hypernet_b32x4096_grouped_w2_backward_mcoords_s'] = round(
+        32 * 4096 * steps / (time.perf_counter() - t0) / 1e6, 3)
     # configs[3] (video, 5x512 d3 o3, 2^20 coordinates per GPU sampled from a 64x512x512 volume): dp_train
     # configs[4]: Poisson on a 512^2 grid: laplace_mse training (W4 + W4s) and W4 inference (y, grad, Laplacian)
     torch.manual_seed(0)
@@ -394,6 +403,37 @@ def dp_train_rates(device, world, rank, steps=5, warmup=2):
     return res
 
 
+PATH_UNITS = {'w1': 2, 'image_w2': 3, 'sdf': 8, 'video': 3, 'poisson': 15, 'poisson_ref': 15, 'hypernet': 2}
+
+
+def path_rooflines(rates):
+    """Per-config roofline for the training paths: the MFMA fraction of the path's algorithmic flops (SURVEY.md §8a
+    work units) at the rate measured live in this run (whole step: kernels + loss / optimizer / sampling ops), and
+    from the committed per-path profile (profiles/pmc_<path>.json, tools/profile_round.sh: rocprofv3 kernel time,
+    FETCH_SIZE / WRITE_SIZE HBM bytes per step and the kernels' I/O-contract bytes)."""
+    out = {}
+    for path, mc in rates.items():
+        if mc is None:
+            continue
+        try:
+            rec = json.load(open(os.path.join(ROOT, 'profiles', 'pmc_%s.json' % path)))
+        except (OSError, ValueError):
+            rec = None
+        if rec is None:
+            continue
+        c = rec['config']
+        F = 2 * (c['d_in'] * c['hidden'] + c['hidden_layers'] * c['hidden'] ** 2 + c['hidden'] * c['d_out'])
+        ach = PATH_UNITS[path] * F * mc * 1e6 / 1e12
+        out[path] = {'bound': 'mfma', 'unit': 'TFLOP/s', 'peak': PEAK_FP32_MFMA_TFLOPS,
+                     'flop_per_coord': PATH_UNITS[path] * F, 'achieved_step': round(ach, 2),
+                     'frac_step': round(ach / PEAK_FP32_MFMA_TFLOPS, 4),
+                     'frac_kernels_rocprof': rec.get('mfma_frac_of_kernel_time'),
+                     'traffic_bytes_per_step': rec.get('hbm_bytes_per_step'),
+                     'io_bytes_per_step': rec.get('io_bytes_per_step'), 'profiled_n': rec.get('n'),
+                     'profile': 'profiles/pmc_%s.json' % path}
+    return out
+
+
 def psnr_fit(device, steps=300):
     """Config-1 fit (256^2 synthetic image, full batch, Adam lr 1e-4, image_mse) on the fused engine."""
     from siren_amd.modules import SingleBVPNet
@@ -490,6 +530,14 @@ def main():
     if rank == 0 and not args.no_extra:
         extra['w2_image_mse_train_mcoords_s'] = round(train_step_rate(device), 3)
         extra['configs'] = config_rates(device)
+        cr, dpr = extra['configs'], dp or {}
+        extra['roofline_by_path'] = path_rooflines({
+            'image_w2': extra['w2_image_mse_train_mcoords_s'],
+            'sdf': dpr.get('sdf_5x256_d3', {}).get('mcoords_s') if n_ranks == 1 else None,
+            'video': dpr.get('video_5x512_d3o3', {}).get('mcoords_s') if n_ranks == 1 else None,
+            'poisson': cr['poisson_512sq_laplace_mse_train_mcoords_s'],
+            'poisson_ref': cr['poisson_512sq_reference_recipe_laplace_mse_train_mcoords_s'],
+            'hypernet': cr['hypernet_b32x4096_grouped_w2_backward_mcoords_s']})
         p, secs = psnr_fit(device)
         extra['psnr_db'] = {'value': round(p, 3), 'reference_cpu': REF_PSNR_DB, 'steps': 300,
                             'fit_seconds': round(secs, 2)}

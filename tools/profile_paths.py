@@ -1,0 +1,136 @@
+"""Runs ONE training / inference path of the engine at its bench configuration, so a rocprofv3 kernel trace or PMC
+pass over this process is attributable to that path (tools/profile_round.sh), and prints its HIP-event timing.
+
+python tools/profile_paths.py <path> [--reps R]     (1 warm-up step + R timed steps; prints one JSON line)
+
+Paths (BASELINE.json configs; F = 2 sum fan_in fan_out FLOP per coordinate):
+  image_w2     5x256 d2 o1, 2^18 coords: forward_store + backward_stored (image_mse train kernels, W2 = 3F)
+  sdf          5x256 d3 o1, 2^19 coords: forward_grad_store + seeded W3 from the kept forward (sdf kernels, 8F)
+  video        5x512 d3 o3, 2^20 coords: forward_store + backward_stored (hidden 512 W2 = 3F)
+  poisson      5x256 d2 o1, 512^2 grid: forward_laplace_store + laplace_backward_stored (W4s = 3 (1 + 2d) F = 15F)
+  poisson_ref  5x256 d2 o1, 512^2 grid: the reference recipe's kernels: W1 (J), d x W3 (H e_i), d x mixed jet
+               (third-order adjoint); the same loss gradient as poisson (15F counted)
+  w3_theta     5x256 d2 o1, 2^19 coords: W3 H v + theta-grads without a kept forward (6F)
+  hypernet     32 x 4096 coords, 5x256 d2 o1 per-element weights: grouped W2 backward (2F per coordinate)
+  w1           5x256 d2 o1, 2^20 coords: the headline W1 launch (2F)
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+PATHS = {  # name: (d, hidden, layers, o, n, work units of F)
+    'image_w2': (2, 256, 3, 1, 1 << 18, 3),
+    'sdf': (3, 256, 3, 1, 1 << 19, 8),
+    'video': (3, 512, 3, 3, 1 << 20, 3),
+    'poisson': (2, 256, 3, 1, 512 * 512, 15),
+    'poisson_ref': (2, 256, 3, 1, 512 * 512, 15),
+    'w3_theta': (2, 256, 3, 1, 1 << 19, 6),
+    'hypernet': (2, 256, 3, 1, 32 * 4096, 2),
+    'w1': (2, 256, 3, 1, 1 << 20, 2),
+}
+
+
+def flop_per_coord(d, H, L, o):
+    return 2 * (d * H + L * H * H + H * o)
+
+
+def build_step(name, dev):
+    from siren_amd.engine import SirenEngine
+    from siren_amd.modules import FCBlock
+    d, H, L, o, n, _ = PATHS[name]
+    torch.manual_seed(0)
+    net = FCBlock(d, o, L, H, outermost_linear=True, nonlinearity='sine')
+    flat = torch.cat([p.detach().reshape(-1) for p in net.parameters()]).to(dev)
+    eng = SirenEngine(d, H, L, o)
+    g = torch.Generator(device=dev).manual_seed(1)
+    if name == 'hypernet':
+        B = 32
+        fb = flat[None].repeat(B, 1) + 1e-3 * torch.randn(B, flat.numel(), device=dev, generator=g)
+        wsb = eng.pack_batched(fb)
+        xb = torch.rand(B, n // B, d, device=dev, generator=g) * 2 - 1
+        gyb = torch.randn(B, n // B, o, device=dev, generator=g)
+        return lambda: eng.backward_params_batched(wsb, xb, gyb)
+    ws = eng.pack(flat)
+    if name.startswith('poisson'):
+        from siren_amd import dataio
+        x = dataio.get_mgrid(512).to(dev)
+    else:
+        x = torch.rand(n, d, device=dev, generator=g) * 2 - 1
+    gy = torch.randn(n, o, device=dev, generator=g)
+    if name == 'w1':
+        return lambda: eng.forward_grad(ws, x)
+    if name in ('image_w2', 'video'):
+        def step():
+            _, tws = eng.forward_store(ws, x)
+            eng.backward_stored(ws, x, gy, tws)
+        return step
+    if name == 'sdf':
+        v = torch.randn(n, d, device=dev, generator=g)
+
+        def step():
+            _, _, kept = eng.forward_grad_store(ws, x)
+            eng.second_order(ws, x, v, want_theta=True, gy=gy, kept=kept)
+        return step
+    if name == 'w3_theta':
+        v = torch.randn(n, d, device=dev, generator=g)
+        return lambda: eng.second_order(ws, x, v, want_theta=True)
+    gl = torch.randn(n, 1, device=dev, generator=g) / n
+    if name == 'poisson':
+        def step():
+            _, tws = eng.forward_laplace_store(ws, x)
+            eng.laplace_backward_stored(ws, x, gl, tws)
+        return step
+    if name == 'poisson_ref':
+        es = []
+        for i in range(d):
+            e = torch.zeros(n, d, device=dev)
+            e[:, i] = 1.
+            es.append(e)
+
+        def step():
+            eng.forward_grad(ws, x)
+            gx = 0.
+            for i in range(d):
+                eng.second_order(ws, x, es[i], want_theta=False)  # the divergence's H e_i nodes (forward)
+            for i in range(d):
+                r = eng.hvp_backward(ws, x, es[i], gl * es[i])      # their backward (third order)
+                gx = gx + r[1]
+            return gx
+        return step
+    raise ValueError(name)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('path', choices=sorted(PATHS))
+    ap.add_argument('--reps', type=int, default=5)
+    a = ap.parse_args()
+    import __graft_entry__
+    __graft_entry__.build()
+    dev = torch.device('cuda', 0)
+    step = build_step(a.path, dev)
+    step()
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(a.reps):
+        step()
+    e1.record(st)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / a.reps
+    d, H, L, o, n, units = PATHS[a.path]
+    flops = units * flop_per_coord(d, H, L, o) * n
+    print(json.dumps({'path': a.path, 'n': n, 'steps_total': a.reps + 1, 'ms_per_step': round(ms, 4),
+                      'flop_per_step': flops, 'tflops': round(flops / ms / 1e9, 2),
+                      'frac_fp32_peak': round(flops / ms / 1e9 / 157.3, 4), 'mcoords_s': round(n / ms / 1e3, 3)}),
+          flush=True)
+
+
+if __name__ == '__main__':
+    main()

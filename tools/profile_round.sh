@@ -1,0 +1,25 @@
+#!/bin/bash
+# Per-path profiles of the training / inference kernels (tools/profile_paths.py): for every path one HIP-event
+# timing run, one rocprofv3 kernel-trace + stats run, and two PMC passes (FETCH_SIZE, WRITE_SIZE: one counter group
+# per pass, never combined with tracing), then tools/path_summary.py -> <out>/pmc_<path>.json.
+# usage (gpurun, from the repo root): bash tools/profile_round.sh <tag> [paths...]
+set -o pipefail
+TAG=${1:-r02}
+shift
+PATHS_TO_RUN=${@:-"w1 image_w2 sdf w3_theta video poisson poisson_ref hypernet"}
+R=$PWD
+O=$R/gpurun_out/prof_$TAG
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+for p in $PATHS_TO_RUN; do
+  mkdir -p $O/$p
+  timeout -k 10 120 python3 $R/tools/profile_paths.py $p > $O/$p/timing.json 2> $O/$p/timing.err || { echo "timing $p failed"; tail -5 $O/$p/timing.err; exit 1; }
+  cat $O/$p/timing.json
+  timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$p/trace -o run -- python3 $R/tools/profile_paths.py $p > $O/$p/trace.log 2>&1 || { echo "trace $p failed"; tail -5 $O/$p/trace.log; exit 1; }
+  i=0
+  for grp in FETCH_SIZE WRITE_SIZE; do
+    i=$((i+1))
+    timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $O/$p/pmc$i -o pmc -- python3 $R/tools/profile_paths.py $p > $O/$p/pmc$i.log 2>&1 || { echo "pmc $grp $p failed"; exit 1; }
+  done
+done
+cd $R && python3 tools/path_summary.py $O $O && echo done
