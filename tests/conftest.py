@@ -90,3 +90,8 @@ def pml_ref_grads(g6, tag):
 @pytest.fixture(scope='session')
 def g7():
     return load_golden('g7')
+
+
+@pytest.fixture(scope='session')
+def g8():
+    return load_golden('g8')

@@ -19,11 +19,15 @@ Fixtures:
   G7  batched (hypernetwork) weights: the reference's HyperNetwork (meta_modules.py:10-53)
       predicts 3 sets of 5x256 d2 o1 weights from 3 embeddings; SingleBVPNet(params=...) on (3, 512, 2) coords:
       the predicted weights, model_out, gradient and the image_mse gradient w.r.t. the predicted weights.
+  G8  reference-pinned inputs and the notebook API: dataio.get_mgrid (dataio.py:20-40) at several shapes, imported
+      with its image/video dependencies stubbed; the notebook SineLayer / Siren (explore_siren.ipynb cells 3 and 5,
+      executed from the notebook's JSON) at hidden 256: outermost_linear True / False, first_omega_0 30 / 3000 —
+      init weights, forward output, coords gradient (and Laplacian, image-mse theta-grads) in fp32 and fp64.
   G6  vector outputs / PML losses: 5x256 d2 o2 (helmholtz_pml, loss_functions.py:139-211)
       and 5x256 d3 o1 (wave_pml, loss_functions.py:112-136), 1024 coords each: jacobian / hessian
       (diff_operators.py:5-24, 46-59), the loss terms and their fp64 theta-grads.
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--skip-fit] [--only g6,g7]
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--skip-fit] [--only g6,g7,g8]
 """
 import argparse
 from collections import OrderedDict
@@ -207,6 +211,75 @@ def make_g7(modules, D, L, meta):
     np.savez_compressed(os.path.join(OUT, 'golden_g7.npz'), **store)
 
 
+def import_reference_dataio():
+    """dataio.py with the image / video packages it imports at module level stubbed (only get_mgrid is used)."""
+    for name in ('skimage', 'skimage.filters', 'skvideo', 'skvideo.io', 'torchvision', 'torchvision.transforms',
+                 'cv2', 'cmapy', 'scipy.io.wavfile'):
+        if name not in sys.modules:
+            try:
+                __import__(name)
+            except ImportError:
+                sys.modules[name] = types.ModuleType(name)
+    tv = sys.modules['torchvision.transforms']
+    for attr in ('Resize', 'Compose', 'ToTensor', 'Normalize', 'CenterCrop'):
+        if not hasattr(tv, attr):
+            setattr(tv, attr, object)
+    sys.modules['torchvision'].transforms = tv
+    import dataio
+    return dataio
+
+
+def notebook_namespace():
+    """Executes the notebook's SineLayer / Siren cell and its diff-operator cell (explore_siren.ipynb) into a fresh
+    namespace (torch, nn, np bound as the notebook's first cell binds them)."""
+    nb = json.load(open(os.path.join(REF, 'explore_siren.ipynb')))
+    ns = {'torch': torch, 'nn': torch.nn, 'np': np}
+    want = ('class SineLayer', 'def laplace(y, x)')
+    for cell in nb['cells']:
+        src = ''.join(cell['source'])
+        if cell['cell_type'] == 'code' and any(w in src for w in want):
+            exec(compile(src, 'explore_siren.ipynb', 'exec'), ns)
+    return ns
+
+
+def make_g8(modules, D, L, meta):
+    dataio = import_reference_dataio()
+    store = {}
+    for key, args in (('mgrid_256', (256,)), ('mgrid_3x7', ((3, 7),)), ('mgrid_32_d3', (32, 3)),
+                      ('mgrid_16x32x48_d3', ((16, 32, 48), 3)), ('mgrid_1x4x5_d3', ((1, 4, 5), 3))):
+        store[key] = dataio.get_mgrid(*args).numpy()
+    ns = notebook_namespace()
+    cases = {'A': dict(args=(2, 256, 3, 1), kw=dict(outermost_linear=True), seed=0, d=2),
+             'B': dict(args=(1, 256, 3, 1), kw=dict(outermost_linear=True, first_omega_0=3000, hidden_omega_0=30.),
+                       seed=1, d=1),
+             'C': dict(args=(2, 256, 3, 3), kw=dict(outermost_linear=False), seed=2, d=2)}
+    for tag, c in cases.items():
+        torch.manual_seed(c['seed'])
+        net = ns['Siren'](*c['args'], **c['kw'])
+        for k, v in state_to_np(net.state_dict()).items():
+            store['%s_w_%s' % (tag, k)] = v
+        gen = torch.Generator().manual_seed(80 + c['seed'])
+        coords = torch.rand(1, 2048, c['d'], generator=gen) * 2 - 1
+        store[tag + '_coords'] = coords.numpy()
+        meta['G8_%s_config' % tag] = {'args': list(c['args']), 'kw': c['kw'], 'seed': c['seed']}
+        for dtype, dt in ((torch.float32, 'f32'), (torch.float64, 'f64')):
+            net = net.to(dtype)
+            out, x = net(coords.to(dtype))
+            store['%s_model_out_%s' % (tag, dt)] = out.detach().numpy()
+            g = ns['gradient'](out, x)
+            store['%s_gradient_%s' % (tag, dt)] = g.detach().numpy()
+            if tag == 'A':
+                store['%s_laplace_%s' % (tag, dt)] = ns['laplace'](out, x).detach().numpy()
+            if tag == 'A' and dt == 'f64':
+                target = torch.sin(5 * coords[..., :1]).to(dtype)
+                loss = ((out - target) ** 2).mean()
+                for k, gk in zip([k for k, _ in net.named_parameters()],
+                                 torch.autograd.grad(loss, list(net.parameters()))):
+                    store['A_image_mse_grad_' + k] = gk.numpy()
+        net.float()
+    np.savez_compressed(os.path.join(OUT, 'golden_g8.npz'), **store)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--skip-fit', action='store_true', help='reuse the G5 weights already in golden_fit.npz')
@@ -217,7 +290,7 @@ def main():
         with open(os.path.join(OUT, 'manifest.json')) as f:
             meta = json.load(f)
         for name in args.only.split(','):
-            {'g6': make_g6, 'g7': make_g7}[name](modules, D, L, meta)
+            {'g6': make_g6, 'g7': make_g7, 'g8': make_g8}[name](modules, D, L, meta)
         with open(os.path.join(OUT, 'manifest.json'), 'w') as f:
             json.dump(meta, f, indent=1, sort_keys=True)
         return

@@ -213,3 +213,30 @@ def test_workspace_queries_at_zero_coords_and_caller_owned_scratch(lib):
     assert lib.siren_hvp_backward(ctypes.byref(cfg), None, None, 5, None, None, None, None, None, None, None, None,
                                   None) == _lib.SIREN_EINVAL
     assert lib.siren_hvp_backward_ws_floats(ctypes.byref(wide), 5, ctypes.byref(cnt)) == _lib.SIREN_EUNSUPPORTED
+
+
+@pytest.mark.parametrize('key,args', [('mgrid_256', (256,)), ('mgrid_3x7', ((3, 7),)), ('mgrid_32_d3', (32, 3)),
+                                      ('mgrid_16x32x48_d3', ((16, 32, 48), 3)), ('mgrid_1x4x5_d3', ((1, 4, 5), 3))])
+def test_get_mgrid_bit_exact_vs_reference(g8, key, args):
+    """siren_amd.dataio.get_mgrid == the reference's dataio.get_mgrid (dataio.py:20-40), bit for bit (G8 fixture,
+    produced by importing the reference's dataio in the build container)."""
+    from siren_amd.dataio import get_mgrid
+    g = get_mgrid(*args)
+    assert g.dtype == torch.float32 and np.array_equal(g.numpy(), g8[key])
+
+
+@pytest.mark.parametrize('tag,args,kw,seed', [
+    ('A', (2, 256, 3, 1), dict(outermost_linear=True), 0),
+    ('B', (1, 256, 3, 1), dict(outermost_linear=True, first_omega_0=3000, hidden_omega_0=30.), 1),
+    ('C', (2, 256, 3, 3), dict(outermost_linear=False), 2)])
+def test_notebook_siren_init_matches_reference(g8, tag, args, kw, seed):
+    """The notebook Siren (explore_siren.ipynb cell 3) built under the same seed has bit-identical weights (same
+    RNG consumption: nn.Linear default init, then the SIREN uniform re-init), and the same state-dict keys."""
+    from siren_amd.modules import Siren
+    torch.manual_seed(seed)
+    s = Siren(*args, **kw)
+    sd = s.state_dict()
+    ref = {k[len(tag) + 3:]: v for k, v in g8.items() if k.startswith(tag + '_w_')}
+    assert list(sd.keys()) == list(ref.keys())
+    for k, v in sd.items():
+        assert np.array_equal(v.numpy(), ref[k]), k
