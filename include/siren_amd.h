@@ -231,6 +231,17 @@ int32_t siren_train_batched_ws_floats(const siren_cfg* cfg, int64_t n, int64_t b
 int32_t siren_backward_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
                                const float* gy, float* tws, float* gx, float* gparams, void* stream);
 
+/* Stored-forward W2 split over batched weights (SirenBatchedFunction's training forward under a hypernetwork): the
+ * forward keeps every element's a_l tiles and cos(w z_l), the backward (the hypernetwork's theta-gradients) is the
+ * reverse sweep only. Hidden 256 with elements below two CU rounds: ONE grouped launch per stage; otherwise the
+ * single-network entry points element by element. tws: siren_train_stored_batched_ws_floats(cfg, n, batch) floats,
+ * kept from the forward to the backward. */
+int32_t siren_train_stored_batched_ws_floats(const siren_cfg* cfg, int64_t n, int64_t batch, int64_t* count);
+int32_t siren_forward_store_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
+                                    float* y, float* tws, void* stream);
+int32_t siren_backward_stored_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
+                                      const float* gy, float* tws, float* gx, float* gparams, void* stream);
+
 /* ---- stored-forward W2 split (linear output; hidden 256: 1..3 hidden layers, hidden 512: 1..8) --------------
  * The training forward (model(model_input), training.py:72) keeps what the backward needs, so
  * train_loss.backward() (training.py:96) runs the L reverse GEMMs only instead of recomputing the forward:

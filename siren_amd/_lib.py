@@ -65,6 +65,9 @@ _SIGS = {
     'siren_adam_step': [_P, _P, _P, _P, _I64, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _I64,
                         ctypes.c_float, _P, _P],
     'siren_second_order_ex': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
+    'siren_train_stored_batched_ws_floats': [_CFG, _I64, _I64, ctypes.POINTER(_I64)],
+    'siren_forward_store_batched': [_CFG, _P, _P, _I64, _I64, _P, _P, _P],
+    'siren_backward_stored_batched': [_CFG, _P, _P, _I64, _I64, _P, _P, _P, _P, _P],
     'siren_hvp_backward_ws_floats': [_CFG, _I64, ctypes.POINTER(_I64)],
     'siren_hvp_backward': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     'siren_w1_phase_profile': [_CFG, _P, _P, _I64, _P, _P, _P, _P],

@@ -247,14 +247,21 @@ class SirenVJP(torch.autograd.Function):
 class SirenBatchedFunction(torch.autograd.Function):
     """y (B, n, d_out) = Phi(x_b; theta_b) for per-element weights theta (B, P) — BatchLinear with batched W
     (modules.py:16-25) under a HyperNetwork (meta_modules.py:41-53, 81-92). Forward: one grouped W0 launch over the
-    batch (siren_forward_batched). Backward: gx from one grouped W1 launch; theta-gradients (what flows back into the
-    hypernetwork) from the W2 pipeline per element (siren_backward_batched). Under create_graph each element
+    batch (siren_forward_batched); under a parameter-gradient graph the grouped stored forward (FWDS: a_l / cos kept,
+    siren_forward_store_batched). Backward: gx from one grouped W1 launch; theta-gradients (what flows back into the
+    hypernetwork) from the grouped reverse-only W2 (siren_backward_stored_batched), or the recompute W2
+    (siren_backward_batched) when nothing was stored. Under create_graph each element
     becomes a SirenVJP node (W1 forward, W3 backward) and theta-gradients recompute with device torch ops."""
 
     @staticmethod
-    def forward(ctx, engine, x, flat):
+    def forward(ctx, engine, x, flat, store=False):
         ws = engine.pack_batched(flat)
-        y = engine.forward_batched(ws, x)
+        ctx.tws = None
+        if store and engine.stored_supported and STORED_FORWARD:
+            # training under a hypernetwork: keep every element's a_l / cos, the backward is reverse-only
+            y, ctx.tws = engine.forward_store_batched(ws, x)
+        else:
+            y = engine.forward_batched(ws, x)
         ctx.engine, ctx.ws = engine, ws
         ctx.save_for_backward(x, flat)
         return y
@@ -269,16 +276,19 @@ class SirenBatchedFunction(torch.autograd.Function):
         gx = gp = None
         if not torch.is_grad_enabled():
             if need_p:
-                gx, gp = engine.backward_params_batched(ws, x, gy)
+                if ctx.tws is not None:
+                    gx, gp = engine.backward_stored_batched(ws, x, gy, ctx.tws)
+                else:
+                    gx, gp = engine.backward_params_batched(ws, x, gy)
             elif need_x:
                 _, gx = engine.forward_grad_batched(ws, x, gy, want_y=False)
-            return None, (gx if need_x else None), gp
+            return None, (gx if need_x else None), gp, None
         if need_x:
             gx = torch.stack([SirenVJP.apply(engine, ws[b], x[b], flat[b], gy[b]) for b in range(x.shape[0])])
         if need_p:
             gp = torch.stack([_torch_path.vjp_params(engine.cfg, x[b], flat[b], gy[b], create_graph=True)
                               for b in range(x.shape[0])])
-        return None, gx, gp
+        return None, gx, gp, None
 
 
 class SirenLaplace(torch.autograd.Function):

@@ -834,4 +834,93 @@ int32_t siren_backward_batched(const siren_cfg* cfg, const float* ws, const floa
     return SIREN_OK;
 }
 
+// ---- stored-forward W2 split over batched weights: the training forward (SirenBatchedFunction) keeps every
+// element's a_l tiles and cos, so the hypernetwork's backward is reverse-only. Grouped (hidden 256, elements below
+// ~2 CU rounds): [a tiles of every element][delta tiles][partial slabs][lane-major cos]; otherwise element b owns the
+// single-network layout at tws + b * siren_train_stored_ws_floats(cfg, n).
+int32_t siren_train_stored_batched_ws_floats(const siren_cfg* cfg, int64_t n, int64_t batch, int64_t* count) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (!stored_ok(cfg)) return fail(SIREN_EUNSUPPORTED, "the stored-forward W2 split needs a linear output layer");
+    if (count == nullptr || n < 0 || batch < 0) return fail(SIREN_EINVAL, "count is NULL or n / batch < 0");
+    if (grouped_w2(cfg, n)) {
+        const TrainPlan plan(cfg, n, batch);
+        *count = batch * (plan.total + plan.act_floats);
+        return SIREN_OK;
+    }
+    int64_t per = 0;
+    if (int rc = siren_train_stored_ws_floats(cfg, n, &per)) return rc;
+    *count = batch * per;
+    return SIREN_OK;
+}
+
+int32_t siren_forward_store_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
+                                    float* y, float* tws, void* stream) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (!stored_ok(cfg)) return fail(SIREN_EUNSUPPORTED, "the stored-forward W2 split needs a linear output layer");
+    if (n < 0 || batch < 0 || batch > 65535) return fail(SIREN_EINVAL, "need n >= 0 and 0 <= batch <= 65535");
+    if (n == 0 || batch == 0) return SIREN_OK;
+    if (ws == nullptr || x == nullptr || y == nullptr || tws == nullptr) return fail(SIREN_EINVAL, "ws/x/y/tws is NULL");
+    const int64_t W = ws_floats(cfg);
+    const int d = cfg->d_in, o = cfg->d_out;
+    if (grouped_w2(cfg, n)) {
+        const TrainPlan plan(cfg, n, batch);
+        float* abuf = tws;
+        float* cbuf = tws + 2 * batch * plan.act_floats + batch * plan.partial_floats;
+        siren::FusedArgs fa{w1_ws(cfg, ws), x, n, nullptr, y, nullptr, d, o, cfg->n_hidden, cfg->omega_first,
+                            cfg->omega_hidden, 0, abuf, cbuf, plan.n_pad, W};
+        siren::launch_w0s(dim3((unsigned)(plan.n_pad / siren::TILE), (unsigned)batch), (hipStream_t)stream, fa);
+        return hip_status("siren_forward_store_batched (grouped)");
+    }
+    int64_t per = 0;
+    if (int rc = siren_train_stored_ws_floats(cfg, n, &per)) return rc;
+    for (int64_t b = 0; b < batch; ++b)
+        if (int rc = siren_forward_store(cfg, ws + b * W, x + b * n * d, n, y + b * n * o, tws + b * per, stream))
+            return rc;
+    return SIREN_OK;
+}
+
+int32_t siren_backward_stored_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
+                                      const float* gy, float* tws, float* gx, float* gparams, void* stream) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (!stored_ok(cfg)) return fail(SIREN_EUNSUPPORTED, "the stored-forward W2 split needs a linear output layer");
+    if (n < 0 || batch < 0 || batch > 65535) return fail(SIREN_EINVAL, "need n >= 0 and 0 <= batch <= 65535");
+    if (batch > 0 && (ws == nullptr || gy == nullptr || gparams == nullptr || tws == nullptr || gx == nullptr ||
+                      (n > 0 && x == nullptr)))
+        return fail(SIREN_EINVAL, "ws/x/gy/tws/gx/gparams is NULL");
+    const int64_t W = ws_floats(cfg), P = param_count(cfg);
+    const int d = cfg->d_in, o = cfg->d_out;
+    if (batch > 0 && n > 0 && grouped_w2(cfg, n)) {
+        const TrainPlan plan(cfg, n, batch);
+        const hipStream_t st = (hipStream_t)stream;
+        const int64_t bact = plan.act_floats, bpart = plan.partial_floats;
+        float* abuf = tws;
+        float* dbuf = tws + batch * bact;
+        float* partial = tws + 2 * batch * bact;
+        float* cbuf = partial + batch * bpart;
+        siren::FusedArgs fa{w1_ws(cfg, ws), x, n, gy, nullptr, gx, d, o, cfg->n_hidden, cfg->omega_first,
+                            cfg->omega_hidden, 0, cbuf, dbuf, plan.n_pad, W};
+        const int64_t tiles = plan.n_pad / siren::TILE;
+        const int64_t per = std::max<int64_t>(1, ((int64_t)cu_count() + batch - 1) / batch);
+        siren::launch_w1(siren::MODE_REV, dim3((unsigned)std::min(tiles, per), (unsigned)batch), st, fa);
+        if (int rc = hip_status("siren_backward_stored_batched (grouped reverse)")) return rc;
+        siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden, (unsigned)batch), st, abuf, dbuf,
+                            plan.n_pad, plan.tps, partial, P, d, o, cfg->n_hidden, 1, cfg->hidden, 0, bact, bpart);
+        if (int rc = hip_status("siren_backward_stored_batched (grouped wgrad)")) return rc;
+        siren::launch_small(dim3((unsigned)plan.splits, (unsigned)batch), st, abuf, dbuf, x, gy, n, plan.n_pad,
+                            plan.tps, partial, P, d, o, cfg->n_hidden, cfg->hidden, bact, bpart);
+        if (int rc = hip_status("siren_backward_stored_batched (grouped small)")) return rc;
+        const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 1024);
+        siren::launch_reduce(dim3((unsigned)rblocks, (unsigned)batch), st, partial, plan.splits, P, gparams, 0, 0, 0,
+                             bpart);
+        return hip_status("siren_backward_stored_batched (grouped reduce)");
+    }
+    int64_t per = 0;
+    if (int rc = siren_train_stored_ws_floats(cfg, n, &per)) return rc;
+    for (int64_t b = 0; b < batch; ++b)
+        if (int rc = siren_backward_stored(cfg, ws + b * W, x + b * n * d, n, gy + b * n * o, tws + b * per,
+                                           gx + b * n * d, gparams + b * P, stream))
+            return rc;
+    return SIREN_OK;
+}
+
 }  // extern "C"

@@ -23,7 +23,7 @@ void launch_w0(dim3 grid, hipStream_t st, const FusedArgs& a) {
 void launch_w0s(dim3 grid, hipStream_t st, const FusedArgs& a) {
 #define SIREN_L(LHV)                                                                                             \
     hipLaunchKernelGGL((w1_kernel<LHV, MODE_FWDS>), grid, dim3(THREADS), 0, st, a.ws, a.x, a.n, (const float*)nullptr, \
-                       a.y, (float*)nullptr, a.d, a.o, a.w0, a.w, a.abuf, a.dbuf, a.n_pad, (int64_t)0)
+                       a.y, (float*)nullptr, a.d, a.o, a.w0, a.w, a.abuf, a.dbuf, a.n_pad, a.ws_bstride)
     switch (a.lh) {
         case 1: SIREN_L(1); break;
         case 2: SIREN_L(2); break;

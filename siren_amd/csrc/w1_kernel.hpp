@@ -444,8 +444,8 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
         if (y != nullptr) y += b * n * o;
         if (gx != nullptr) gx += b * n * d;
         if (gy != nullptr) gy += b * n * o;
-        if constexpr ((MODE & MODE_BASE) == MODE_STORE) {  // grouped W2: per-element a / delta tiles
-            abuf += b * (LH + 1) * n_pad * H;
+        if constexpr (STORE || FWDS || REV) {  // grouped W2: per-element a / delta tiles and lane-major cos
+            abuf += b * (LH + 1) * n_pad * H;    // (each (LH + 1) n_pad H floats)
             dbuf += b * (LH + 1) * n_pad * H;
         }
     }

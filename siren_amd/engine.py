@@ -319,6 +319,35 @@ class SirenEngine:
                    'siren_backward_batched')
         return gx, gp
 
+    def forward_store_batched(self, ws, x):
+        """Training forward over batched weights (stored-forward split): y (B, n, d_out) plus every element's a_l
+        tiles and cos(w z_l) in a workspace returned with y (siren_forward_store_batched)."""
+        self._require()
+        x = self._check_xb(x)
+        B, n = x.shape[:2]
+        cnt = ctypes.c_int64()
+        _lib.check(self.lib.siren_train_stored_batched_ws_floats(ctypes.byref(self.cfg), n, B, ctypes.byref(cnt)),
+                   'siren_train_stored_batched_ws_floats')
+        tws = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
+        y = torch.empty(B, n, self.cfg.d_out, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_forward_store_batched(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, B, _ptr(y),
+                                                        _ptr(tws), _stream(x.device)), 'siren_forward_store_batched')
+        return y, tws
+
+    def backward_stored_batched(self, ws, x, gy, tws):
+        """Reverse-only W2 over batched weights from forward_store_batched's workspace: (gx (B, n, d_in),
+        gparams (B, param_count))."""
+        self._require()
+        x = self._check_xb(x)
+        B, n = x.shape[:2]
+        gy = gy.contiguous()
+        gx = torch.empty_like(x)
+        gp = torch.empty(B, self.param_count, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_backward_stored_batched(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, B, _ptr(gy),
+                                                          _ptr(tws), _ptr(gx), _ptr(gp), _stream(x.device)),
+                   'siren_backward_stored_batched')
+        return gx, gp
+
     def forward_store(self, ws, x):
         """Training forward (stored-forward W2 split): y plus the a_l tiles and cos(w z_l) the reverse-only
         backward needs, kept in a workspace returned with y."""

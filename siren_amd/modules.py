@@ -205,7 +205,7 @@ def _fused_apply_batched(engine, coords, weights_biases):
         raise ValueError('coords batch %d does not match the weights batch %d' % (x.shape[0], B))
     if x is coords:
         x = coords.view(coords.shape)  # a non-leaf edge, as in _fused_apply
-    return SirenBatchedFunction.apply(engine, x, flat)
+    return SirenBatchedFunction.apply(engine, x, flat, torch.is_grad_enabled() and flat.requires_grad)
 
 
 # ----------------------------------------------------------------------------------------------------------

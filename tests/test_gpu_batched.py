@@ -99,3 +99,25 @@ def test_hypernetwork_end_to_end(cuda, g7):
     loss = ((out['model_out'] - torch.tensor(g7['gt_img'], device=cuda)) ** 2).mean()
     loss.backward()
     assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in hyper.parameters())
+
+
+@pytest.mark.parametrize('B,n,d,L,o,H', [(4, 4097, 2, 3, 1, 256), (3, 65, 3, 3, 1, 256), (2, 40000, 2, 3, 1, 256),
+                                         (32, 4096, 2, 3, 1, 256), (2, 700, 3, 3, 3, 512)])
+def test_stored_batched_split_matches_recompute(cuda, B, n, d, L, o, H):
+    """The hypernetwork training path: the grouped stored forward (FWDS) + reverse-only grouped W2 equals the
+    recompute W2 (grouped for small elements, element by element for large ones and hidden 512)."""
+    from siren_amd.engine import SirenEngine
+    eng = SirenEngine(d, H, L, o)
+    flat = torch.tensor(random_flat(B, d, L, o, H, seed=B + n), device=cuda)
+    x = torch.rand(B, n, d, device=cuda) * 2 - 1
+    gy = torch.randn(B, n, o, device=cuda)
+    wsb = eng.pack_batched(flat)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()  # fresh allocations: an element the grouped launch misses cannot pass on stale memory
+    ys, tws = eng.forward_store_batched(wsb, x)
+    yr = eng.forward_batched(wsb, x)
+    assert float((ys - yr).abs().max()) <= 2e-6 * max(1., float(yr.abs().max()))
+    gxs, gps = eng.backward_stored_batched(wsb, x, gy, tws)
+    gxr, gpr = eng.backward_params_batched(wsb, x, gy)
+    assert float((gxs - gxr).abs().max()) <= 1e-5 * float(gxr.abs().max())
+    assert float((gps - gpr).abs().max()) <= 1e-5 * float(gpr.abs().max())

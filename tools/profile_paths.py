@@ -11,7 +11,8 @@ Paths (BASELINE.json configs; F = 2 sum fan_in fan_out FLOP per coordinate, SURV
   poisson_ref  5x256 d2 o1, 512^2 grid: the reference recipe's kernels: W1 (J), d x W3 (H e_i), d x mixed jet
                (third-order adjoint); the same loss gradient as poisson (15F counted)
   w3_theta     5x256 d2 o1, 2^19 coords: W3 H v + theta-grads without a kept forward (6F)
-  hypernet     32 x 4096 coords, 5x256 d2 o1 per-element weights: grouped W2 backward (2F per coordinate)
+  hypernet     32 x 4096 coords, 5x256 d2 o1 per-element weights: grouped stored forward + grouped reverse-only W2
+               (the hypernetwork training kernels, W2 = 3F)
   w1           5x256 d2 o1, 2^20 coords: the headline W1 launch (2F)
 """
 import argparse
@@ -30,7 +31,7 @@ PATHS = {  # name: (d, hidden, layers, o, n, work units of F)
     'poisson': (2, 256, 3, 1, 512 * 512, 15),
     'poisson_ref': (2, 256, 3, 1, 512 * 512, 15),
     'w3_theta': (2, 256, 3, 1, 1 << 19, 6),
-    'hypernet': (2, 256, 3, 1, 32 * 4096, 2),
+    'hypernet': (2, 256, 3, 1, 32 * 4096, 3),
     'w1': (2, 256, 3, 1, 1 << 20, 2),
 }
 
@@ -54,7 +55,10 @@ def build_step(name, dev):
         wsb = eng.pack_batched(fb)
         xb = torch.rand(B, n // B, d, device=dev, generator=g) * 2 - 1
         gyb = torch.randn(B, n // B, o, device=dev, generator=g)
-        return lambda: eng.backward_params_batched(wsb, xb, gyb)
+        def step():
+            _, tws = eng.forward_store_batched(wsb, xb)
+            eng.backward_stored_batched(wsb, xb, gyb, tws)
+        return step
     ws = eng.pack(flat)
     if name.startswith('poisson'):
         from siren_amd import dataio
