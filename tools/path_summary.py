@@ -112,6 +112,22 @@ def summarise(rdir, path):
                'hbm_gbs': round((rd + wr) / t['avg_ns'], 1) if t['avg_ns'] > 0 else None,
                'hbm_frac': round((rd + wr) / t['avg_ns'] / HBM_GBS, 4) if t['avg_ns'] > 0 else None,
                'io_bytes_per_launch': io, 'traffic_over_io': round((rd + wr) / io, 3) if io else None}
+        if 'SQ_INSTS_MFMA' in c or 'SQ_WAVE_CYCLES' in c:
+            # SQ counters (MI355X_MICROARCH.md: SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* in quad-cycles,
+            # SQ_VALU_MFMA_BUSY_CYCLES in cycles summed over SIMDs; GRBM_GUI_ACTIVE summed over the 8 XCDs)
+            rec['sq'] = {kk: c[kk] for kk in sorted(c) if kk.startswith('SQ_') or kk.startswith('GRBM')}
+            mf = c.get('SQ_INSTS_MFMA', 0.)
+            if mf:
+                rec['valu_per_mfma'] = round(c.get('SQ_INSTS_VALU', 0.) / mf, 3)
+                rec['lds_per_mfma'] = round(c.get('SQ_INSTS_LDS', 0.) / mf, 3) if 'SQ_INSTS_LDS' in c else None
+            if c.get('GRBM_GUI_ACTIVE') and c.get('SQ_VALU_MFMA_BUSY_CYCLES'):
+                rec['mfma_busy_frac'] = round(c['SQ_VALU_MFMA_BUSY_CYCLES'] / 1024 / (c['GRBM_GUI_ACTIVE'] / 8), 4)
+            if c.get('SQ_WAVE_CYCLES'):
+                rec['wait_inst_any_frac'] = round(c.get('SQ_WAIT_INST_ANY', 0.) / c['SQ_WAVE_CYCLES'], 4)
+                rec['wait_any_frac'] = round(c.get('SQ_WAIT_ANY', 0.) / c['SQ_WAVE_CYCLES'], 4)
+                rec['active_inst_any_frac'] = round(c.get('SQ_ACTIVE_INST_ANY', 0.) / c['SQ_WAVE_CYCLES'], 4)
+            if c.get('SQ_INSTS_LDS'):
+                rec['lds_bank_conflict_per_lds_inst'] = round(c.get('SQ_LDS_BANK_CONFLICT', 0.) / c['SQ_INSTS_LDS'], 4)
         kernels[k] = rec
         tot_ns += t['avg_ns'] * per_step
         tot_bytes += (rd + wr) * per_step
