@@ -18,9 +18,9 @@ for p in $PATHS_TO_RUN; do
   cat $O/$p/timing.json
   timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$p/trace -o run -- python3 $R/tools/profile_paths.py $p > $O/$p/trace.log 2>&1 || { echo "trace $p failed"; tail -5 $O/$p/trace.log; exit 1; }
   i=0
-  GROUPS="FETCH_SIZE WRITE_SIZE"
-  if [ -n "$SQ_PASSES" ]; then GROUPS="$GROUPS SQA SQB SQC"; fi
-  for grp in $GROUPS; do
+  PASSLIST="FETCH_SIZE WRITE_SIZE"
+  if [ -n "$SQ_PASSES" ]; then PASSLIST="$PASSLIST SQA SQB SQC"; fi
+  for grp in $PASSLIST; do
     case $grp in
       SQA) grp="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE";;
       SQB) grp="SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU";;
