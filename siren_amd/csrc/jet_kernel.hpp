@@ -29,6 +29,7 @@
 // reverse gives every cotangent of the node at once:
 //   gx = W0^T zb_0,value   gv = W0^T zb_0,v   gu_j = D2 y_j[v, g] (the forward's last jet)   dtheta as for W4s
 // with the first layer's tangents W0 v / W0 g (per coordinate) and the output seed sum_j u_j Wout_j.
+#include "lds_ops.h"
 #include "ring.hpp"
 #include "siren_common.h"
 #include "siren_params.h"
@@ -150,18 +151,7 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
         for (int kb2 = 0; kb2 < NB; ++kb2) {
             ring_wait(s, nslices);
             ring_issue(stream, ring, s + 2, nslices, wave, lane);
-            const float* sl = ring + (s % NBUF) * SLICE + lane * 4;
-            const f32x4 bop = act[kb2];
-#pragma unroll
-            for (int ob = 0; ob < NB; ob += 2) {
-                const f32x4 a0 = *(const f32x4*)(sl + ob * 256);
-                const f32x4 a1 = *(const f32x4*)(sl + (ob + 1) * 256);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    acc[ob] = mfma4(a0[r], bop[r], acc[ob]);
-                    acc[ob + 1] = mfma4(a1[r], bop[r], acc[ob + 1]);
-                }
-            }
+            slice_mma<NB>(lds_addr(ring + (s % NBUF) * SLICE) + 16u * lane, act[kb2], acc);  // lds_ops.h
             ++s;
         }
         if (p < lh) {

@@ -34,6 +34,7 @@
 #pragma once
 #include <type_traits>
 
+#include "lds_ops.h"
 #include "siren_common.h"
 
 namespace siren {
@@ -78,19 +79,6 @@ __device__ __forceinline__ f32x4 from_agpr(f32x4 v) {
 __device__ __forceinline__ f32x4 pin(f32x4 v) {
     asm("; pin" : "+v"(v));
     return v;
-}
-
-// ds_read_b128 at a compile-time byte offset from a VGPR base (not visible to hipcc's waitcnt insertion).
-template <int OFF>
-__device__ __forceinline__ f32x4 lds_read4(unsigned vaddr) {
-    static_assert(OFF >= 0 && OFF < 65536, "ds offset field is 16 bits");
-    f32x4 r;
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(vaddr), "i"(OFF));
-    return r;
-}
-template <int N>
-__device__ __forceinline__ void lgkm_wait(f32x4& a, f32x4& b) {
-    asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N));
 }
 
 template <int MODE>

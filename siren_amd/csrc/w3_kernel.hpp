@@ -28,28 +28,12 @@
 // cos(w z_l) (lane-major, kC) of every layer come from the forward's workspace, so the hidden layers run the
 // tangent GEMMs only (half the forward MFMAs), only zdot is spilled, and kA doubles as the THETA A buffer.
 #pragma once
+#include "lds_ops.h"
 #include "ring.hpp"
 #include "siren_common.h"
 #include "siren_params.h"
 
 namespace siren {
-
-// A-operand pass over one slice for the primal (bp) and tangent (bt) column tiles.
-__device__ __forceinline__ void slice_mma2(const float* sl, const f32x4& bp, const f32x4& bt, f32x4 (&accp)[NB],
-                                           f32x4 (&acct)[NB]) {
-    f32x4 a = *(const f32x4*)(sl);
-#pragma unroll
-    for (int ob = 0; ob < NB; ++ob) {
-        f32x4 nx;
-        if (ob + 1 < NB) nx = *(const f32x4*)(sl + (ob + 1) * 256);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            accp[ob] = mfma4(a[r], bp[r], accp[ob]);
-            acct[ob] = mfma4(a[r], bt[r], acct[ob]);
-        }
-        if (ob + 1 < NB) a = nx;
-    }
-}
 
 __device__ __forceinline__ void layer_mma2(const float* __restrict__ stream, float* ring, int& s, int nslices,
                                            int wave, int lane, const f32x4 (&bp)[NB], const f32x4 (&bt)[NB],
@@ -63,7 +47,7 @@ __device__ __forceinline__ void layer_mma2(const float* __restrict__ stream, flo
     for (int kb = 0; kb < NB; ++kb) {
         ring_wait(s, nslices);
         ring_issue(stream, ring, s + 2, nslices, wave, lane);
-        slice_mma2(ring + (s % NBUF) * SLICE + lane * 4, bp[kb], bt[kb], accp, acct);
+        slice_mma2<NB>(lds_addr(ring + (s % NBUF) * SLICE) + 16u * lane, bp[kb], bt[kb], accp, acct);  // lds_ops.h
         ++s;
     }
 }
@@ -77,25 +61,7 @@ __device__ __forceinline__ void layer_mma1(const float* __restrict__ stream, flo
     for (int kb = 0; kb < NB; ++kb) {
         ring_wait(s, nslices);
         ring_issue(stream, ring, s + 2, nslices, wave, lane);
-        const float* sl = ring + (s % NBUF) * SLICE + lane * 4;
-        f32x4 a0 = *(const f32x4*)(sl), a1 = *(const f32x4*)(sl + 256);
-#pragma unroll
-        for (int ob = 0; ob < NB; ob += 2) {
-            f32x4 n0, n1;
-            if (ob + 2 < NB) {
-                n0 = *(const f32x4*)(sl + (ob + 2) * 256);
-                n1 = *(const f32x4*)(sl + (ob + 3) * 256);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                acct[ob] = mfma4(a0[r], bt[kb][r], acct[ob]);
-                acct[ob + 1] = mfma4(a1[r], bt[kb][r], acct[ob + 1]);
-            }
-            if (ob + 2 < NB) {
-                a0 = n0;
-                a1 = n1;
-            }
-        }
+        slice_mma<NB>(lds_addr(ring + (s % NBUF) * SLICE) + 16u * lane, bt[kb], acct);  // lds_ops.h
         ++s;
     }
 }

@@ -19,6 +19,7 @@
 // wgrad_kernel / small_kernel read with h = 512). Stored-forward W2 split: MODE_FWDS = the forward passes with
 // a_l tiles to abuf and cos(w z_l) of layers 0..L (L + 1 scratch layers) to the scratch; MODE_REV = the seed from
 // the stored cos(w z_L) and the L reverse passes only, delta_l tiles to dbuf.
+#include "lds_ops.h"
 #include "siren_common.h"
 #include "siren_params.h"
 
@@ -50,29 +51,6 @@ __device__ __forceinline__ void wring_wait(int s, int nslices) {
     else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-}
-
-// acc[ob] += W-slice(ob) x B, 128 MFMAs; pairs of output blocks so consecutive MFMAs never chain
-__device__ __forceinline__ void wslice_mma(const float* sl, const f32x4& bop, f32x4 (&acc)[WNB]) {
-    f32x4 a0 = *(const f32x4*)(sl);
-    f32x4 a1 = *(const f32x4*)(sl + 256);
-#pragma unroll
-    for (int ob = 0; ob < WNB; ob += 2) {
-        f32x4 n0, n1;
-        if (ob + 2 < WNB) {
-            n0 = *(const f32x4*)(sl + (ob + 2) * 256);
-            n1 = *(const f32x4*)(sl + (ob + 3) * 256);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            acc[ob] = mfma4(a0[r], bop[r], acc[ob]);
-            acc[ob + 1] = mfma4(a1[r], bop[r], acc[ob + 1]);
-        }
-        if (ob + 2 < WNB) {
-            a0 = n0;
-            a1 = n1;
-        }
-    }
 }
 
 // STORE-mode tile writer; the pointer is stepped through an opaque register so the compiler cannot hoist 32
@@ -169,11 +147,18 @@ __global__ __launch_bounds__(THREADS, 1) void wide_kernel(
     for (int p = p0; p < npass; ++p) {
 #pragma unroll
         for (int ob = 0; ob < WNB; ++ob) acc[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // reverse passes: cos(w z_lm) block kb of the epilogue is loaded into act[kb] as soon as slice kb has
+        // consumed it (the B operand is dead after its slice), so the epilogue's 32 scratch loads are in flight
+        // under the remaining slices instead of exposed after the GEMM. The ring's vmcnt(8) stays correct (it
+        // only waits for more).
+        const bool rev_pass = GRAD && p >= lh;
+        const float* cpre = rev_pass ? sp + (int64_t)(2 * lh - p - 1) * lstride : sp;
 #pragma unroll
         for (int kb = 0; kb < WNB; ++kb) {
             wring_wait(s, nslices);
             wring_issue(stream, ring, s + 2, nslices, wave, lane);
-            wslice_mma(ring + (s % WNBUF) * WSLICE + lane * 4, act[kb], acc);
+            slice_mma<WNB>(lds_addr(ring + (s % WNBUF) * WSLICE) + 16u * lane, act[kb], acc);  // lds_ops.h
+            if (rev_pass) act[kb] = *(const f32x4*)(cpre + kb * 256);
             ++s;
         }
         if (p < lh - 1) {
@@ -258,9 +243,8 @@ __global__ __launch_bounds__(THREADS, 1) void wide_kernel(
             // reverse pass through W_l (l = 2L - p): delta_{l-1} = (delta_l W_l) . cos(w z_{l-1}) . w_{l-1}
             const int lm = 2 * lh - p - 1;
             const float wl = lm == 0 ? w0 : w;
-            const float* cp = sp + (int64_t)lm * lstride;
 #pragma unroll
-            for (int rb = 0; rb < WNB; ++rb) act[rb] = (acc[rb] * *(const f32x4*)(cp + rb * 256)) * wl;
+            for (int rb = 0; rb < WNB; ++rb) act[rb] = (acc[rb] * act[rb]) * wl;  // act = the prefetched cos
             if (DSTORE) wstore_tile(dbuf + (int64_t)lm * lstride + toff, act);
         }
     }
