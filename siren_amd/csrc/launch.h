@@ -42,14 +42,14 @@ void launch_jet_phase(int phase, dim3 grid, hipStream_t st, const float* ws, con
                       const float* glap, float* gx, int d, int o, int lh, float w0, float w, float* spill, float* abuf,
                       float* dbuf, int64_t n_pad, float* y, float* lap);
 void launch_small_jet(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x,
-                      const float* glap, int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d,
+                      const float* glap, int64_t n, int64_t n_pad, int64_t tps, float* eslab, int64_t E, int d,
                       int o, int lh);
 // tu_jet.hip: the third-order adjoint (mixed jet along per-coordinate tangents v, g; output weighting u nullable)
 void launch_jet_mix(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* v,
                     const float* g, const float* u, float* gx, float* gv, float* gu, int d, int o, int lh, float w0,
                     float w, float* spill, float* abuf, float* dbuf, int64_t n_pad);
 void launch_small_mix(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* v,
-                      const float* g, const float* u, int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P,
+                      const float* g, const float* u, int64_t n, int64_t n_pad, int64_t tps, float* eslab, int64_t E,
                       int d, int o, int lh);
 // tu_wide.hip: hidden width 512 (mode as siren_common.h MODE_*); spill = cos scratch for MODE_W1 / MODE_STORE
 void launch_wide(int mode, dim3 grid, hipStream_t st, const FusedArgs& a, float* spill);
@@ -60,17 +60,21 @@ void launch_w3(bool theta, dim3 grid, hipStream_t st, const float* ws, const flo
                const float* kC = nullptr);
 void launch_small_w3(dim3 grid, hipStream_t st, const float* At, const float* D, const float* Dt, const float* AL,
                      const float* x, const float* v, const float* gy, const float* u, int64_t n, int64_t n_pad, int64_t tps,
-                     float* partial, int64_t P, int d, int o, int lh);
+                     float* eslab, int64_t E, int d, int o, int lh);
 // tu_train.hip
 // bstride_act / bstride_part: grouped W2 over batched weights (grid.z of wgrad, grid.y of small / reduce = element)
 void launch_wgrad(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, int64_t n_pad, int64_t tps,
                   float* partial, int64_t P, int d, int o, int lh, int with_bias, int h, int jet_bias = 0,
                   int64_t bstride_act = 0, int64_t bstride_part = 0);
+// edge-layer launchers (launch_small*): grid (edge splits, hidden / 256, batch), tps = the edge split's tiles,
+// eslab / E = the compact edge slabs (siren_capi.hip EdgeSplit), bstride_e = their stride between batch elements
 void launch_small(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* gy,
-                  int64_t n, int64_t n_pad, int64_t tps, float* partial, int64_t P, int d, int o, int lh, int h,
-                  int64_t bstride_act = 0, int64_t bstride_part = 0);
+                  int64_t n, int64_t n_pad, int64_t tps, float* eslab, int64_t E, int d, int o, int lh, int h,
+                  int64_t bstride_act = 0, int64_t bstride_e = 0);
 void launch_reduce(dim3 grid, hipStream_t st, const float* partial, int64_t S, int64_t P, float* gp, int64_t S2,
-                   int64_t lo, int64_t hi, int64_t bstride_part = 0);
+                   int64_t lo, int64_t hi, int64_t bstride_part = 0, int64_t begin = 0, int64_t end = -1);
+void launch_edge_reduce(dim3 grid, hipStream_t st, const float* eslab, int64_t SE, int64_t E, int64_t hidden0,
+                        int64_t wout, float* gp, int64_t P, int64_t bstride_e);
 
 constexpr int STEP_BLOCKS = 1024;  // partial sums of the clip-norm pass (4 workgroups per CU)
 // tu_step.hip: device point-cloud sampling (dataio.py:420-442), clip_grad_norm_ + Adam over the flat bucket

@@ -103,14 +103,38 @@ int64_t wgrad_splits(const siren_cfg* cfg) {
     return s > 0 ? s : 1;
 }
 
+// Edge-layer split (edge_kernel): the first / output layers' gradients reduce the coordinate tiles over their own,
+// finer split into compact slabs [W0 | b0 | Wout | bout] (E floats each), about two CU rounds of workgroups over
+// (split, 256-neuron block, element); edge_reduce_kernel sums them into the parameter order. (Tied to the wgrad
+// split, hidden 512 ran 42 workgroups at 1.6 TB/s.)
+struct EdgeSplit {
+    int64_t splits, tps, E, floats;
+    EdgeSplit(const siren_cfg* cfg, int64_t ntiles, int64_t batch = 1) {
+        const int64_t hb = std::max(1, cfg->hidden / 256);
+        const int64_t want = std::max<int64_t>(1, 512 / hb / std::max<int64_t>(1, batch));
+        splits = std::max<int64_t>(1, std::min(ntiles, want));
+        tps = std::max<int64_t>(1, (ntiles + splits - 1) / splits);
+        splits = std::max<int64_t>(1, (ntiles + tps - 1) / tps);
+        const siren::ParamOffsets off(cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden);
+        E = off.hidden0 + (int64_t)cfg->d_out * (cfg->hidden + 1);
+        floats = splits * E;
+    }
+    dim3 grid(const siren_cfg* cfg, int64_t batch = 1) const {
+        return dim3((unsigned)splits, (unsigned)std::max(1, cfg->hidden / 256), (unsigned)batch);
+    }
+};
+
 // W2 backward workspace: sin activations and deltas of every sine layer in 16-coordinate tiles, S
-// param-shaped partial slabs of the split-K weight-gradient reduction and, for hidden 512, the cos scratch
-// of the wide kernel (layers 0..L-1).
+// param-shaped partial slabs of the split-K weight-gradient reduction (+ the edge slabs) and, for hidden 512, the cos
+// scratch of the wide kernel (layers 0..L-1).
 struct TrainPlan {
     int64_t n_pad, tiles, splits, tps, act_floats, partial_floats, spill_floats, total;
+    int64_t eslab_off;  // edge slabs at partial + eslab_off
+    EdgeSplit es;
     // batch > 1: a grouped W2 over that many elements shares the CU rounds (fewer splits per element, so the
     // per-split slabs stay a small fraction of the traffic)
-    TrainPlan(const siren_cfg* cfg, int64_t n, int64_t batch = 1) {
+    TrainPlan(const siren_cfg* cfg, int64_t n, int64_t batch = 1, int64_t slab_sets = 1)
+        : es(cfg, (n + siren::TILE - 1) / siren::TILE * siren::TILE / 16, batch) {
         n_pad = (n + siren::TILE - 1) / siren::TILE * siren::TILE;
         tiles = n_pad / 16;
         const int64_t want = std::max<int64_t>(1, wgrad_splits(cfg) / std::max<int64_t>(1, batch));
@@ -120,11 +144,26 @@ struct TrainPlan {
         splits = std::max<int64_t>(1, (tiles + tps - 1) / tps);
         if (splits < 1) splits = 1;
         act_floats = (int64_t)(cfg->n_hidden + 1) * n_pad * cfg->hidden;
-        partial_floats = splits * param_count(cfg);
+        eslab_off = slab_sets * splits * param_count(cfg);
+        partial_floats = eslab_off + es.floats;
         spill_floats = wide(cfg) ? (int64_t)cfg->n_hidden * n_pad * cfg->hidden : 0;
         total = 2 * act_floats + partial_floats + spill_floats;
     }
 };
+// hidden layers: the split-K slabs (S, + S2 for W3's second set); edge layers: the compact edge slabs
+int finish_grads(const siren_cfg* cfg, hipStream_t st, const float* partial, int64_t S, int64_t S2, const float* eslab,
+                 const EdgeSplit& es, float* gparams, const char* what, int64_t batch = 1, int64_t bpart = 0) {
+    const siren::ParamOffsets off(cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden);
+    const int64_t P = param_count(cfg);
+    const int64_t cap = batch > 1 ? 1024 : 4096;
+    const int64_t rblocks = std::max<int64_t>(1, std::min<int64_t>((off.wout - off.hidden0 + 255) / 256, cap));
+    siren::launch_reduce(dim3((unsigned)rblocks, (unsigned)batch), st, partial, S, P, gparams, S2, off.hidden0,
+                         off.wout, bpart, off.hidden0, off.wout);
+    const int64_t eblocks = std::max<int64_t>(1, std::min<int64_t>((es.E + 255) / 256, 1024));
+    siren::launch_edge_reduce(dim3((unsigned)eblocks, (unsigned)batch), st, eslab, es.splits, es.E, off.hidden0,
+                              off.wout, gparams, P, bpart);
+    return hip_status(what);
+}
 }  // namespace
 
 extern "C" {
@@ -289,12 +328,11 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
     siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden, quads), st, abuf, dbuf, plan.n_pad,
                         plan.tps, partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1, cfg->hidden);
     if (int rc = hip_status("siren_backward (wgrad)")) return rc;
-    siren::launch_small(dim3((unsigned)plan.splits), st, abuf, dbuf, x, gy, n, plan.n_pad, plan.tps, partial, P,
-                        cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden);
+    siren::launch_small(plan.es.grid(cfg), st, abuf, dbuf, x, gy, n, plan.n_pad, plan.es.tps, partial + plan.eslab_off,
+                        plan.es.E, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden);
     if (int rc = hip_status("siren_backward (small)")) return rc;
-    const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 4096);
-    siren::launch_reduce(dim3((unsigned)rblocks), st, partial, plan.splits, P, gparams, 0, 0, 0);
-    return hip_status("siren_backward (reduce)");
+    return finish_grads(cfg, st, partial, plan.splits, 0, partial + plan.eslab_off, plan.es, gparams,
+                        "siren_backward (reduce)");
 }
 
 // ---- stored-forward W2 split: the training forward keeps a_l and cos(w z_l) so the backward is reverse-only ----
@@ -379,12 +417,11 @@ int32_t siren_backward_stored(const siren_cfg* cfg, const float* ws, const float
     siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden, quads), st, abuf, dbuf, plan.n_pad,
                         plan.tps, partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1, cfg->hidden);
     if (int rc = hip_status("siren_backward_stored (wgrad)")) return rc;
-    siren::launch_small(dim3((unsigned)plan.splits), st, abuf, dbuf, x, gy, n, plan.n_pad, plan.tps, partial, P,
-                        cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden);
+    siren::launch_small(plan.es.grid(cfg), st, abuf, dbuf, x, gy, n, plan.n_pad, plan.es.tps, partial + plan.eslab_off,
+                        plan.es.E, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden);
     if (int rc = hip_status("siren_backward_stored (small)")) return rc;
-    const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 4096);
-    siren::launch_reduce(dim3((unsigned)rblocks), st, partial, plan.splits, P, gparams, 0, 0, 0);
-    return hip_status("siren_backward_stored (reduce)");
+    return finish_grads(cfg, st, partial, plan.splits, 0, partial + plan.eslab_off, plan.es, gparams,
+                        "siren_backward_stored (reduce)");
 }
 
 // ---- W4s: backward of the fused Laplacian (laplace_mse training) ------------------------------------------
@@ -399,8 +436,9 @@ int check_jet(const siren_cfg* cfg) {
 
 // jet tiles are 16 columns = 4 coordinates x 4 streams: a-jets, zb-jets and z-jets of every layer + S slabs
 struct JetPlan {
-    int64_t n_pad, cols, tiles, splits, tps, buf_floats, partial_floats, total;
-    JetPlan(const siren_cfg* cfg, int64_t n) {
+    int64_t n_pad, cols, tiles, splits, tps, buf_floats, partial_floats, total, eslab_off;
+    EdgeSplit es;
+    JetPlan(const siren_cfg* cfg, int64_t n) : es(cfg, (n + 15) / 16 * 16 / 4) {
         n_pad = (n + 15) / 16 * 16;
         cols = 4 * n_pad;
         tiles = cols / 16;
@@ -411,7 +449,8 @@ struct JetPlan {
         splits = std::max<int64_t>(1, (tiles + tps - 1) / tps);
         if (splits < 1) splits = 1;
         buf_floats = (int64_t)(cfg->n_hidden + 1) * cols * siren::H;
-        partial_floats = splits * param_count(cfg);
+        eslab_off = splits * param_count(cfg);
+        partial_floats = eslab_off + es.floats;
         total = 3 * buf_floats + partial_floats;
     }
 };
@@ -448,12 +487,11 @@ int32_t siren_laplace_backward(const siren_cfg* cfg, const float* ws, const floa
     siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden), st, abuf, dbuf, plan.cols, plan.tps,
                         partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1, siren::H, 1);
     if (int rc = hip_status("siren_laplace_backward (wgrad)")) return rc;
-    siren::launch_small_jet(dim3((unsigned)plan.splits), st, abuf, dbuf, x, glap, n, plan.n_pad, plan.tps, partial,
-                            P, cfg->d_in, cfg->d_out, cfg->n_hidden);
+    siren::launch_small_jet(plan.es.grid(cfg), st, abuf, dbuf, x, glap, n, plan.n_pad, plan.es.tps,
+                            partial + plan.eslab_off, plan.es.E, cfg->d_in, cfg->d_out, cfg->n_hidden);
     if (int rc = hip_status("siren_laplace_backward (small)")) return rc;
-    const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 4096);
-    siren::launch_reduce(dim3((unsigned)rblocks), st, partial, plan.splits, P, gparams, 0, 0, 0);
-    return hip_status("siren_laplace_backward (reduce)");
+    return finish_grads(cfg, st, partial, plan.splits, 0, partial + plan.eslab_off, plan.es, gparams,
+                        "siren_laplace_backward (reduce)");
 }
 
 // ---- split W4 / W4s for laplace_mse training: the forward jet keeps its stores, the backward is reverse-only ----
@@ -498,12 +536,11 @@ int32_t siren_laplace_backward_stored(const siren_cfg* cfg, const float* ws, con
     siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden), st, abuf, dbuf, plan.cols, plan.tps,
                         partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1, siren::H, 1);
     if (int rc = hip_status("siren_laplace_backward_stored (wgrad)")) return rc;
-    siren::launch_small_jet(dim3((unsigned)plan.splits), st, abuf, dbuf, x, glap, n, plan.n_pad, plan.tps, partial,
-                            P, cfg->d_in, cfg->d_out, cfg->n_hidden);
+    siren::launch_small_jet(plan.es.grid(cfg), st, abuf, dbuf, x, glap, n, plan.n_pad, plan.es.tps,
+                            partial + plan.eslab_off, plan.es.E, cfg->d_in, cfg->d_out, cfg->n_hidden);
     if (int rc = hip_status("siren_laplace_backward_stored (small)")) return rc;
-    const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 4096);
-    siren::launch_reduce(dim3((unsigned)rblocks), st, partial, plan.splits, P, gparams, 0, 0, 0);
-    return hip_status("siren_laplace_backward_stored (reduce)");
+    return finish_grads(cfg, st, partial, plan.splits, 0, partial + plan.eslab_off, plan.es, gparams,
+                        "siren_laplace_backward_stored (reduce)");
 }
 
 // ---- third-order adjoint: the backward of a Hessian-vector-product node (jet_kernel.hpp MIX) -----------------
@@ -548,19 +585,19 @@ int32_t siren_hvp_backward(const siren_cfg* cfg, const float* ws, const float* x
     siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden), st, abuf, dbuf, plan.cols, plan.tps,
                         partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1, siren::H, 1);
     if (int rc = hip_status("siren_hvp_backward (wgrad)")) return rc;
-    siren::launch_small_mix(dim3((unsigned)plan.splits), st, abuf, dbuf, x, v, g, u, n, plan.n_pad, plan.tps, partial,
-                            P, cfg->d_in, cfg->d_out, cfg->n_hidden);
+    siren::launch_small_mix(plan.es.grid(cfg), st, abuf, dbuf, x, v, g, u, n, plan.n_pad, plan.es.tps,
+                            partial + plan.eslab_off, plan.es.E, cfg->d_in, cfg->d_out, cfg->n_hidden);
     if (int rc = hip_status("siren_hvp_backward (small)")) return rc;
-    const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 4096);
-    siren::launch_reduce(dim3((unsigned)rblocks), st, partial, plan.splits, P, gparams, 0, 0, 0);
-    return hip_status("siren_hvp_backward (reduce)");
+    return finish_grads(cfg, st, partial, plan.splits, 0, partial + plan.eslab_off, plan.es, gparams,
+                        "siren_hvp_backward (reduce)");
 }
 
 // ---- W3: second-order adjoint (Hessian-vector product + mixed theta gradient), d_out == 1 ---------------
 namespace {
 struct W3Plan {
-    int64_t n_pad, tiles, splits, tps, spill_floats, buf_floats, partial_floats, total;
-    W3Plan(const siren_cfg* cfg, int64_t n, bool theta) {
+    int64_t n_pad, tiles, splits, tps, spill_floats, buf_floats, partial_floats, total, eslab_off;
+    EdgeSplit es;
+    W3Plan(const siren_cfg* cfg, int64_t n, bool theta) : es(cfg, (n + siren::TILE - 1) / siren::TILE * siren::TILE / 16) {
         const TrainPlan tp(cfg, n);
         n_pad = tp.n_pad;
         tiles = tp.tiles;
@@ -568,7 +605,8 @@ struct W3Plan {
         tps = tp.tps;
         spill_floats = n_pad * (int64_t)(cfg->n_hidden + 1) * 3 * siren::H;
         buf_floats = theta ? (int64_t)(cfg->n_hidden + 1) * n_pad * siren::H : 0;
-        partial_floats = theta ? 2 * splits * param_count(cfg) : 0;
+        eslab_off = 2 * splits * param_count(cfg);
+        partial_floats = theta ? eslab_off + es.floats : 0;
         total = spill_floats + 4 * buf_floats + partial_floats;
     }
 };
@@ -636,14 +674,11 @@ static int32_t second_order_impl(const siren_cfg* cfg, const float* ws, const fl
                         cfg->n_hidden, 0, siren::H);
     if (int rc = hip_status("siren_second_order (wgrad)")) return rc;
     const float* a_last = A + (int64_t)cfg->n_hidden * plan.n_pad * siren::H;  // a_L rows (first-order seed)
-    siren::launch_small_w3(dim3((unsigned)plan.splits), st, At, D, Dt, a_last, x, v, gy, u, n, plan.n_pad, plan.tps,
-                           partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden);
+    siren::launch_small_w3(plan.es.grid(cfg), st, At, D, Dt, a_last, x, v, gy, u, n, plan.n_pad, plan.es.tps,
+                           partial + plan.eslab_off, plan.es.E, cfg->d_in, cfg->d_out, cfg->n_hidden);
     if (int rc = hip_status("siren_second_order (small)")) return rc;
-    const siren::ParamOffsets off(cfg->d_in, cfg->d_out, cfg->n_hidden);
-    const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 4096);
-    siren::launch_reduce(dim3((unsigned)rblocks), st, partial, plan.splits, P, gparams, plan.splits, off.hidden0,
-                         off.wout);
-    return hip_status("siren_second_order (reduce)");
+    return finish_grads(cfg, st, partial, plan.splits, plan.splits, partial + plan.eslab_off, plan.es, gparams,
+                        "siren_second_order (reduce)");
 }
 
 int32_t siren_second_order_ex(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
@@ -819,13 +854,11 @@ int32_t siren_backward_batched(const siren_cfg* cfg, const float* ws, const floa
         siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden, (unsigned)batch), st, abuf, dbuf,
                             plan.n_pad, plan.tps, partial, P, d, o, cfg->n_hidden, 1, cfg->hidden, 0, bact, bpart);
         if (int rc = hip_status("siren_backward_batched (grouped wgrad)")) return rc;
-        siren::launch_small(dim3((unsigned)plan.splits, (unsigned)batch), st, abuf, dbuf, x, gy, n, plan.n_pad,
-                            plan.tps, partial, P, d, o, cfg->n_hidden, cfg->hidden, bact, bpart);
+        siren::launch_small(plan.es.grid(cfg, batch), st, abuf, dbuf, x, gy, n, plan.n_pad, plan.es.tps,
+                            partial + plan.eslab_off, plan.es.E, d, o, cfg->n_hidden, cfg->hidden, bact, bpart);
         if (int rc = hip_status("siren_backward_batched (grouped small)")) return rc;
-        const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 1024);
-        siren::launch_reduce(dim3((unsigned)rblocks, (unsigned)batch), st, partial, plan.splits, P, gparams, 0, 0, 0,
-                             bpart);
-        return hip_status("siren_backward_batched (grouped reduce)");
+        return finish_grads(cfg, st, partial, plan.splits, 0, partial + plan.eslab_off, plan.es, gparams,
+                            "siren_backward_batched (grouped reduce)", batch, bpart);
     }
     for (int64_t b = 0; b < batch; ++b)
         if (int rc = siren_backward(cfg, ws + b * W, x + b * n * d, n, gy + b * n * o, tws, nullptr,
@@ -906,13 +939,11 @@ int32_t siren_backward_stored_batched(const siren_cfg* cfg, const float* ws, con
         siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden, (unsigned)batch), st, abuf, dbuf,
                             plan.n_pad, plan.tps, partial, P, d, o, cfg->n_hidden, 1, cfg->hidden, 0, bact, bpart);
         if (int rc = hip_status("siren_backward_stored_batched (grouped wgrad)")) return rc;
-        siren::launch_small(dim3((unsigned)plan.splits, (unsigned)batch), st, abuf, dbuf, x, gy, n, plan.n_pad,
-                            plan.tps, partial, P, d, o, cfg->n_hidden, cfg->hidden, bact, bpart);
+        siren::launch_small(plan.es.grid(cfg, batch), st, abuf, dbuf, x, gy, n, plan.n_pad, plan.es.tps,
+                            partial + plan.eslab_off, plan.es.E, d, o, cfg->n_hidden, cfg->hidden, bact, bpart);
         if (int rc = hip_status("siren_backward_stored_batched (grouped small)")) return rc;
-        const int64_t rblocks = std::min<int64_t>((P + 255) / 256, 1024);
-        siren::launch_reduce(dim3((unsigned)rblocks, (unsigned)batch), st, partial, plan.splits, P, gparams, 0, 0, 0,
-                             bpart);
-        return hip_status("siren_backward_stored_batched (grouped reduce)");
+        return finish_grads(cfg, st, partial, plan.splits, 0, partial + plan.eslab_off, plan.es, gparams,
+                            "siren_backward_stored_batched (grouped reduce)", batch, bpart);
     }
     int64_t per = 0;
     if (int rc = siren_train_stored_ws_floats(cfg, n, &per)) return rc;

@@ -130,47 +130,73 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
 //             db0 = sum zb_0,value, dWout_j = sum u_j a_L,second, dbout = 0
 enum { EDGE_W2 = 0, EDGE_W3 = 1, EDGE_JET = 2, EDGE_MIX = 3 };
 constexpr int EDGE_CHUNK = 16;  // tiles per LDS staging chunk
+// Thread groups per workgroup: group g walks its own quarter of the split's tile range (the split is the wgrad
+// kernel's, so one workgroup per split: 42 of them at hidden 512) and the groups' per-neuron sums are combined in
+// LDS in a fixed order (deterministic). One 256-thread group per split reached 1.6 TB/s at hidden 512 (DESIGN.md
+// §3.11); four keep 4x the row loads in flight.
+// The jet kinds keep ~120 VGPRs at four groups; EDGE_W2 / EDGE_W3 (16 column scalars and up to four row streams per
+// tile) need their 256-VGPR budget, so they run two groups (512 threads).
+constexpr int edge_groups(int kind) { return kind == 2 || kind == 3 ? 4 : 2; }
+constexpr int edge_threads(int kind) { return edge_groups(kind) * THREADS; }
+constexpr int EDGE_ACC = 14;  // per-thread sums: gw0[4], gb0, gwo[4], gbo, gbj[4]
 
 template <int KIND>
-__global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__ r0, const float* __restrict__ r1,
-                                                       const float* __restrict__ r2, const float* __restrict__ r3,
-                                                       const float* __restrict__ x, const float* __restrict__ sc,
-                                                       const float* __restrict__ sgy, const float* __restrict__ su,
-                                                       int64_t n, int64_t ntiles,
-                                                       int64_t tps, float* __restrict__ partial, int64_t P, int d,
-                                                       int o, int lh, int h, int64_t bstride_act = 0,
-                                                       int64_t bstride_part = 0) {
-    // per-column scalars of one chunk: [col][0..3] = x (d_in <= 4), [col][4..7] = gy / v / glap, [col][8..11] = the
-    // first-order seed gy (n, o) of a seeded W3 (sgy != nullptr: rows r3 = a_L add gy^T a_L to dWout, sum gy to
-    // dbout), [col][12..15] = W3's output weighting u (n, o) (ones when su == nullptr)
+__global__ __launch_bounds__(edge_threads(KIND)) void edge_kernel(const float* __restrict__ r0, const float* __restrict__ r1,
+                                                            const float* __restrict__ r2, const float* __restrict__ r3,
+                                                            const float* __restrict__ x, const float* __restrict__ sc,
+                                                            const float* __restrict__ sgy, const float* __restrict__ su,
+                                                            int64_t n, int64_t ntiles,
+                                                            int64_t tps, float* __restrict__ eslab, int64_t E, int d,
+                                                            int o, int lh, int h, int64_t bstride_act = 0,
+                                                            int64_t bstride_e = 0) {
+    // per-column scalars of one chunk (per group): [col][0..3] = x (d_in <= 4), [col][4..7] = gy / v / glap,
+    // [col][8..11] = the first-order seed gy (n, o) of a seeded W3 (sgy != nullptr: rows r3 = a_L add gy^T a_L to
+    // dWout, sum gy to dbout) / EDGE_MIX's g, [col][12..15] = W3's / EDGE_MIX's output weighting u (n, o) (ones when
+    // su == nullptr)
     constexpr bool JETK = KIND == EDGE_JET || KIND == EDGE_MIX;
+    constexpr int EDGE_GROUPS = edge_groups(KIND);
+    static_assert(JETK == (EDGE_GROUPS == 4), "edge_groups follows the kind");
     constexpr int CPT = JETK ? 4 : 16;  // coordinates per tile
     constexpr int NSC = (KIND == EDGE_W3 || KIND == EDGE_MIX) ? 16 : 9;
-    __shared__ __attribute__((aligned(16))) float scal[EDGE_CHUNK * CPT][NSC];
+    constexpr int SCAL = EDGE_CHUNK * CPT * NSC;  // floats of one group's staging area
+    constexpr int SMEM = EDGE_GROUPS * SCAL > EDGE_GROUPS * THREADS * EDGE_ACC ? EDGE_GROUPS * SCAL
+                                                                              : EDGE_GROUPS * THREADS * EDGE_ACC;
+    __shared__ __attribute__((aligned(16))) float smem[SMEM];
+    const int grp = threadIdx.x / THREADS, tl = threadIdx.x % THREADS;
+    float (*scal)[NSC] = (float (*)[NSC])(smem + grp * SCAL);
     const bool seeded = KIND == EDGE_W3 && sgy != nullptr;
     const bool weighted = KIND == EDGE_W3 && su != nullptr;
     const ParamOffsets off(d, o, lh, h);
     const int s = blockIdx.x;
     const int64_t t0 = (int64_t)s * tps, t1 = t0 + tps < ntiles ? t0 + tps : ntiles;
-    if (gridDim.y > 1) {  // grouped W2 (EDGE_W2 over batched weights): grid.y = batch element
-        const int64_t b = blockIdx.y;
+    // this group's quarter [g0, g1) of the split; every group runs the same number of chunk trips (barriers)
+    const int64_t q = (t1 - t0 + EDGE_GROUPS - 1) / EDGE_GROUPS;
+    const int64_t g0 = t0 + grp * q < t1 ? t0 + grp * q : t1, g1 = g0 + q < t1 ? g0 + q : t1;
+    const int64_t trips = (q + EDGE_CHUNK - 1) / EDGE_CHUNK;
+    if (gridDim.z > 1) {  // grouped W2 (EDGE_W2 over batched weights): grid.z = batch element
+        const int64_t b = blockIdx.z;
         r0 += b * bstride_act;
         r1 += b * bstride_act;
         x += b * n * d;
         sc += b * n * o;
-        partial += b * bstride_part;
+        eslab += b * bstride_e;
     }
     const int64_t tstride = (int64_t)h * 16;
     const int ns = KIND == EDGE_W2 ? o : ((KIND == EDGE_W3 || KIND == EDGE_MIX) ? d : 1);  // scalars besides x
-    float* out = partial + (int64_t)s * P;
-    for (int tb = 0; tb < h; tb += THREADS) {
-        const int t = tb + threadIdx.x;
+    // this split's compact edge slab: [W0 (h, d) | b0 (h) | Wout (o, h) | bout (o)] (edge_reduce_kernel maps it back
+    // to the parameter order); grid.y = the 256-neuron block
+    float* out = eslab + (int64_t)s * E;
+    const int64_t ewo = off.hidden0, ebo = off.hidden0 + (int64_t)o * h;
+    {
+        const int tb = blockIdx.y * THREADS;
+        const int t = tb + tl;
         float gw0[MAXD] = {0.f, 0.f, 0.f, 0.f}, gb0 = 0.f;
         float gwo[MAXO] = {0.f, 0.f, 0.f, 0.f}, gbo = 0.f, gbj[MAXO] = {0.f, 0.f, 0.f, 0.f};
-        for (int64_t c0 = t0; c0 < t1; c0 += EDGE_CHUNK) {
-            const int nt = (int)(t1 - c0 < EDGE_CHUNK ? t1 - c0 : EDGE_CHUNK);
+        for (int64_t it = 0; it < trips; ++it) {
+            const int64_t c0 = g0 + it * EDGE_CHUNK;
+            const int nt = (int)(g1 - c0 < 0 ? 0 : (g1 - c0 < EDGE_CHUNK ? g1 - c0 : EDGE_CHUNK));
             __syncthreads();
-            for (int e = threadIdx.x; e < EDGE_CHUNK * CPT; e += THREADS) {
+            for (int e = tl; e < EDGE_CHUNK * CPT; e += THREADS) {
                 const int64_t cd = c0 * CPT + e;
                 const bool ok = e < nt * CPT && cd < n;
 #pragma unroll
@@ -195,53 +221,53 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
             }
             __syncthreads();
             if (t < h) {
-#pragma unroll(JETK ? 8 : 2)
+#pragma unroll(JETK ? 8 : 1)
                 for (int i = 0; i < nt; ++i) {
                     const int64_t tile = c0 + i;
                     const f32x4* a = (const f32x4*)(r0 + tile * tstride + t * 16);
                     const f32x4* b = (const f32x4*)(r1 + tile * tstride + t * 16);
                     f32x4 av[4], bv[4], cv[4], ev[4];
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        av[q] = a[q];
-                        bv[q] = b[q];
-                        if (KIND == EDGE_W3) cv[q] = ((const f32x4*)(r2 + tile * tstride + t * 16))[q];
-                        if (KIND == EDGE_W3) ev[q] = seeded ? ((const f32x4*)(r3 + tile * tstride + t * 16))[q] : f32x4{};
+                    for (int qq = 0; qq < 4; ++qq) {
+                        av[qq] = a[qq];
+                        bv[qq] = b[qq];
+                        if (KIND == EDGE_W3) cv[qq] = ((const f32x4*)(r2 + tile * tstride + t * 16))[qq];
+                        if (KIND == EDGE_W3) ev[qq] = seeded ? ((const f32x4*)(r3 + tile * tstride + t * 16))[qq] : f32x4{};
                     }
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
+                    for (int qq = 0; qq < 4; ++qq) {
                         if constexpr (KIND == EDGE_JET) {
                             // columns 4q..4q+3 = coordinate q of the tile, streams (value, d/dx1, d/dx2, second)
-                            const float* sv = scal[i * 4 + q];
-                            gb0 += av[q][0];
-                            gw0[0] += av[q][0] * sv[0] + av[q][1];
-                            gw0[1] += av[q][0] * sv[1] + av[q][2];
-                            gwo[0] += sv[4] * bv[q][3];
+                            const float* sv = scal[i * 4 + qq];
+                            gb0 += av[qq][0];
+                            gw0[0] += av[qq][0] * sv[0] + av[qq][1];
+                            gw0[1] += av[qq][0] * sv[1] + av[qq][2];
+                            gwo[0] += sv[4] * bv[qq][3];
                         } else if constexpr (KIND == EDGE_MIX) {
-                            const float* sv = scal[i * 4 + q];
-                            gb0 += av[q][0];
+                            const float* sv = scal[i * 4 + qq];
+                            gb0 += av[qq][0];
 #pragma unroll
                             for (int k = 0; k < MAXD; ++k)
-                                gw0[k] += av[q][0] * sv[k] + av[q][1] * sv[4 + k] + av[q][2] * sv[8 + k];
+                                gw0[k] += av[qq][0] * sv[k] + av[qq][1] * sv[4 + k] + av[qq][2] * sv[8 + k];
 #pragma unroll
-                            for (int j = 0; j < MAXO; ++j) gwo[j] += sv[12 + j] * bv[q][3];
+                            for (int j = 0; j < MAXO; ++j) gwo[j] += sv[12 + j] * bv[qq][3];
                         } else {
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
-                                const float* sv = scal[i * 16 + 4 * q + r];
-                                gb0 += av[q][r];
+                                const float* sv = scal[i * 16 + 4 * qq + r];
+                                gb0 += av[qq][r];
                                 if constexpr (KIND == EDGE_W2) {
 #pragma unroll
-                                    for (int k = 0; k < MAXD; ++k) gw0[k] += av[q][r] * sv[k];
+                                    for (int k = 0; k < MAXD; ++k) gw0[k] += av[qq][r] * sv[k];
 #pragma unroll
-                                    for (int j = 0; j < MAXO; ++j) gwo[j] += sv[4 + j] * bv[q][r];
+                                    for (int j = 0; j < MAXO; ++j) gwo[j] += sv[4 + j] * bv[qq][r];
                                     gbo += t < MAXO ? sv[4 + (t & 3)] : 0.f;
                                 } else {
 #pragma unroll
-                                    for (int k = 0; k < MAXD; ++k) gw0[k] += cv[q][r] * sv[4 + k] + av[q][r] * sv[k];
+                                    for (int k = 0; k < MAXD; ++k) gw0[k] += cv[qq][r] * sv[4 + k] + av[qq][r] * sv[k];
 #pragma unroll
                                     for (int j = 0; j < MAXO; ++j) {
-                                        gwo[j] += sv[12 + j] * bv[q][r] + sv[8 + j] * ev[q][r];
+                                        gwo[j] += sv[12 + j] * bv[qq][r] + sv[8 + j] * ev[qq][r];
                                         gbj[j] += sv[8 + j];
                                     }
                                 }
@@ -251,7 +277,35 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
                 }
             }
         }
-        if (t < h) {
+        // combine the groups' sums in a fixed order (the staging area is reused)
+        __syncthreads();
+        {
+            float* red = smem + (grp * THREADS + tl) * EDGE_ACC;
+#pragma unroll
+            for (int k = 0; k < MAXD; ++k) red[k] = gw0[k];
+            red[4] = gb0;
+#pragma unroll
+            for (int j = 0; j < MAXO; ++j) {
+                red[5 + j] = gwo[j];
+                red[10 + j] = gbj[j];
+            }
+            red[9] = gbo;
+        }
+        __syncthreads();
+        if (grp == 0 && t < h) {
+#pragma unroll
+            for (int gg = 1; gg < EDGE_GROUPS; ++gg) {
+                const float* red = smem + (gg * THREADS + tl) * EDGE_ACC;
+#pragma unroll
+                for (int k = 0; k < MAXD; ++k) gw0[k] += red[k];
+                gb0 += red[4];
+#pragma unroll
+                for (int j = 0; j < MAXO; ++j) {
+                    gwo[j] += red[5 + j];
+                    gbj[j] += red[10 + j];
+                }
+                gbo += red[9];
+            }
 #pragma unroll
             for (int k = 0; k < MAXD; ++k)
                 if (k < d) out[off.w0 + (int64_t)t * d + k] = gw0[k];
@@ -259,34 +313,37 @@ __global__ __launch_bounds__(THREADS) void edge_kernel(const float* __restrict__
             if constexpr (KIND == EDGE_W2) {
 #pragma unroll
                 for (int j = 0; j < MAXO; ++j)
-                    if (j < o) out[off.wout + (int64_t)j * h + t] = gwo[j];
-                if (t < o) out[off.bout + t] = gbo;
+                    if (j < o) out[ewo + (int64_t)j * h + t] = gwo[j];
+                if (t < o) out[ebo + t] = gbo;
             } else if constexpr (KIND == EDGE_W3) {
 #pragma unroll
                 for (int j = 0; j < MAXO; ++j) {
-                    if (j < o) out[off.wout + (int64_t)j * h + t] = gwo[j];
-                    if (j < o && t == j) out[off.bout + t] = gbj[j];
+                    if (j < o) out[ewo + (int64_t)j * h + t] = gwo[j];
+                    if (j < o && t == j) out[ebo + t] = gbj[j];
                 }
             } else if constexpr (KIND == EDGE_MIX) {
 #pragma unroll
                 for (int j = 0; j < MAXO; ++j)
-                    if (j < o) out[off.wout + (int64_t)j * h + t] = gwo[j];
-                if (t < o) out[off.bout + t] = 0.f;
+                    if (j < o) out[ewo + (int64_t)j * h + t] = gwo[j];
+                if (t < o) out[ebo + t] = 0.f;
             } else {
-                for (int j = 0; j < o; ++j) out[off.wout + (int64_t)j * h + t] = gwo[0];
-                if (t < o) out[off.bout + t] = 0.f;
+                for (int j = 0; j < o; ++j) out[ewo + (int64_t)j * h + t] = gwo[0];
+                if (t < o) out[ebo + t] = 0.f;
             }
         }
     }
 }
 
-// gp[i] = sum over the partial slabs; indices in [lo, hi) (the hidden layers' W/b) sum S + S2 slabs, the others
-// (first and output layer, written by the small kernels into the first S slabs only) sum S.
+// gp[i] = sum over the partial slabs for i in [begin, end); indices in [lo, hi) (the hidden layers' W/b) sum S + S2
+// slabs, the others S.
 __global__ void reduce_kernel(const float* __restrict__ partial, int64_t S, int64_t P, float* __restrict__ gp,
-                              int64_t S2 = 0, int64_t lo = 0, int64_t hi = 0, int64_t bstride_part = 0) {
+                              int64_t S2 = 0, int64_t lo = 0, int64_t hi = 0, int64_t bstride_part = 0,
+                              int64_t begin = 0, int64_t end = -1) {
     partial += (int64_t)blockIdx.y * bstride_part;  // grouped: grid.y = batch element, gp rows of P
     gp += (int64_t)blockIdx.y * P;
-    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < P; idx += (int64_t)gridDim.x * blockDim.x) {
+    if (end < 0) end = P;
+    for (int64_t idx = begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < end;
+         idx += (int64_t)gridDim.x * blockDim.x) {
         const int64_t ns = (idx >= lo && idx < hi) ? S + S2 : S;
         // 8 independent partial sums keep 8 slab loads in flight per thread (one dependent chain was
         // latency-bound); the combine order is fixed, so the result stays deterministic
@@ -299,6 +356,25 @@ __global__ void reduce_kernel(const float* __restrict__ partial, int64_t S, int6
         }
         for (; s < ns; ++s) a[0] += col[s * P];
         gp[idx] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    }
+}
+
+// The edge layers' gradient: sum of the SE compact edge slabs (edge_kernel) into the parameter order: compact index
+// c < hidden0 is W0 / b0 (parameter c), the rest Wout / bout (parameter wout + c - hidden0). grid.y = batch element.
+__global__ void edge_reduce_kernel(const float* __restrict__ eslab, int64_t SE, int64_t E, int64_t hidden0,
+                                   int64_t wout, float* __restrict__ gp, int64_t P, int64_t bstride_e) {
+    eslab += (int64_t)blockIdx.y * bstride_e;
+    gp += (int64_t)blockIdx.y * P;
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < E; c += (int64_t)gridDim.x * blockDim.x) {
+        float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        const float* col = eslab + c;
+        int64_t s = 0;
+        for (; s + 8 <= SE; s += 8) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) a[q] += col[(s + q) * E];
+        }
+        for (; s < SE; ++s) a[0] += col[s * E];
+        gp[c < hidden0 ? c : wout + (c - hidden0)] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     }
 }
 
