@@ -53,6 +53,14 @@ void launch_small_mix(dim3 grid, hipStream_t st, const float* abuf, const float*
                       int d, int o, int lh);
 // tu_wide.hip: hidden width 512 (mode as siren_common.h MODE_*); spill = cos scratch for MODE_W1 / MODE_STORE
 void launch_wide(int mode, dim3 grid, hipStream_t st, const FusedArgs& a, float* spill);
+// tu_wide_jet.hip: second order at hidden 512 (two-stream jet: 8 coordinates x (value, tangent) per wave, 32 per
+// workgroup); abuf / dbuf / spill: (L + 1) layers x 2 n_pad columns x 512 floats each
+void launch_wide_jet2(dim3 grid, hipStream_t st, const float* ws, const float* x, const float* v, const float* gy,
+                      const float* u, int64_t n, int d, int o, int lh, float w0, float w, float* gx, float* ydot,
+                      float* spill, float* abuf, float* dbuf, int64_t n_pad);
+void launch_small_j2(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* v,
+                     const float* gy, const float* u, int64_t n, int64_t n_pad, int64_t tps, float* eslab, int64_t E,
+                     int d, int o, int lh);
 // tu_w3.hip (launch_small_w3 lives in tu_train.hip with the other edge-layer reductions)
 void launch_w3(bool theta, dim3 grid, hipStream_t st, const float* ws, const float* x, const float* v, const float* gy,
                const float* u, float* ydot, int o, int64_t n, float* gx, float* spill, float* A, float* At, float* D,

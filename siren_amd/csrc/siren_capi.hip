@@ -612,11 +612,32 @@ struct W3Plan {
 };
 }  // namespace
 
+// hidden 512: the two-stream jet (wide_jet_kernel.hpp): a-, zb- and z-jets of L + 1 layers over 2 n_pad columns
+// (n_pad: 32 coordinates per workgroup), the split-K slabs and the edge slabs
+namespace {
+struct W3WidePlan {
+    int64_t n_pad, cols, tiles, splits, tps, buf_floats, eslab_off, partial_floats, total;
+    EdgeSplit es;
+    W3WidePlan(const siren_cfg* cfg, int64_t n) : es(cfg, (n + 31) / 32 * 32 / 8) {
+        n_pad = (n + 31) / 32 * 32;
+        cols = 2 * n_pad;
+        tiles = cols / 16;
+        const int64_t want = wgrad_splits(cfg);
+        splits = std::max<int64_t>(1, std::min(tiles, want));
+        tps = std::max<int64_t>(1, (tiles + splits - 1) / splits);
+        splits = std::max<int64_t>(1, (tiles + tps - 1) / tps);
+        buf_floats = (int64_t)(cfg->n_hidden + 1) * cols * cfg->hidden;
+        eslab_off = splits * param_count(cfg);
+        partial_floats = eslab_off + es.floats;
+        total = 3 * buf_floats + partial_floats;
+    }
+};
+}  // namespace
+
 int32_t siren_second_order_ws_floats(const siren_cfg* cfg, int64_t n, int32_t want_theta, int64_t* count) {
     if (int rc = check_cfg(cfg, true)) return rc;
-    if (wide(cfg)) return fail(SIREN_EUNSUPPORTED, "siren_second_order covers hidden_features == 256");
     if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
-    *count = W3Plan(cfg, n, want_theta != 0).total;
+    *count = wide(cfg) ? W3WidePlan(cfg, n).total : W3Plan(cfg, n, want_theta != 0).total;
     return SIREN_OK;
 }
 
@@ -630,14 +651,53 @@ int32_t siren_second_order_seeded(const siren_cfg* cfg, const float* ws, const f
     return siren_second_order_ex(cfg, ws, x, n, v, nullptr, gy, tws, gx, gparams, nullptr, stream);
 }
 
+// hidden 512: one two-stream jet launch (forward + reverse), then the split-K wgrad over 2 n_pad columns, the
+// EDGE_J2 edge layers and the slab reductions
+static int32_t second_order_wide(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
+                                 const float* u, const float* gy, float* tws, float* gx, float* gparams, float* ydot,
+                                 void* stream) {
+    if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    const W3WidePlan plan(cfg, n);
+    const hipStream_t st = (hipStream_t)stream;
+    const int64_t P = param_count(cfg);
+    const bool theta = gparams != nullptr;
+    if (n == 0) {
+        if (theta) (void)hipMemsetAsync(gparams, 0, P * sizeof(float), st);
+        return hip_status("siren_second_order (hidden 512)");
+    }
+    if (ws == nullptr || tws == nullptr || gx == nullptr || x == nullptr || v == nullptr)
+        return fail(SIREN_EINVAL, "ws/x/v/tws/gx is NULL");
+    float* abuf = tws;
+    float* dbuf = abuf + plan.buf_floats;
+    float* spill = dbuf + plan.buf_floats;
+    float* partial = spill + plan.buf_floats;
+    siren::launch_wide_jet2(dim3((unsigned)(plan.n_pad / 32)), st, ws, x, v, gy, u, n, cfg->d_in, cfg->d_out,
+                            cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, gx, ydot, spill, abuf, dbuf, plan.n_pad);
+    if (int rc = hip_status("siren_second_order (hidden 512 jet)")) return rc;
+    if (!theta) return SIREN_OK;
+    const unsigned quads = (unsigned)((cfg->hidden / 256) * (cfg->hidden / 256));
+    siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden, quads), st, abuf, dbuf, plan.cols,
+                        plan.tps, partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1, cfg->hidden, 2);
+    if (int rc = hip_status("siren_second_order (hidden 512 wgrad)")) return rc;
+    siren::launch_small_j2(plan.es.grid(cfg), st, abuf, dbuf, x, v, gy, u, n, plan.n_pad, plan.es.tps,
+                           partial + plan.eslab_off, plan.es.E, cfg->d_in, cfg->d_out, cfg->n_hidden);
+    if (int rc = hip_status("siren_second_order (hidden 512 small)")) return rc;
+    return finish_grads(cfg, st, partial, plan.splits, 0, partial + plan.eslab_off, plan.es, gparams,
+                        "siren_second_order (hidden 512 reduce)");
+}
+
 static int32_t second_order_impl(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
                           const float* u, const float* gy, float* tws, float* gx, float* gparams, float* ydot,
                           float* kept, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
+    if (!cfg->outermost_linear)
+        return fail(SIREN_EUNSUPPORTED, "siren_second_order needs a linear output layer");
+    if (wide(cfg)) {
+        if (kept != nullptr) return fail(SIREN_EUNSUPPORTED, "the kept-forward W3 covers hidden 256");
+        return second_order_wide(cfg, ws, x, n, v, u, gy, tws, gx, gparams, ydot, stream);
+    }
     if (cfg->n_hidden > siren::MAX_LH_GRAD)
-        return fail(SIREN_EUNSUPPORTED, "siren_second_order needs 1 <= num_hidden_layers <= 3");
-    if (!cfg->outermost_linear || wide(cfg))
-        return fail(SIREN_EUNSUPPORTED, "siren_second_order covers hidden 256 with a linear output layer");
+        return fail(SIREN_EUNSUPPORTED, "siren_second_order needs 1 <= num_hidden_layers <= 3 at hidden 256");
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
     if (ws == nullptr || tws == nullptr || gx == nullptr || (n > 0 && (x == nullptr || v == nullptr)))
         return fail(SIREN_EINVAL, "ws/x/v/tws/gx is NULL");

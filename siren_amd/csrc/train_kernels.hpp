@@ -81,7 +81,10 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
         // bias gradient: thread t owns neuron t (jet tiles: the bias only enters the value columns 0, 4, 8, 12)
         {
             const f32x4* row = (const f32x4*)(sd + threadIdx.x * 16);
-            if (jet_bias) {
+            if (jet_bias == 2) {  // two-stream jet tiles (wide_jet_kernel.hpp): value columns 0, 2, ..., 14
+                bsum += ((row[0][0] + row[0][2]) + (row[1][0] + row[1][2])) +
+                        ((row[2][0] + row[2][2]) + (row[3][0] + row[3][2]));
+            } else if (jet_bias) {
                 bsum += (row[0][0] + row[1][0]) + (row[2][0] + row[3][0]);
             } else {
                 const f32x4 v = row[0] + row[1] + row[2] + row[3];
@@ -128,7 +131,11 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
 //   EDGE_MIX: the mixed jet (third-order adjoint, jet_kernel.hpp MIX): rows as EDGE_JET, scalars x, v (sc), g (sgy)
 //             (n, d) and u (su, (n, o), NULL = ones): dW0[:, k] = sum zb_0,value x_k + zb_0,v v_k + zb_0,g g_k,
 //             db0 = sum zb_0,value, dWout_j = sum u_j a_L,second, dbout = 0
-enum { EDGE_W2 = 0, EDGE_W3 = 1, EDGE_JET = 2, EDGE_MIX = 3 };
+//   EDGE_J2 : two-stream jet tiles (wide_jet_kernel.hpp: 16 columns = 8 coordinates x (value, tangent along v)),
+//             rows zb_0 jet, a_L jet; scalars x, v (sc), gy (sgy, nullable), u (su, NULL = ones):
+//             dW0[:, k] = sum zb_0,val x_k + zb_0,tan v_k, db0 = sum zb_0,val, dWout_j = sum gy_j a_L,val + u_j a_L,tan,
+//             dbout_j = sum gy_j
+enum { EDGE_W2 = 0, EDGE_W3 = 1, EDGE_JET = 2, EDGE_MIX = 3, EDGE_J2 = 4 };
 constexpr int EDGE_CHUNK = 16;  // tiles per LDS staging chunk
 // Thread groups per workgroup: group g walks its own quarter of the split's tile range (the split is the wgrad
 // kernel's, so one workgroup per split: 42 of them at hidden 512) and the groups' per-neuron sums are combined in
@@ -155,9 +162,8 @@ __global__ __launch_bounds__(edge_threads(KIND)) void edge_kernel(const float* _
     // su == nullptr)
     constexpr bool JETK = KIND == EDGE_JET || KIND == EDGE_MIX;
     constexpr int EDGE_GROUPS = edge_groups(KIND);
-    static_assert(JETK == (EDGE_GROUPS == 4), "edge_groups follows the kind");
-    constexpr int CPT = JETK ? 4 : 16;  // coordinates per tile
-    constexpr int NSC = (KIND == EDGE_W3 || KIND == EDGE_MIX) ? 16 : 9;
+    constexpr int CPT = JETK ? 4 : (KIND == EDGE_J2 ? 8 : 16);  // coordinates per tile
+    constexpr int NSC = (KIND == EDGE_W3 || KIND == EDGE_MIX || KIND == EDGE_J2) ? 16 : 9;
     constexpr int SCAL = EDGE_CHUNK * CPT * NSC;  // floats of one group's staging area
     constexpr int SMEM = EDGE_GROUPS * SCAL > EDGE_GROUPS * THREADS * EDGE_ACC ? EDGE_GROUPS * SCAL
                                                                               : EDGE_GROUPS * THREADS * EDGE_ACC;
@@ -182,7 +188,7 @@ __global__ __launch_bounds__(edge_threads(KIND)) void edge_kernel(const float* _
         eslab += b * bstride_e;
     }
     const int64_t tstride = (int64_t)h * 16;
-    const int ns = KIND == EDGE_W2 ? o : ((KIND == EDGE_W3 || KIND == EDGE_MIX) ? d : 1);  // scalars besides x
+    const int ns = KIND == EDGE_W2 ? o : ((KIND == EDGE_W3 || KIND == EDGE_MIX || KIND == EDGE_J2) ? d : 1);
     // this split's compact edge slab: [W0 (h, d) | b0 (h) | Wout (o, h) | bout (o)] (edge_reduce_kernel maps it back
     // to the parameter order); grid.y = the 256-neuron block
     float* out = eslab + (int64_t)s * E;
@@ -209,6 +215,12 @@ __global__ __launch_bounds__(edge_threads(KIND)) void edge_kernel(const float* _
                         scal[e][8 + j] = (ok && seeded && j < o) ? sgy[cd * o + j] : 0.f;
                         scal[e][12 + j] = weighted ? ((ok && j < o) ? su[cd * o + j] : 0.f) : 1.f;
                     }
+                } else if constexpr (KIND == EDGE_J2) {
+#pragma unroll
+                    for (int j = 0; j < MAXO; ++j) {
+                        scal[e][8 + j] = (ok && sgy != nullptr && j < o) ? sgy[cd * o + j] : 0.f;
+                        scal[e][12 + j] = (ok && j < o) ? (su != nullptr ? su[cd * o + j] : 1.f) : 0.f;
+                    }
                 } else if constexpr (KIND == EDGE_MIX) {
 #pragma unroll
                     for (int k = 0; k < MAXD; ++k) scal[e][8 + k] = (ok && k < d) ? sgy[cd * d + k] : 0.f;
@@ -221,7 +233,7 @@ __global__ __launch_bounds__(edge_threads(KIND)) void edge_kernel(const float* _
             }
             __syncthreads();
             if (t < h) {
-#pragma unroll(JETK ? 8 : 1)
+#pragma unroll(JETK ? 8 : (KIND == EDGE_J2 ? 2 : 1))
                 for (int i = 0; i < nt; ++i) {
                     const int64_t tile = c0 + i;
                     const f32x4* a = (const f32x4*)(r0 + tile * tstride + t * 16);
@@ -243,6 +255,22 @@ __global__ __launch_bounds__(edge_threads(KIND)) void edge_kernel(const float* _
                             gw0[0] += av[qq][0] * sv[0] + av[qq][1];
                             gw0[1] += av[qq][0] * sv[1] + av[qq][2];
                             gwo[0] += sv[4] * bv[qq][3];
+                        } else if constexpr (KIND == EDGE_J2) {
+                            // columns 4qq + r: coordinate 2qq + r / 2, stream r & 1
+#pragma unroll
+                            for (int rr = 0; rr < 2; ++rr) {
+                                const float* sv = scal[i * 8 + 2 * qq + rr];
+                                const float zv = av[qq][2 * rr], zt = av[qq][2 * rr + 1];
+                                const float av_ = bv[qq][2 * rr], at_ = bv[qq][2 * rr + 1];
+                                gb0 += zv;
+#pragma unroll
+                                for (int k = 0; k < MAXD; ++k) gw0[k] += zv * sv[k] + zt * sv[4 + k];
+#pragma unroll
+                                for (int j = 0; j < MAXO; ++j) {
+                                    gwo[j] += sv[8 + j] * av_ + sv[12 + j] * at_;
+                                    gbj[j] += sv[8 + j];
+                                }
+                            }
                         } else if constexpr (KIND == EDGE_MIX) {
                             const float* sv = scal[i * 4 + qq];
                             gb0 += av[qq][0];
@@ -315,7 +343,7 @@ __global__ __launch_bounds__(edge_threads(KIND)) void edge_kernel(const float* _
                 for (int j = 0; j < MAXO; ++j)
                     if (j < o) out[ewo + (int64_t)j * h + t] = gwo[j];
                 if (t < o) out[ebo + t] = gbo;
-            } else if constexpr (KIND == EDGE_W3) {
+            } else if constexpr (KIND == EDGE_W3 || KIND == EDGE_J2) {
 #pragma unroll
                 for (int j = 0; j < MAXO; ++j) {
                     if (j < o) out[ewo + (int64_t)j * h + t] = gwo[j];

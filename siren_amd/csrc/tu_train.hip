@@ -44,6 +44,16 @@ void launch_small_mix(dim3 grid, hipStream_t st, const float* abuf, const float*
                        H, (int64_t)0, (int64_t)0);
 }
 
+// rows: zb_0 jet (dbuf layer 0), a_L jet (abuf layer L) of the two-stream tiles (2 n_pad columns per layer, h = 512)
+void launch_small_j2(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* v,
+                     const float* gy, const float* u, int64_t n, int64_t n_pad, int64_t tps, float* eslab, int64_t E,
+                     int d, int o, int lh) {
+    constexpr int WHH = 512;
+    hipLaunchKernelGGL(edge_kernel<EDGE_J2>, grid, dim3(edge_threads(EDGE_J2)), 0, st, dbuf,
+                       abuf + (int64_t)lh * 2 * n_pad * WHH, NOF, NOF, x, v, gy, u, n, n_pad / 8, tps, eslab, E, d, o,
+                       lh, WHH, (int64_t)0, (int64_t)0);
+}
+
 void launch_reduce(dim3 grid, hipStream_t st, const float* partial, int64_t S, int64_t P, float* gp, int64_t S2,
                    int64_t lo, int64_t hi, int64_t bstride_part, int64_t begin, int64_t end) {
     hipLaunchKernelGGL(reduce_kernel, grid, dim3(256), 0, st, partial, S, P, gp, S2, lo, hi, bstride_part, begin, end);

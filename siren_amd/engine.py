@@ -50,8 +50,9 @@ class SirenEngine:
         self.stored_supported = (self.supported and bool(outermost_linear) and not (int(flags) & 1) and
                                  (int(hidden) == 512 or (1 <= n_hidden <= 3 and omega_first != 0
                                                          and omega_hidden != 0)))
-        self.second_order_supported = (self.supported and int(hidden) == 256 and 1 <= n_hidden <= 3
-                                       and int(d_out) <= 4 and bool(outermost_linear))
+        # hidden 512: the two-stream jet kernel (wide_jet_kernel.hpp), 1..8 hidden layers
+        self.second_order_supported = (self.supported and int(d_out) <= 4 and bool(outermost_linear)
+                                       and ((int(hidden) == 256 and 1 <= n_hidden <= 3) or int(hidden) == 512))
         # the third-order adjoint (mixed jet, siren_hvp_backward): hidden 256, linear output, 1..5 hidden layers
         self.hvp_backward_supported = (self.supported and int(hidden) == 256 and 1 <= n_hidden <= 5
                                        and bool(outermost_linear))
@@ -397,8 +398,8 @@ class SirenEngine:
         ydot = J v (n, d_out) = dF/du when want_ydot."""
         self._require()
         if not self.second_order_supported:
-            raise _lib.SirenUnsupported('siren_second_order covers hidden 256, d_out <= 4, linear output, '
-                                        '1..3 hidden layers')
+            raise _lib.SirenUnsupported('siren_second_order covers d_out <= 4, linear output, hidden 256 with 1..3 '
+                                        'hidden layers or hidden 512')
         x = self._check_x(x)
         n, o = x.shape[0], self.cfg.d_out
         v = v.contiguous()

@@ -95,3 +95,8 @@ def g7():
 @pytest.fixture(scope='session')
 def g8():
     return load_golden('g8')
+
+
+@pytest.fixture(scope='session')
+def g9():
+    return load_golden('g9')

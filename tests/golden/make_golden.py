@@ -23,6 +23,8 @@ Fixtures:
       with its image/video dependencies stubbed; the notebook SineLayer / Siren (explore_siren.ipynb cells 3 and 5,
       executed from the notebook's JSON) at hidden 256: outermost_linear True / False, first_omega_0 30 / 3000 —
       init weights, forward output, coords gradient (and Laplacian, image-mse theta-grads) in fp32 and fp64.
+  G9  second order at hidden 512 (a G4-style pin for the hidden-512 W3): SingleBVPNet(hidden_features=512) seed 0,
+      d2 o1 gradients_mse (1024 coords) and d3 o1 sdf (512 on + 512 off surface): gradient and fp64 theta-grads.
   G6  vector outputs / PML losses: 5x256 d2 o2 (helmholtz_pml, loss_functions.py:139-211)
       and 5x256 d3 o1 (wave_pml, loss_functions.py:112-136), 1024 coords each: jacobian / hessian
       (diff_operators.py:5-24, 46-59), the loss terms and their fp64 theta-grads.
@@ -280,6 +282,45 @@ def make_g8(modules, D, L, meta):
     np.savez_compressed(os.path.join(OUT, 'golden_g8.npz'), **store)
 
 
+def make_g9(modules, D, L, meta):
+    store = {}
+    gen = torch.Generator().manual_seed(9)
+    coords = torch.rand(1, 1024, 2, generator=gen) * 2 - 1
+    gt_grad = torch.randn(1, 1024, 2, generator=gen) * 10.
+    torch.manual_seed(0)
+    net = modules.SingleBVPNet(type='sine', in_features=2, out_features=1, hidden_features=512, num_hidden_layers=3)
+    for k, v in state_to_np(net.state_dict()).items():
+        store['A_w_' + k] = v
+    store['A_coords'], store['A_gt_gradients'] = coords.numpy(), gt_grad.numpy()
+    net = net.double()
+    out = net({'coords': coords.double()})
+    store['A_gradient_f64'] = D.gradient(out['model_out'], out['model_in']).detach().numpy()
+    grads, total = grads_of(net, L.gradients_mse(out, {'gradients': gt_grad.double()}))
+    meta['G9_gradients_mse_f64'] = total
+    for k, v in grads.items():
+        store['A_gradients_mse_grad_' + k] = v
+    gen = torch.Generator().manual_seed(19)
+    on = torch.randn(512, 3, generator=gen, dtype=torch.float64)
+    on_n = on / on.norm(dim=-1, keepdim=True)
+    coords3 = torch.cat([on_n * 0.5, torch.rand(512, 3, generator=gen, dtype=torch.float64) * 2 - 1], 0).float()[None]
+    normals = torch.cat([on_n, -torch.ones(512, 3, dtype=torch.float64)], 0).float()[None]
+    sdf = torch.cat([torch.zeros(512, 1), -torch.ones(512, 1)], 0)[None]
+    torch.manual_seed(0)
+    net3 = modules.SingleBVPNet(type='sine', in_features=3, out_features=1, hidden_features=512, num_hidden_layers=3)
+    for k, v in state_to_np(net3.state_dict()).items():
+        store['B_w_' + k] = v
+    store['B_coords'], store['B_gt_sdf'], store['B_gt_normals'] = coords3.numpy(), sdf.numpy(), normals.numpy()
+    net3 = net3.double()
+    out = net3({'coords': coords3.double()})
+    ld = L.sdf(out, {'sdf': sdf.double(), 'normals': normals.double()})
+    for k, v in ld.items():
+        meta['G9_sdf_%s_f64' % k] = float(v)
+    grads, total = grads_of(net3, ld)
+    for k, v in grads.items():
+        store['B_sdf_grad_' + k] = v
+    np.savez_compressed(os.path.join(OUT, 'golden_g9.npz'), **store)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--skip-fit', action='store_true', help='reuse the G5 weights already in golden_fit.npz')
@@ -290,7 +331,7 @@ def main():
         with open(os.path.join(OUT, 'manifest.json')) as f:
             meta = json.load(f)
         for name in args.only.split(','):
-            {'g6': make_g6, 'g7': make_g7, 'g8': make_g8}[name](modules, D, L, meta)
+            {'g6': make_g6, 'g7': make_g7, 'g8': make_g8, 'g9': make_g9}[name](modules, D, L, meta)
         with open(os.path.join(OUT, 'manifest.json'), 'w') as f:
             json.dump(meta, f, indent=1, sort_keys=True)
         return

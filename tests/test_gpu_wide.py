@@ -164,3 +164,88 @@ def test_wide_stored_forward_split_matches_recompute(cuda, n, d, L, o):
     rgp = torch.cat([t.reshape(-1) for t in g[1:]]).numpy()
     assert np.max(np.abs(gp_s.cpu().numpy() - rgp)) <= 1e-4 * np.max(np.abs(rgp))
     assert np.max(np.abs(gx_s.cpu().numpy() - g[0].numpy())) <= tol_rel(g[0].numpy())
+
+
+# ---- second order at hidden 512 (wide_jet_kernel.hpp: two-stream jet) -------------------------------------------
+def w3_ref(x, layers, v, u, gy):
+    """fp64 autograd: F = sum gy . y + <v, J^T u>; returns dF/dx, dF/dtheta, J v."""
+    xt = torch.tensor(x, dtype=torch.float64, requires_grad=True)
+    params = [torch.tensor(t, dtype=torch.float64, requires_grad=True) for W, b in layers for t in (W, b)]
+    y = O.torch_forward(xt, params)
+    ut = torch.ones_like(y) if u is None else torch.tensor(u, dtype=torch.float64)
+    Ju = torch.autograd.grad(y, xt, ut, create_graph=True)[0]
+    F = (Ju * torch.tensor(v, dtype=torch.float64)).sum()
+    if gy is not None:
+        F = F + (y * torch.tensor(gy, dtype=torch.float64)).sum()
+    grads = torch.autograd.grad(F, [xt] + params, allow_unused=True, retain_graph=True)
+    gp = torch.cat([(torch.zeros_like(p) if g is None else g).reshape(-1) for g, p in zip(grads[1:], params)])
+    vt = torch.tensor(v, dtype=torch.float64)
+    jv = torch.stack([(torch.autograd.grad(y[:, j].sum(), xt, retain_graph=True)[0] * vt).sum(-1)
+                      for j in range(y.shape[1])], -1)
+    return grads[0].numpy(), gp.detach().numpy(), jv.numpy()
+
+
+@pytest.mark.parametrize('n,d,L,o,weighted,seeded', [(1, 2, 3, 1, False, False), (33, 2, 3, 1, False, True),
+                                                      (1000, 3, 3, 3, True, True), (2053, 3, 1, 1, False, False),
+                                                      (700, 1, 2, 2, True, False), (64, 4, 5, 4, True, True)])
+def test_wide_second_order_vs_fp64(cuda, n, d, L, o, weighted, seeded):
+    """H v, the mixed theta-gradient and J v at hidden 512 (siren_second_order_ex -> the two-stream jet kernel +
+    MFMA wgrad over 2n columns + EDGE_J2) against fp64 autograd."""
+    layers = random_layers(d, L, o, seed=5 * n + L)
+    eng = wide_engine(d, L, o)
+    assert eng.second_order_supported
+    ws = eng.pack(to_dev(O.flatten(layers), cuda))
+    rng = np.random.default_rng(n + 3 * o)
+    x = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    v = rng.normal(size=(n, d)).astype(np.float32)
+    u = rng.normal(size=(n, o)).astype(np.float32) if weighted else None
+    gy = rng.normal(size=(n, o)).astype(np.float32) if seeded else None
+    X, V = to_dev(x, cuda), to_dev(v, cuda)
+    gx, gp, ydot = eng.second_order(ws, X, V, want_theta=True, gy=to_dev(gy, cuda) if seeded else None,
+                                    u=to_dev(u, cuda) if weighted else None, want_ydot=True)
+    gx2, none = eng.second_order(ws, X, V, want_theta=False, gy=to_dev(gy, cuda) if seeded else None,
+                                 u=to_dev(u, cuda) if weighted else None)
+    rgx, rgp, rjv = w3_ref(x, layers, v, u, gy)
+    assert none is None and torch.equal(gx, gx2)
+    assert np.max(np.abs(gx.cpu().numpy() - rgx)) <= tol_rel(rgx)
+    assert np.max(np.abs(gp.cpu().numpy() - rgp)) <= 1e-4 * np.max(np.abs(rgp))
+    assert np.max(np.abs(ydot.cpu().numpy() - rjv)) <= tol_rel(rjv)
+
+
+def _no_torch_second_order(monkeypatch):
+    from siren_amd import _torch_path
+
+    def boom(*a, **k):
+        raise AssertionError('device-torch recompute used on a second-order path')
+    for name in ('vjp_vjp', 'jacobian_vjp', 'vjp_params'):
+        monkeypatch.setattr(_torch_path, name, boom)
+
+
+@pytest.mark.parametrize('case', ['A', 'B'])
+def test_g9_second_order_losses_at_hidden512_vs_reference(cuda, g9, manifest, case, monkeypatch):
+    """gradients_mse (d2) and sdf (d3) training at hidden_features=512 through the drop-in API against the
+    reference's fp64 theta-gradients (G9), with the device-torch second-order recompute forbidden; two passes (the
+    second runs with jet mode switched on)."""
+    from siren_amd.modules import SingleBVPNet
+    from siren_amd import loss_functions as LF
+    _no_torch_second_order(monkeypatch)
+    d = 2 if case == 'A' else 3
+    m = SingleBVPNet(in_features=d, hidden_features=512, verbose=False).to(cuda)
+    m.load_state_dict({k[len(case) + 3:]: torch.tensor(v) for k, v in g9.items() if k.startswith(case + '_w_')})
+    coords = to_dev(g9[case + '_coords'], cuda)
+    for _ in range(2):
+        m.zero_grad()
+        out = m({'coords': coords})
+        if case == 'A':
+            terms = LF.gradients_mse(out, {'gradients': to_dev(g9['A_gt_gradients'], cuda)})
+            key = 'A_gradients_mse_grad_'
+        else:
+            terms = LF.sdf(out, {'sdf': to_dev(g9['B_gt_sdf'], cuda), 'normals': to_dev(g9['B_gt_normals'], cuda)})
+            key = 'B_sdf_grad_'
+            for k, t in terms.items():
+                ref = manifest['G9_sdf_%s_f64' % k]
+                assert abs(float(t.mean()) - ref) <= 1e-4 * max(1., abs(ref)), k
+        sum(t.mean() for t in terms.values()).backward()
+        for k, p in m.named_parameters():
+            ref = g9[key + k]
+            assert np.max(np.abs(p.grad.cpu().numpy() - ref)) <= 1e-4 * np.max(np.abs(ref)) + 1e-12, k

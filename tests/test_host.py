@@ -57,7 +57,9 @@ def test_param_count_and_workspace(lib):
     assert lib.siren_param_count(ctypes.byref(wide), ctypes.byref(c)) == 0 and c.value == 791555
     assert lib.siren_workspace_floats(ctypes.byref(wide), ctypes.byref(c)) == 0
     assert c.value == 7168 + 2 * 3 * 32 * 8192          # small block padded to 1 KiB + 32 KiB slices
-    assert lib.siren_second_order_ws_floats(ctypes.byref(wide), 10, 1, ctypes.byref(c)) == _lib.SIREN_EUNSUPPORTED
+    # hidden 512 second order (the two-stream jet): a-, zb-, z-jets of 4 layers over 2 x 32 columns + slabs
+    assert lib.siren_second_order_ws_floats(ctypes.byref(wide), 10, 1, ctypes.byref(c)) == 0
+    assert c.value > 3 * 4 * 64 * 512
 
 
 def test_zero_coords_is_a_noop(lib):
@@ -183,7 +185,9 @@ def test_new_entry_points_validate_before_any_device_work(lib):
     assert lib.siren_adam_scratch_floats(ctypes.byref(cnt)) == 0 and cnt.value > 1024
     wide = _lib.SirenCfg(3, 512, 3, 3, 30., 30., 1, 0)
     assert lib.siren_second_order_ex(ctypes.byref(wide), None, None, 1, None, None, None, None, None, None, None,
-                                     None) == _lib.SIREN_EUNSUPPORTED
+                                     None) == _lib.SIREN_EINVAL   # hidden 512 is covered; NULL buffers are not
+    assert lib.siren_second_order_kept(ctypes.byref(wide), P(64), P(64), 1, P(64), None, P(64), P(64), P(64), None,
+                                       None) == _lib.SIREN_EUNSUPPORTED  # the kept forward is hidden 256 only
 
 
 def test_workspace_queries_at_zero_coords_and_caller_owned_scratch(lib):

@@ -14,6 +14,7 @@ Paths (BASELINE.json configs; F = 2 sum fan_in fan_out FLOP per coordinate, SURV
   hypernet     32 x 4096 coords, 5x256 d2 o1 per-element weights: grouped stored forward + grouped reverse-only W2
                (the hypernetwork training kernels, W2 = 3F)
   w1           5x256 d2 o1, 2^20 coords: the headline W1 launch (2F)
+  w3_wide      5x512 d3 o1, 2^18 coords: W3 H v + theta-grads at hidden 512 (two-stream jet + wgrad, 6F)
 """
 import argparse
 import json
@@ -33,6 +34,7 @@ PATHS = {  # name: (d, hidden, layers, o, n, work units of F)
     'w3_theta': (2, 256, 3, 1, 1 << 19, 6),
     'hypernet': (2, 256, 3, 1, 32 * 4096, 3),
     'w1': (2, 256, 3, 1, 1 << 20, 2),
+    'w3_wide': (3, 512, 3, 1, 1 << 18, 6),
 }
 
 
@@ -80,7 +82,7 @@ def build_step(name, dev):
             _, _, kept = eng.forward_grad_store(ws, x)
             eng.second_order(ws, x, v, want_theta=True, gy=gy, kept=kept)
         return step
-    if name == 'w3_theta':
+    if name in ('w3_theta', 'w3_wide'):
         v = torch.randn(n, d, device=dev, generator=g)
         return lambda: eng.second_order(ws, x, v, want_theta=True)
     gl = torch.randn(n, 1, device=dev, generator=g) / n
