@@ -50,7 +50,7 @@ void launch_jet_mix(dim3 grid, hipStream_t st, const float* ws, const float* x, 
                     float w, float* spill, float* abuf, float* dbuf, int64_t n_pad);
 void launch_small_mix(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* v,
                       const float* g, const float* u, int64_t n, int64_t n_pad, int64_t tps, float* eslab, int64_t E,
-                      int d, int o, int lh);
+                      int d, int o, int lh, int h);
 // tu_wide.hip: hidden width 512 (mode as siren_common.h MODE_*); spill = cos scratch for MODE_W1 / MODE_STORE
 void launch_wide(int mode, dim3 grid, hipStream_t st, const FusedArgs& a, float* spill);
 // tu_wide_jet.hip: second order at hidden 512 (two-stream jet: 8 coordinates x (value, tangent) per wave, 32 per
@@ -58,6 +58,9 @@ void launch_wide(int mode, dim3 grid, hipStream_t st, const FusedArgs& a, float*
 void launch_wide_jet2(dim3 grid, hipStream_t st, const float* ws, const float* x, const float* v, const float* gy,
                       const float* u, int64_t n, int d, int o, int lh, float w0, float w, float* gx, float* ydot,
                       float* spill, float* abuf, float* dbuf, int64_t n_pad);
+void launch_wide_mix(dim3 grid, hipStream_t st, const float* ws, const float* x, const float* v, const float* g,
+                     const float* u, int64_t n, int d, int o, int lh, float w0, float w, float* gx, float* gv,
+                     float* gu, float* spill, float* abuf, float* dbuf, int64_t n_pad);
 void launch_small_j2(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* v,
                      const float* gy, const float* u, int64_t n, int64_t n_pad, int64_t tps, float* eslab, int64_t E,
                      int d, int o, int lh);

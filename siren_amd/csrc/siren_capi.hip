@@ -543,12 +543,36 @@ int32_t siren_laplace_backward_stored(const siren_cfg* cfg, const float* ws, con
                         "siren_laplace_backward_stored (reduce)");
 }
 
+// hidden 512: the two-stream jet (wide_jet_kernel.hpp): a-, zb- and z-jets of L + 1 layers over 2 n_pad columns
+// (n_pad: 32 coordinates per workgroup), the split-K slabs and the edge slabs
+namespace {
+// ns = 2 (W3: 32 coordinates per workgroup) or 4 (the mixed jet of the third-order adjoint: 16)
+struct W3WidePlan {
+    int64_t n_pad, cols, tiles, splits, tps, buf_floats, eslab_off, partial_floats, total;
+    EdgeSplit es;
+    W3WidePlan(const siren_cfg* cfg, int64_t n, int ns = 2)
+        : es(cfg, (n + 64 / ns - 1) / (64 / ns) * (64 / ns) * ns / 16) {
+        n_pad = (n + 64 / ns - 1) / (64 / ns) * (64 / ns);
+        cols = ns * n_pad;
+        tiles = cols / 16;
+        const int64_t want = wgrad_splits(cfg);
+        splits = std::max<int64_t>(1, std::min(tiles, want));
+        tps = std::max<int64_t>(1, (tiles + splits - 1) / splits);
+        splits = std::max<int64_t>(1, (tiles + tps - 1) / tps);
+        buf_floats = (int64_t)(cfg->n_hidden + 1) * cols * cfg->hidden;
+        eslab_off = splits * param_count(cfg);
+        partial_floats = eslab_off + es.floats;
+        total = 3 * buf_floats + partial_floats;
+    }
+};
+}  // namespace
+
 // ---- third-order adjoint: the backward of a Hessian-vector-product node (jet_kernel.hpp MIX) -----------------
 namespace {
 int check_mix(const siren_cfg* cfg) {
     if (int rc = check_cfg(cfg, true)) return rc;
-    if (wide(cfg) || !cfg->outermost_linear || cfg->n_hidden > 5)
-        return fail(SIREN_EUNSUPPORTED, "siren_hvp_backward covers hidden 256, linear output, 1..5 hidden layers");
+    if (!cfg->outermost_linear || (!wide(cfg) && cfg->n_hidden > 5))
+        return fail(SIREN_EUNSUPPORTED, "siren_hvp_backward covers a linear output layer (hidden 256: 1..5 hidden layers)");
     return SIREN_OK;
 }
 }  // namespace
@@ -556,8 +580,35 @@ int check_mix(const siren_cfg* cfg) {
 int32_t siren_hvp_backward_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count) {
     if (int rc = check_mix(cfg)) return rc;
     if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
-    *count = JetPlan(cfg, n).total;
+    *count = wide(cfg) ? W3WidePlan(cfg, n, 4).total : JetPlan(cfg, n).total;
     return SIREN_OK;
+}
+
+// hidden 512: the four-stream mixed jet of wide_jet_kernel<4> (16 coordinates per workgroup), wgrad over 4 n_pad
+// columns (value-column bias), EDGE_MIX at h = 512
+static int32_t hvp_backward_wide(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
+                                 const float* u, const float* g, float* tws, float* gx, float* gparams, float* gv,
+                                 float* gu, void* stream) {
+    const W3WidePlan plan(cfg, n, 4);
+    const hipStream_t st = (hipStream_t)stream;
+    const int64_t P = param_count(cfg);
+    float* abuf = tws;
+    float* dbuf = abuf + plan.buf_floats;
+    float* spill = dbuf + plan.buf_floats;
+    float* partial = spill + plan.buf_floats;
+    siren::launch_wide_mix(dim3((unsigned)(plan.n_pad / 16)), st, ws, x, v, g, u, n, cfg->d_in, cfg->d_out,
+                           cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, gx, gv, gu, spill, abuf, dbuf, plan.n_pad);
+    if (int rc = hip_status("siren_hvp_backward (hidden 512 mixed jet)")) return rc;
+    if (gparams == nullptr) return SIREN_OK;
+    const unsigned quads = (unsigned)((cfg->hidden / 256) * (cfg->hidden / 256));
+    siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden, quads), st, abuf, dbuf, plan.cols,
+                        plan.tps, partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1, cfg->hidden, 1);
+    if (int rc = hip_status("siren_hvp_backward (hidden 512 wgrad)")) return rc;
+    siren::launch_small_mix(plan.es.grid(cfg), st, abuf, dbuf, x, v, g, u, n, plan.n_pad, plan.es.tps,
+                            partial + plan.eslab_off, plan.es.E, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden);
+    if (int rc = hip_status("siren_hvp_backward (hidden 512 small)")) return rc;
+    return finish_grads(cfg, st, partial, plan.splits, 0, partial + plan.eslab_off, plan.es, gparams,
+                        "siren_hvp_backward (hidden 512 reduce)");
 }
 
 int32_t siren_hvp_backward(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
@@ -574,6 +625,7 @@ int32_t siren_hvp_backward(const siren_cfg* cfg, const float* ws, const float* x
     }
     if (ws == nullptr || tws == nullptr || gx == nullptr || x == nullptr || v == nullptr || g == nullptr)
         return fail(SIREN_EINVAL, "ws/x/v/g/tws/gx is NULL");
+    if (wide(cfg)) return hvp_backward_wide(cfg, ws, x, n, v, u, g, tws, gx, gparams, gv, gu, stream);
     float* abuf = tws;
     float* dbuf = abuf + plan.buf_floats;
     float* spill = dbuf + plan.buf_floats;
@@ -586,7 +638,7 @@ int32_t siren_hvp_backward(const siren_cfg* cfg, const float* ws, const float* x
                         partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1, siren::H, 1);
     if (int rc = hip_status("siren_hvp_backward (wgrad)")) return rc;
     siren::launch_small_mix(plan.es.grid(cfg), st, abuf, dbuf, x, v, g, u, n, plan.n_pad, plan.es.tps,
-                            partial + plan.eslab_off, plan.es.E, cfg->d_in, cfg->d_out, cfg->n_hidden);
+                            partial + plan.eslab_off, plan.es.E, cfg->d_in, cfg->d_out, cfg->n_hidden, siren::H);
     if (int rc = hip_status("siren_hvp_backward (small)")) return rc;
     return finish_grads(cfg, st, partial, plan.splits, 0, partial + plan.eslab_off, plan.es, gparams,
                         "siren_hvp_backward (reduce)");
@@ -612,27 +664,6 @@ struct W3Plan {
 };
 }  // namespace
 
-// hidden 512: the two-stream jet (wide_jet_kernel.hpp): a-, zb- and z-jets of L + 1 layers over 2 n_pad columns
-// (n_pad: 32 coordinates per workgroup), the split-K slabs and the edge slabs
-namespace {
-struct W3WidePlan {
-    int64_t n_pad, cols, tiles, splits, tps, buf_floats, eslab_off, partial_floats, total;
-    EdgeSplit es;
-    W3WidePlan(const siren_cfg* cfg, int64_t n) : es(cfg, (n + 31) / 32 * 32 / 8) {
-        n_pad = (n + 31) / 32 * 32;
-        cols = 2 * n_pad;
-        tiles = cols / 16;
-        const int64_t want = wgrad_splits(cfg);
-        splits = std::max<int64_t>(1, std::min(tiles, want));
-        tps = std::max<int64_t>(1, (tiles + splits - 1) / splits);
-        splits = std::max<int64_t>(1, (tiles + tps - 1) / tps);
-        buf_floats = (int64_t)(cfg->n_hidden + 1) * cols * cfg->hidden;
-        eslab_off = splits * param_count(cfg);
-        partial_floats = eslab_off + es.floats;
-        total = 3 * buf_floats + partial_floats;
-    }
-};
-}  // namespace
 
 int32_t siren_second_order_ws_floats(const siren_cfg* cfg, int64_t n, int32_t want_theta, int64_t* count) {
     if (int rc = check_cfg(cfg, true)) return rc;

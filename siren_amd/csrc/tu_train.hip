@@ -38,10 +38,10 @@ void launch_small_jet(dim3 grid, hipStream_t st, const float* abuf, const float*
 
 void launch_small_mix(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* v,
                       const float* g, const float* u, int64_t n, int64_t n_pad, int64_t tps, float* eslab, int64_t E,
-                      int d, int o, int lh) {
+                      int d, int o, int lh, int h) {
     hipLaunchKernelGGL(edge_kernel<EDGE_MIX>, grid, dim3(edge_threads(EDGE_MIX)), 0, st, dbuf,
-                       abuf + (int64_t)lh * 4 * n_pad * H, NOF, NOF, x, v, g, u, n, n_pad / 4, tps, eslab, E, d, o, lh,
-                       H, (int64_t)0, (int64_t)0);
+                       abuf + (int64_t)lh * 4 * n_pad * h, NOF, NOF, x, v, g, u, n, n_pad / 4, tps, eslab, E, d, o, lh,
+                       h, (int64_t)0, (int64_t)0);
 }
 
 // rows: zb_0 jet (dbuf layer 0), a_L jet (abuf layer L) of the two-stream tiles (2 n_pad columns per layer, h = 512)

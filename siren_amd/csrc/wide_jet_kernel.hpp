@@ -61,19 +61,28 @@ __device__ __forceinline__ f32x4 jet2_sin_adjoint(const f32x4& u, const f32x4& z
     return out;
 }
 
-// grid.x = tiles of 32 coordinates (4 waves x 8); abuf / dbuf: a- / zb-jets of layers 0..L as 16-column tiles
-// [l][tile][neuron][16] with n_cols = 2 n_pad columns per layer; spill: z-jets lane-major, layer stride n_cols * 512
-__global__ __launch_bounds__(THREADS, 1) void wide_jet2_kernel(
+// NS = 4 (MIX): the third-order adjoint at hidden 512 (jet_kernel.hpp's mixed jet: streams value, tangent along v,
+// tangent along g, mixed second order; 4 coordinates per wave): the backward of the Hessian-vector-product node
+// h = sum_j u_j H_j v given its cotangent g (siren_hvp_backward); outputs gx (value lanes), gv = W0^T zb_0,v (out2)
+// and gu_j = D2 y_j[v, g] (out3), seed sum_j u_j Wout_j on the second-order stream.
+//
+// grid.x = tiles of 64 / NS coordinates (4 waves x 16 / NS); abuf / dbuf: a- / zb-jets of layers 0..L as 16-column
+// tiles [l][tile][neuron][16] with NS n_pad columns per layer; spill: z-jets lane-major, layer stride NS n_pad * 512.
+// NS = 2: tg unused, out2 = ydot (n, o), out3 unused. NS = 4: gy unused, out2 = gv (n, d), out3 = gu (n, o).
+template <int NS>
+__global__ __launch_bounds__(THREADS, 1) void wide_jet_kernel(
     const float* __restrict__ ws, const float* __restrict__ x, const float* __restrict__ v,
-    const float* __restrict__ gy, const float* __restrict__ u, int64_t n, int d, int o, int lh, float w0, float w,
-    float* __restrict__ gx, float* __restrict__ ydot, float* __restrict__ spill, float* __restrict__ abuf,
-    float* __restrict__ dbuf, int64_t n_pad) {
+    const float* __restrict__ tg, const float* __restrict__ gy, const float* __restrict__ u, int64_t n, int d, int o,
+    int lh, float w0, float w, float* __restrict__ gx, float* __restrict__ out2, float* __restrict__ out3,
+    float* __restrict__ spill, float* __restrict__ abuf, float* __restrict__ dbuf, int64_t n_pad) {
+    static_assert(NS == 2 || NS == 4, "two-stream (W3) or four-stream (mixed) jets");
+    constexpr int CPW = 16 / NS;  // coordinates per wave
     __shared__ __attribute__((aligned(16))) float lds[WNBUF * WSLICE + WSMALL_MAX];
     const SmallLayout L(WH);
     float* ring = lds;
     float* sm = lds + WNBUF * WSLICE;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int g = lane >> 4, c = lane & 15, js = c & 1;
+    const int g = lane >> 4, c = lane & 15, js = c % NS;
     const int npass = 2 * lh;
     const int nslices = npass * WNB;
     const float* stream = ws + L.pad(lh);
@@ -81,16 +90,33 @@ __global__ __launch_bounds__(THREADS, 1) void wide_jet2_kernel(
         const int nf4 = (L.floats(lh) + 3) / 4;
         for (int e = threadIdx.x; e < nf4; e += THREADS) ((f32x4*)sm)[e] = ((const f32x4*)ws)[e];
     }
-    const int64_t coord = (int64_t)blockIdx.x * 32 + wave * 8 + (c >> 1);
+    const int64_t coord = (int64_t)blockIdx.x * (WAVES * CPW) + wave * CPW + c / NS;
     const bool valid = coord < n;
     const int64_t wt = (int64_t)blockIdx.x * WAVES + wave;  // this wave's 16-column tile
-    const int64_t lstride = 2 * n_pad * WH;                   // floats per layer (2 n_pad columns)
+    const int64_t lstride = NS * n_pad * WH;                  // floats per layer (NS n_pad columns)
     const int64_t toff = wt * (WH * 16) + 4 * g * 16 + c;     // tile layout: tile + lane
     float* sp = spill + wt * (WH * 16) + lane * 4;            // scratch: lane-major blocks
     const float val = js == 0 ? 1.f : 0.f;
-    float jcf[MAXD];  // first-layer coefficient of W0[:, k]: x_k (value lanes) or v_k (tangent lanes)
+    // per-lane jet coefficients: first-layer coefficient of W0[:, k] (x_k on the value stream, the tangent's
+    // components on the tangent streams), the sine's stream factors and the adjoint's stream masks
+    float jcf[MAXD];
 #pragma unroll
-    for (int k = 0; k < MAXD; ++k) jcf[k] = (valid && k < d) ? (js == 0 ? x[coord * d + k] : v[coord * d + k]) : 0.f;
+    for (int k = 0; k < MAXD; ++k) {
+        const float* tp = (NS == 4 && js == 2) ? tg : v;
+        jcf[k] = (valid && k < d && js < 3) ? (js == 0 ? x[coord * d + k] : tp[coord * d + k]) : 0.f;
+    }
+    const float kb0 = js == 0 ? 0.f : w0, kb = js == 0 ? 0.f : w;
+    const float kg0 = (NS == 4 && js == 3) ? w0 * w0 : 0.f, kg = (NS == 4 && js == 3) ? w * w : 0.f;
+    const float m12 = (js == 1 || js == 2) ? 1.f : 0.f;
+    const bool s1 = js == 1;
+    auto jsin = [&](const f32x4& z, float wl, float kbl, float kgl) -> f32x4 {
+        if constexpr (NS == 2) return jet2_sin(z, wl, val, kbl);
+        else return jet_sin<true>(z, wl, val, kbl, kgl);
+    };
+    auto jadj = [&](const f32x4& uu, const f32x4& z, float wl) -> f32x4 {
+        if constexpr (NS == 2) return jet2_sin_adjoint(uu, z, wl, val);
+        else return jet_sin_adjoint<true>(uu, z, wl, val, m12, s1);
+    };
     __syncthreads();
     int s = 0;
     wring_issue(stream, ring, s, nslices, wave, lane);
@@ -106,7 +132,7 @@ __global__ __launch_bounds__(THREADS, 1) void wide_jet2_kernel(
         for (int k = 0; k < MAXD; ++k)
             if (k < d) z += jcf[k] * *(const f32x4*)(sm + L.w0 + k * WH + nb);
         *(f32x4*)(sp + rb * 256) = z;
-        act[rb] = jet2_sin(z, w0, val, w0 * (1.f - val));
+        act[rb] = jsin(z, w0, kb0, kg0);
     }
     wstore_tile(abuf + toff, act);
 
@@ -119,11 +145,11 @@ __global__ __launch_bounds__(THREADS, 1) void wide_jet2_kernel(
         const bool rev_pass = p >= lh;
         const float* zpre = rev_pass ? sp + (int64_t)(2 * lh - p - 1) * lstride : sp;
 #pragma unroll
-        for (int kb = 0; kb < WNB; ++kb) {
+        for (int kb2 = 0; kb2 < WNB; ++kb2) {
             wring_wait(s, nslices);
             wring_issue(stream, ring, s + 2, nslices, wave, lane);
-            slice_mma<WNB>(lds_addr(ring + (s % WNBUF) * WSLICE) + 16u * lane, act[kb], acc);
-            if (rev_pass) act[kb] = *(const f32x4*)(zpre + kb * 256);
+            slice_mma<WNB>(lds_addr(ring + (s % WNBUF) * WSLICE) + 16u * lane, act[kb2], acc);
+            if (rev_pass) act[kb2] = *(const f32x4*)(zpre + kb2 * 256);
             ++s;
         }
         if (p < lh) {
@@ -135,12 +161,15 @@ __global__ __launch_bounds__(THREADS, 1) void wide_jet2_kernel(
             for (int rb = 0; rb < WNB; ++rb) {
                 const f32x4 z = acc[rb] + val * *(const f32x4*)(bl + 16 * rb);
                 *(f32x4*)(zp + rb * 256) = z;
-                act[rb] = jet2_sin(z, w, val, w * (1.f - val));
+                act[rb] = jsin(z, w, kb, kg);
             }
             wstore_tile(abuf + (int64_t)l * lstride + toff, act);
             if (l == lh) {
-                // outputs: y_j (value lanes) and ydot_j = (J v)_j (tangent lanes); then the reverse seed
-                float wj_lane[MAXO];  // this lane's output weight: gy_j (value) or u_j (tangent)
+                // outputs per stream: NS = 2 ydot_j = (J v)_j on tangent lanes; NS = 4 gu_j = D2 y_j[v, g] on the
+                // second-order lanes; then the reverse seed with this lane's output weights
+                float wj_lane[MAXO];
+                constexpr int OUT_STREAM = NS == 2 ? 1 : 3;
+                float* outp = NS == 2 ? out2 : out3;
 #pragma unroll
                 for (int j = 0; j < MAXO; ++j) {
                     float pj = 0.f;
@@ -151,11 +180,15 @@ __global__ __launch_bounds__(THREADS, 1) void wide_jet2_kernel(
                             pj += wv[0] * act[rb][0] + wv[1] * act[rb][1] + wv[2] * act[rb][2] + wv[3] * act[rb][3];
                         }
                         pj = sum_groups(pj);
-                        if (valid && g == 0 && js == 1 && ydot != nullptr) ydot[coord * o + j] = pj;
+                        if (valid && g == 0 && js == OUT_STREAM && outp != nullptr) outp[coord * o + j] = pj;
                     }
-                    const float gj = (gy != nullptr && valid && j < o) ? gy[coord * o + j] : 0.f;
                     const float uj = (j < o) ? (u != nullptr ? (valid ? u[coord * o + j] : 0.f) : (valid ? 1.f : 0.f)) : 0.f;
-                    wj_lane[j] = js == 0 ? gj : uj;
+                    if constexpr (NS == 2) {
+                        const float gj = (gy != nullptr && valid && j < o) ? gy[coord * o + j] : 0.f;
+                        wj_lane[j] = js == 0 ? gj : uj;
+                    } else {
+                        wj_lane[j] = js == 3 ? uj : 0.f;
+                    }
                 }
 #pragma unroll
                 for (int rb = 0; rb < WNB; ++rb) {
@@ -163,7 +196,7 @@ __global__ __launch_bounds__(THREADS, 1) void wide_jet2_kernel(
                     const f32x4 ua = wj_lane[0] * *(const f32x4*)wo + wj_lane[1] * *(const f32x4*)(wo + WH) +
                                      wj_lane[2] * *(const f32x4*)(wo + 2 * WH) + wj_lane[3] * *(const f32x4*)(wo + 3 * WH);
                     const f32x4 z = acc[rb] + val * *(const f32x4*)(bl + 16 * rb);  // z_L jet, still in acc
-                    act[rb] = jet2_sin_adjoint(ua, z, w, val);
+                    act[rb] = jadj(ua, z, w);
                 }
                 wstore_tile(dbuf + (int64_t)lh * lstride + toff, act);
             }
@@ -172,12 +205,12 @@ __global__ __launch_bounds__(THREADS, 1) void wide_jet2_kernel(
             const int lm = 2 * lh - p - 1;
             const float wl = lm == 0 ? w0 : w;
 #pragma unroll
-            for (int rb = 0; rb < WNB; ++rb) act[rb] = jet2_sin_adjoint(acc[rb], act[rb], wl, val);
+            for (int rb = 0; rb < WNB; ++rb) act[rb] = jadj(acc[rb], act[rb], wl);
             wstore_tile(dbuf + (int64_t)lm * lstride + toff, act);
         }
     }
 
-    // ---- gx = W0^T zb_0 (value lanes) -------------------------------------------------------------------------------
+    // ---- gx = W0^T zb_0 (value lanes); NS = 4: gv = W0^T zb_0,v (stream-1 lanes) ------------------------------------
 #pragma unroll
     for (int k = 0; k < MAXD; ++k) {
         if (k < d) {
@@ -189,6 +222,7 @@ __global__ __launch_bounds__(THREADS, 1) void wide_jet2_kernel(
             }
             q = sum_groups(q);
             if (valid && g == 0 && js == 0) gx[coord * d + k] = q;
+            if (NS == 4 && out2 != nullptr && valid && g == 0 && js == 1) out2[coord * d + k] = q;
         }
     }
 }

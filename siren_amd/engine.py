@@ -53,9 +53,10 @@ class SirenEngine:
         # hidden 512: the two-stream jet kernel (wide_jet_kernel.hpp), 1..8 hidden layers
         self.second_order_supported = (self.supported and int(d_out) <= 4 and bool(outermost_linear)
                                        and ((int(hidden) == 256 and 1 <= n_hidden <= 3) or int(hidden) == 512))
-        # the third-order adjoint (mixed jet, siren_hvp_backward): hidden 256, linear output, 1..5 hidden layers
-        self.hvp_backward_supported = (self.supported and int(hidden) == 256 and 1 <= n_hidden <= 5
-                                       and bool(outermost_linear))
+        # the third-order adjoint (mixed jet, siren_hvp_backward): linear output, hidden 256 with 1..5 hidden layers
+        # or hidden 512 (wide_jet_kernel<4>)
+        self.hvp_backward_supported = (self.supported and bool(outermost_linear)
+                                       and ((int(hidden) == 256 and 1 <= n_hidden <= 5) or int(hidden) == 512))
 
     # ------------------------------------------------------------------------------------------------------
     def _require(self):
@@ -139,7 +140,8 @@ class SirenEngine:
         of sum_c <g_c, h_c>."""
         self._require()
         if not self.hvp_backward_supported:
-            raise _lib.SirenUnsupported('siren_hvp_backward covers hidden 256, linear output, 1..5 hidden layers')
+            raise _lib.SirenUnsupported('siren_hvp_backward covers a linear output, hidden 256 (1..5 hidden layers) '
+                                        'or hidden 512')
         x = self._check_x(x)
         n, d, o = x.shape[0], self.cfg.d_in, self.cfg.d_out
         for name, t, w in (('v', v, d), ('g', g, d), ('u', u, o)):
