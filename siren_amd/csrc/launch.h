@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace siren {
 
 struct FusedArgs {
@@ -86,6 +88,18 @@ void launch_reduce(dim3 grid, hipStream_t st, const float* partial, int64_t S, i
                    int64_t lo, int64_t hi, int64_t bstride_part = 0, int64_t begin = 0, int64_t end = -1);
 void launch_edge_reduce(dim3 grid, hipStream_t st, const float* eslab, int64_t SE, int64_t E, int64_t hidden0,
                         int64_t wout, float* gp, int64_t P, int64_t bstride_e);
+
+// layered.hip: hidden widths other than 256 / 512, layer by layer over coordinate chunks (rocBLAS GEMMs + fused
+// epilogues); the packed workspace = [params][chunk scratch]
+constexpr int64_t LAYERED_CHUNK = 16384;
+struct LayeredPlan {
+    int d, H, lh, o;
+    int64_t P, chunk, buf, scratch;
+    LayeredPlan(int d_, int H_, int lh_, int o_, int64_t n);
+};
+int64_t layered_ws_floats(int d, int H, int lh, int o);
+int layered_run(int mode, const LayeredPlan& plan, const float* ws, float w0, float w, const float* x, int64_t n,
+                const float* gy, float* y, float* gx, float* gparams, hipStream_t st, std::string& err);
 
 constexpr int STEP_BLOCKS = 1024;  // partial sums of the clip-norm pass (4 workgroups per CU)
 // tu_step.hip: device point-cloud sampling (dataio.py:420-442), clip_grad_norm_ + Adam over the flat bucket

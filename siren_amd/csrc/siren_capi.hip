@@ -27,12 +27,17 @@ int check_cfg(const siren_cfg* cfg, bool fused) {
     if (!std::isfinite(cfg->omega_first) || !std::isfinite(cfg->omega_hidden))
         return fail(SIREN_EINVAL, "omega values must be finite");
     if (fused) {
-        if (cfg->hidden != siren::H && cfg->hidden != 512)
-            return fail(SIREN_EUNSUPPORTED, "fused kernels need hidden_features 256 or 512");
+        const bool fused_h = cfg->hidden == siren::H || cfg->hidden == 512;
+        const bool layered_h = cfg->hidden % 64 == 0 && cfg->hidden >= 64 && cfg->hidden <= 4096;
+        if (!fused_h && !layered_h)
+            return fail(SIREN_EUNSUPPORTED, "hidden_features must be 256 / 512 (fused kernels) or a multiple of 64 in "
+                                            "[64, 4096] (layered path)");
         if (cfg->d_in > siren::MAXD) return fail(SIREN_EUNSUPPORTED, "fused kernels need in_features <= 4");
         if (cfg->d_out > siren::MAXO) return fail(SIREN_EUNSUPPORTED, "fused kernels need out_features <= 4");
-        if (cfg->n_hidden < 1 || cfg->n_hidden > siren::MAX_LH_FWD)
-            return fail(SIREN_EUNSUPPORTED, "fused kernels need 1 <= num_hidden_layers <= 8");
+        if (cfg->n_hidden < 1 || cfg->n_hidden > (fused_h ? siren::MAX_LH_FWD : 16))
+            return fail(SIREN_EUNSUPPORTED, "need 1 <= num_hidden_layers <= 8 (16 on the layered path)");
+        if (!fused_h && !cfg->outermost_linear)
+            return fail(SIREN_EUNSUPPORTED, "the layered path (hidden other than 256 / 512) needs a linear output layer");
     }
     return SIREN_OK;
 }
@@ -44,6 +49,12 @@ int hip_status(const char* what) {
 }
 
 bool wide(const siren_cfg* cfg) { return cfg->hidden == 512; }
+// hidden widths the fused kernels do not hold in registers: layer-by-layer over coordinate chunks (layered.hip)
+bool layered(const siren_cfg* cfg) { return cfg->hidden != siren::H && cfg->hidden != 512; }
+int layered_unsupported(const char* what) {
+    return fail(SIREN_EUNSUPPORTED, std::string(what) + " covers hidden 256 / 512 (the layered path of other widths "
+                                                        "runs W0, W1 and W2: siren_forward / _forward_grad / _backward)");
+}
 
 // packed workspace: small block + forward slices + transposed slices (16 x hidden floats each); at hidden 256 a
 // second, phase-scaled copy follows for w1_kernel (pack_kernel: weights and biases times w / 2 pi, so its
@@ -53,9 +64,23 @@ int64_t ws_base(const siren_cfg* cfg) {
     const int64_t h = cfg->hidden;
     return small_pad(cfg) + 2ll * cfg->n_hidden * (h / 16) * (16 * h);
 }
-int64_t ws_floats(const siren_cfg* cfg) { return wide(cfg) ? ws_base(cfg) : 2 * ws_base(cfg); }
+int64_t ws_floats(const siren_cfg* cfg) {
+    if (layered(cfg)) return siren::layered_ws_floats(cfg->d_in, cfg->hidden, cfg->n_hidden, cfg->d_out);
+    return wide(cfg) ? ws_base(cfg) : 2 * ws_base(cfg);
+}
 // the phase-scaled image needs w0, w != 0 (its reverse multipliers are w0 / s and 2 pi with s = w / 2 pi)
-bool w1_ok(const siren_cfg* cfg) { return !wide(cfg) && cfg->omega_first != 0.f && cfg->omega_hidden != 0.f; }
+bool w1_ok(const siren_cfg* cfg) {
+    return !wide(cfg) && !layered(cfg) && cfg->omega_first != 0.f && cfg->omega_hidden != 0.f;
+}
+int layered_call(int mode, const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* gy, float* y,
+                 float* gx, float* gp, void* stream, const char* what) {
+    const siren::LayeredPlan plan(cfg->d_in, cfg->hidden, cfg->n_hidden, cfg->d_out, n);
+    std::string err;
+    if (siren::layered_run(mode, plan, ws, cfg->omega_first, cfg->omega_hidden, x, n, gy, y, gx, gp,
+                           (hipStream_t)stream, err) != 0)
+        return fail(SIREN_EHIP, std::string(what) + ": " + err);
+    return hip_status(what);
+}
 const float* w1_ws(const siren_cfg* cfg, const float* ws) { return ws + ws_base(cfg); }
 constexpr float kInv2Pi = 0.159154943091895336f;
 
@@ -189,6 +214,10 @@ int32_t siren_workspace_floats(const siren_cfg* cfg, int64_t* count) {
 int32_t siren_pack(const siren_cfg* cfg, const float* params, float* ws, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (params == nullptr || ws == nullptr) return fail(SIREN_EINVAL, "params/ws is NULL");
+    if (layered(cfg)) {  // the parameters as they are; the rest of ws is the layered path's chunk scratch
+        (void)hipMemcpyAsync(ws, params, param_count(cfg) * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream);
+        return hip_status("siren_pack");
+    }
     siren::launch_pack(params, ws, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden, small_pad(cfg), ws_floats(cfg),
                        wide(cfg) ? 0 : ws_base(cfg), cfg->omega_first * kInv2Pi, cfg->omega_hidden * kInv2Pi,
                        (hipStream_t)stream);
@@ -203,6 +232,7 @@ int32_t siren_forward(const siren_cfg* cfg, const float* ws, const float* x, int
     const int64_t blocks = (n + siren::TILE - 1) / siren::TILE;
     if (blocks > 0x7fffffffll) return fail(SIREN_EINVAL, "n too large");
     const dim3 grid((unsigned)blocks);
+    if (layered(cfg)) return layered_call(0, cfg, ws, x, n, nullptr, y, nullptr, nullptr, stream, "siren_forward");
     siren::FusedArgs fa{ws, x, n, nullptr, y, nullptr, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first,
                         cfg->omega_hidden, cfg->outermost_linear ? 0 : 1, nullptr, nullptr, 0};
     if (wide(cfg))
@@ -229,11 +259,12 @@ int32_t siren_forward_grad_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* c
 int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* gy,
                            float* y, float* gx, float* tws, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
-    if (cfg->n_hidden > siren::MAX_LH_GRAD && !wide(cfg))
+    if (cfg->n_hidden > siren::MAX_LH_GRAD && !wide(cfg) && !layered(cfg))
         return fail(SIREN_EUNSUPPORTED, "siren_forward_grad needs 1 <= num_hidden_layers <= 3 at hidden 256");
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
     if (n == 0) return SIREN_OK;
     if (ws == nullptr || x == nullptr || gx == nullptr) return fail(SIREN_EINVAL, "ws/x/gx is NULL");
+    if (layered(cfg)) return layered_call(1, cfg, ws, x, n, gy, y, gx, nullptr, stream, "siren_forward_grad");
     const int64_t blocks = (n + siren::TILE - 1) / siren::TILE;
     if (blocks > 0x7fffffffll) return fail(SIREN_EINVAL, "n too large");
     const dim3 grid((unsigned)blocks);
@@ -287,7 +318,7 @@ int32_t siren_forward_laplace(const siren_cfg* cfg, const float* ws, const float
 int32_t siren_train_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
-    *count = TrainPlan(cfg, n).total;
+    *count = layered(cfg) ? 0 : TrainPlan(cfg, n).total;
     return SIREN_OK;
 }
 
@@ -295,9 +326,19 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
                        float* tws, void* reserved, float* gx, float* gparams, void* stream) {
     (void)reserved;
     if (int rc = check_cfg(cfg, true)) return rc;
-    if (cfg->n_hidden > siren::MAX_LH_GRAD && !wide(cfg))
+    if (cfg->n_hidden > siren::MAX_LH_GRAD && !wide(cfg) && !layered(cfg))
         return fail(SIREN_EUNSUPPORTED, "siren_backward needs 1 <= num_hidden_layers <= 3 at hidden 256");
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    if (layered(cfg)) {  // the chunk scratch lives in ws; tws is not used
+        if (n == 0) {  // empty tensors may carry NULL data pointers: only gparams is written
+            if (gparams == nullptr) return fail(SIREN_EINVAL, "gparams is NULL");
+            (void)hipMemsetAsync(gparams, 0, param_count(cfg) * sizeof(float), (hipStream_t)stream);
+            return hip_status("siren_backward");
+        }
+        if (ws == nullptr || x == nullptr || gy == nullptr || gx == nullptr || gparams == nullptr)
+            return fail(SIREN_EINVAL, "ws/x/gy/gx/gparams is NULL");
+        return layered_call(2, cfg, ws, x, n, gy, nullptr, gx, gparams, stream, "siren_backward");
+    }
     if (ws == nullptr || gy == nullptr || tws == nullptr || gx == nullptr || gparams == nullptr ||
         (n > 0 && x == nullptr))
         return fail(SIREN_EINVAL, "ws/x/gy/tws/gx/gparams is NULL");
@@ -337,7 +378,7 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
 
 // ---- stored-forward W2 split: the training forward keeps a_l and cos(w z_l) so the backward is reverse-only ----
 bool stored_ok(const siren_cfg* cfg) {
-    if (!cfg->outermost_linear || (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) != 0) return false;
+    if (!cfg->outermost_linear || (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) != 0 || layered(cfg)) return false;
     return wide(cfg) || (w1_ok(cfg) && cfg->n_hidden <= siren::MAX_LH_GRAD);
 }
 // stored-split workspace: [a_l tiles][delta_l tiles][partial slabs][hidden 512: cos scratch of L + 1 layers]
@@ -428,7 +469,7 @@ int32_t siren_backward_stored(const siren_cfg* cfg, const float* ws, const float
 namespace {
 int check_jet(const siren_cfg* cfg) {
     if (int rc = check_cfg(cfg, true)) return rc;
-    if (wide(cfg) || cfg->d_in > 2 || !cfg->outermost_linear || cfg->n_hidden > 5)
+    if (wide(cfg) || layered(cfg) || cfg->d_in > 2 || !cfg->outermost_linear || cfg->n_hidden > 5)
         return fail(SIREN_EUNSUPPORTED,
                     "the fused Laplacian covers hidden 256, in_features <= 2, linear output, 1..5 hidden layers");
     return SIREN_OK;
@@ -571,6 +612,7 @@ struct W3WidePlan {
 namespace {
 int check_mix(const siren_cfg* cfg) {
     if (int rc = check_cfg(cfg, true)) return rc;
+    if (layered(cfg)) return layered_unsupported("siren_hvp_backward");
     if (!cfg->outermost_linear || (!wide(cfg) && cfg->n_hidden > 5))
         return fail(SIREN_EUNSUPPORTED, "siren_hvp_backward covers a linear output layer (hidden 256: 1..5 hidden layers)");
     return SIREN_OK;
@@ -667,6 +709,7 @@ struct W3Plan {
 
 int32_t siren_second_order_ws_floats(const siren_cfg* cfg, int64_t n, int32_t want_theta, int64_t* count) {
     if (int rc = check_cfg(cfg, true)) return rc;
+    if (layered(cfg)) return layered_unsupported("siren_second_order");
     if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
     *count = wide(cfg) ? W3WidePlan(cfg, n).total : W3Plan(cfg, n, want_theta != 0).total;
     return SIREN_OK;
@@ -723,6 +766,7 @@ static int32_t second_order_impl(const siren_cfg* cfg, const float* ws, const fl
     if (int rc = check_cfg(cfg, true)) return rc;
     if (!cfg->outermost_linear)
         return fail(SIREN_EUNSUPPORTED, "siren_second_order needs a linear output layer");
+    if (layered(cfg)) return layered_unsupported("siren_second_order");
     if (wide(cfg)) {
         if (kept != nullptr) return fail(SIREN_EUNSUPPORTED, "the kept-forward W3 covers hidden 256");
         return second_order_wide(cfg, ws, x, n, v, u, gy, tws, gx, gparams, ydot, stream);
@@ -847,6 +891,11 @@ int32_t siren_pack_batched(const siren_cfg* cfg, const float* params, int64_t ba
     if (batch < 0 || batch > 65535) return fail(SIREN_EINVAL, "batch must be in [0, 65535]");
     if (batch == 0) return SIREN_OK;
     if (params == nullptr || ws == nullptr) return fail(SIREN_EINVAL, "params/ws is NULL");
+    if (layered(cfg)) {
+        for (int64_t b = 0; b < batch; ++b)
+            if (int rc = siren_pack(cfg, params + b * param_count(cfg), ws + b * ws_floats(cfg), stream)) return rc;
+        return SIREN_OK;
+    }
     siren::launch_pack(params, ws, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden, small_pad(cfg), ws_floats(cfg),
                        wide(cfg) ? 0 : ws_base(cfg), cfg->omega_first * kInv2Pi, cfg->omega_hidden * kInv2Pi,
                        (hipStream_t)stream, (int)batch, param_count(cfg));

@@ -40,14 +40,17 @@ class SirenEngine:
         self.supported = rc == _lib.SIREN_OK
         self.unsupported_reason = None if self.supported else self.lib.siren_last_error().decode()
         self.ws_floats = cnt.value if self.supported else 0
-        # hidden 256 keeps cos(w z_l) of every layer in registers (1..3 hidden layers); hidden 512 spills it
-        self.grad_supported = self.supported and (1 <= n_hidden <= 3 or int(hidden) == 512)
+        # hidden 256 keeps cos(w z_l) of every layer in registers (1..3 hidden layers); hidden 512 spills it; other
+        # widths run the layered path (layered.hip: rocBLAS layer GEMMs + fused epilogues, W0 / W1 / W2 only)
+        self.layered = int(hidden) not in (256, 512)
+        self.grad_supported = self.supported and (1 <= n_hidden <= 3 or int(hidden) == 512 or self.layered)
         # the W3 second-order kernel: hidden 256, d_out <= 4 (vector outputs via an output weighting), linear output
         # the W4 jet kernel (fused Laplacian): hidden 256, d_in <= 2, linear output, 1..5 hidden layers
         self.laplace_supported = (self.supported and int(hidden) == 256 and int(d_in) <= 2 and 1 <= n_hidden <= 5
                                   and bool(outermost_linear) and omega_first != 0 and omega_hidden != 0)
         # stored-forward W2 split: training forward keeps a_l / cos, backward is reverse-only
         self.stored_supported = (self.supported and bool(outermost_linear) and not (int(flags) & 1) and
+                                 not self.layered and
                                  (int(hidden) == 512 or (1 <= n_hidden <= 3 and omega_first != 0
                                                          and omega_hidden != 0)))
         # hidden 512: the two-stream jet kernel (wide_jet_kernel.hpp), 1..8 hidden layers

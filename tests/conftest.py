@@ -100,3 +100,8 @@ def g8():
 @pytest.fixture(scope='session')
 def g9():
     return load_golden('g9')
+
+
+@pytest.fixture(scope='session')
+def g10():
+    return load_golden('g10')

@@ -25,6 +25,9 @@ Fixtures:
       init weights, forward output, coords gradient (and Laplacian, image-mse theta-grads) in fp32 and fp64.
   G9  second order at hidden 512 (a G4-style pin for the hidden-512 W3): SingleBVPNet(hidden_features=512) seed 0,
       d2 o1 gradients_mse (1024 coords) and d3 o1 sdf (512 on + 512 off surface): gradient and fp64 theta-grads.
+  G10 hidden 1024 (the reference's train_video.py width): SingleBVPNet(in 3, out 3, hidden 1024) seed 0, 512 coords:
+      parameter checksums (fp64 sums + first rows: the init pin without 12 MB of weights), model_out / gradient (fp32
+      and fp64) and a slice of the fp64 image_mse theta-grads (first / output layers whole, 4 rows of every hidden W).
   G6  vector outputs / PML losses: 5x256 d2 o2 (helmholtz_pml, loss_functions.py:139-211)
       and 5x256 d3 o1 (wave_pml, loss_functions.py:112-136), 1024 coords each: jacobian / hessian
       (diff_operators.py:5-24, 46-59), the loss terms and their fp64 theta-grads.
@@ -321,6 +324,31 @@ def make_g9(modules, D, L, meta):
     np.savez_compressed(os.path.join(OUT, 'golden_g9.npz'), **store)
 
 
+def make_g10(modules, D, L, meta):
+    store = {}
+    gen = torch.Generator().manual_seed(10)
+    coords = torch.rand(1, 512, 3, generator=gen) * 2 - 1
+    gt = 0.5 + 0.5 * torch.sin(3 * coords + torch.tensor([0., 1., 2.]))
+    store['coords'], store['gt_img'] = coords.numpy(), gt.numpy()
+    torch.manual_seed(0)
+    net = modules.SingleBVPNet(type='sine', in_features=3, out_features=3, hidden_features=1024, num_hidden_layers=3)
+    for k, v in net.state_dict().items():
+        a = v.numpy()
+        store['sum_' + k] = np.array(a.astype(np.float64).sum())
+        store['head_' + k] = a.reshape(a.shape[0], -1)[:4].copy() if a.ndim == 2 else a[:16].copy()
+    for dtype, tag in ((torch.float32, 'f32'), (torch.float64, 'f64')):
+        net = net.to(dtype)
+        out = net({'coords': coords.to(dtype)})
+        store['G10_model_out_' + tag] = out['model_out'].detach().numpy()
+        store['G10_gradient_' + tag] = D.gradient(out['model_out'], out['model_in']).detach().numpy()
+        if tag == 'f64':
+            grads, total = grads_of(net, L.image_mse(None, out, {'img': gt.to(dtype)}))
+            meta['G10_image_mse_f64'] = total
+            for k, g in grads.items():
+                store['G10_grad_' + k] = g if (g.ndim == 1 or g.shape[0] <= 4 or g.shape[1] <= 4) else g[:4].copy()
+    np.savez_compressed(os.path.join(OUT, 'golden_g10.npz'), **store)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--skip-fit', action='store_true', help='reuse the G5 weights already in golden_fit.npz')
@@ -331,7 +359,7 @@ def main():
         with open(os.path.join(OUT, 'manifest.json')) as f:
             meta = json.load(f)
         for name in args.only.split(','):
-            {'g6': make_g6, 'g7': make_g7, 'g8': make_g8, 'g9': make_g9}[name](modules, D, L, meta)
+            {'g6': make_g6, 'g7': make_g7, 'g8': make_g8, 'g9': make_g9, 'g10': make_g10}[name](modules, D, L, meta)
         with open(os.path.join(OUT, 'manifest.json'), 'w') as f:
             json.dump(meta, f, indent=1, sort_keys=True)
         return

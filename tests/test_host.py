@@ -49,9 +49,18 @@ def test_param_count_and_workspace(lib):
     assert lib.siren_workspace_floats(ctypes.byref(cfg), ctypes.byref(c)) == 0
     assert c.value == 2 * (4096 + 2 * 3 * 16 * 4096)  # unscaled image + the W1 kernel's phase-scaled copy
     assert lib.siren_train_ws_floats(ctypes.byref(cfg), 1000, ctypes.byref(c)) == 0 and c.value > 0
-    bad = _lib.SirenCfg(2, 128, 3, 1, 30., 30., 1, 0)
+    bad = _lib.SirenCfg(2, 100, 3, 1, 30., 30., 1, 0)   # not a multiple of 64: no kernel path
     assert lib.siren_workspace_floats(ctypes.byref(bad), ctypes.byref(c)) == _lib.SIREN_EUNSUPPORTED
     assert b'256' in lib.siren_last_error()
+    # hidden 1024 (train_video.py's width): the layered path; ws = the parameters + the chunk scratch
+    big = _lib.SirenCfg(3, 1024, 3, 3, 30., 30., 1, 0)
+    assert lib.siren_param_count(ctypes.byref(big), ctypes.byref(c)) == 0
+    P = c.value
+    assert lib.siren_workspace_floats(ctypes.byref(big), ctypes.byref(c)) == 0
+    assert c.value == P + (2 * 4 + 2) * 16384 * 1024 + 16384
+    fs = _lib.SirenCfg(3, 1024, 3, 3, 30., 30., 0, 0)   # final sine: not on the layered path
+    assert lib.siren_workspace_floats(ctypes.byref(fs), ctypes.byref(c)) == _lib.SIREN_EUNSUPPORTED
+    assert lib.siren_second_order_ws_floats(ctypes.byref(big), 10, 1, ctypes.byref(c)) == _lib.SIREN_EUNSUPPORTED
     assert lib.siren_param_count(None, ctypes.byref(c)) == _lib.SIREN_EINVAL
     wide = _lib.SirenCfg(3, 512, 3, 3, 30., 30., 1, 0)
     assert lib.siren_param_count(ctypes.byref(wide), ctypes.byref(c)) == 0 and c.value == 791555

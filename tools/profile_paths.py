@@ -35,6 +35,8 @@ PATHS = {  # name: (d, hidden, layers, o, n, work units of F)
     'hypernet': (2, 256, 3, 1, 32 * 4096, 3),
     'w1': (2, 256, 3, 1, 1 << 20, 2),
     'w3_wide': (3, 512, 3, 1, 1 << 18, 6),
+    'video1024': (3, 1024, 3, 3, 1 << 18, 3),   # the layered path (train_video.py's width)
+    'fwd1024': (3, 1024, 3, 3, 1 << 18, 1),
 }
 
 
@@ -70,6 +72,13 @@ def build_step(name, dev):
     gy = torch.randn(n, o, device=dev, generator=g)
     if name == 'w1':
         return lambda: eng.forward_grad(ws, x)
+    if name == 'fwd1024':
+        return lambda: eng.forward(ws, x)
+    if name == 'video1024':
+        def step():
+            eng.forward(ws, x)
+            eng.backward_params(ws, x, gy)
+        return step
     if name in ('image_w2', 'video'):
         def step():
             _, tws = eng.forward_store(ws, x)
