@@ -402,12 +402,20 @@ def dp_train_rates(device, world, rank, steps=5, warmup=2):
             opt.allreduce_grad(world, nv)
         opt.step()
     res['video_5x512_d3o3'] = timed(video_step, nv, opt)
+    # the same loop at train_video.py's own width (hidden_features=1024, experiment_scripts/train_video.py): the
+    # layered path (layered.hip: rocBLAS layer GEMMs + fused epilogues, stored-forward split)
+    torch.manual_seed(0)
+    m = SingleBVPNet(in_features=3, out_features=3, hidden_features=1024, verbose=False).to(device)
+    sd.broadcast_parameters(m)
+    opt = FusedAdam(m.parameters(), lr=1e-4)
+    res['video_5x1024_d3o3'] = timed(video_step, nv, opt)
     del m, opt, mgrid, vid
     torch.cuda.empty_cache()
     return res
 
 
-PATH_UNITS = {'w1': 2, 'image_w2': 3, 'sdf': 8, 'video': 3, 'poisson': 15, 'poisson_ref': 15, 'hypernet': 3}
+PATH_UNITS = {'w1': 2, 'image_w2': 3, 'sdf': 8, 'video': 3, 'video1024': 3, 'poisson': 15, 'poisson_ref': 15,
+              'hypernet': 3}
 
 
 def path_rooflines(rates):
@@ -539,6 +547,7 @@ def main():
             'image_w2': extra['w2_image_mse_train_mcoords_s'],
             'sdf': dpr.get('sdf_5x256_d3', {}).get('mcoords_s') if n_ranks == 1 else None,
             'video': dpr.get('video_5x512_d3o3', {}).get('mcoords_s') if n_ranks == 1 else None,
+            'video1024': dpr.get('video_5x1024_d3o3', {}).get('mcoords_s') if n_ranks == 1 else None,
             'poisson': cr['poisson_512sq_laplace_mse_train_mcoords_s'],
             'poisson_ref': cr['poisson_512sq_reference_recipe_laplace_mse_train_mcoords_s'],
             'hypernet': cr['hypernet_b32x4096_grouped_w2_train_mcoords_s']})

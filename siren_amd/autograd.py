@@ -65,7 +65,7 @@ class SirenFunction(torch.autograd.Function):
     def forward(ctx, engine, jet, x, flat, store=False):
         ws = engine.pack(flat)
         ctx.tws = None
-        if store and engine.stored_supported and STORED_FORWARD:
+        if store and engine.stored_for(x.shape[0]) and STORED_FORWARD:
             # training forward: keep a_l / cos(w z_l) so the weight-gradient backward is reverse-only
             y, ctx.tws = engine.forward_store(ws, x)
         else:
@@ -257,7 +257,7 @@ class SirenBatchedFunction(torch.autograd.Function):
     def forward(ctx, engine, x, flat, store=False):
         ws = engine.pack_batched(flat)
         ctx.tws = None
-        if store and engine.stored_supported and STORED_FORWARD:
+        if store and engine.stored_for(x.shape[1], x.shape[0]) and STORED_FORWARD:
             # training under a hypernetwork: keep every element's a_l / cos, the backward is reverse-only
             y, ctx.tws = engine.forward_store_batched(ws, x)
         else:

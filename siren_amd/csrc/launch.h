@@ -92,14 +92,24 @@ void launch_edge_reduce(dim3 grid, hipStream_t st, const float* eslab, int64_t S
 // layered.hip: hidden widths other than 256 / 512, layer by layer over coordinate chunks (rocBLAS GEMMs + fused
 // epilogues); the packed workspace = [params][chunk scratch]
 constexpr int64_t LAYERED_CHUNK = 16384;
+constexpr int LAYERED_RPB = 64;  // rows per workgroup of the bias-reducing epilogues (slab rows = chunk / 64)
+enum LayeredMode : int {
+    LAY_FWD = 1,    // run the forward sweep
+    LAY_Y = 2,      // write y
+    LAY_GX = 4,     // vjp_x: gx = sum_j gy_j dPhi_j/dx
+    LAY_THETA = 8,  // parameter gradients
+    LAY_TWS = 16,   // a_l / cos_l of every layer live in the caller's n x H buffers (stored-forward split)
+};
 struct LayeredPlan {
     int d, H, lh, o;
-    int64_t P, chunk, buf, scratch;
+    int64_t P, P_pad, chunk, buf, R, wt, scratch;
     LayeredPlan(int d_, int H_, int lh_, int o_, int64_t n);
 };
 int64_t layered_ws_floats(int d, int H, int lh, int o);
+void layered_pack(const LayeredPlan& plan, const float* params, float* ws, hipStream_t st);
+inline int64_t layered_stored_floats(int H, int lh, int64_t n) { return 2 * (int64_t)(lh + 1) * n * H; }
 int layered_run(int mode, const LayeredPlan& plan, const float* ws, float w0, float w, const float* x, int64_t n,
-                const float* gy, float* y, float* gx, float* gparams, hipStream_t st, std::string& err);
+                const float* gy, float* y, float* gx, float* gparams, float* tws, hipStream_t st, std::string& err);
 
 constexpr int STEP_BLOCKS = 1024;  // partial sums of the clip-norm pass (4 workgroups per CU)
 // tu_step.hip: device point-cloud sampling (dataio.py:420-442), clip_grad_norm_ + Adam over the flat bucket

@@ -73,10 +73,10 @@ bool w1_ok(const siren_cfg* cfg) {
     return !wide(cfg) && !layered(cfg) && cfg->omega_first != 0.f && cfg->omega_hidden != 0.f;
 }
 int layered_call(int mode, const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* gy, float* y,
-                 float* gx, float* gp, void* stream, const char* what) {
+                 float* gx, float* gp, float* tws, void* stream, const char* what) {
     const siren::LayeredPlan plan(cfg->d_in, cfg->hidden, cfg->n_hidden, cfg->d_out, n);
     std::string err;
-    if (siren::layered_run(mode, plan, ws, cfg->omega_first, cfg->omega_hidden, x, n, gy, y, gx, gp,
+    if (siren::layered_run(mode, plan, ws, cfg->omega_first, cfg->omega_hidden, x, n, gy, y, gx, gp, tws,
                            (hipStream_t)stream, err) != 0)
         return fail(SIREN_EHIP, std::string(what) + ": " + err);
     return hip_status(what);
@@ -214,8 +214,9 @@ int32_t siren_workspace_floats(const siren_cfg* cfg, int64_t* count) {
 int32_t siren_pack(const siren_cfg* cfg, const float* params, float* ws, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (params == nullptr || ws == nullptr) return fail(SIREN_EINVAL, "params/ws is NULL");
-    if (layered(cfg)) {  // the parameters as they are; the rest of ws is the layered path's chunk scratch
-        (void)hipMemcpyAsync(ws, params, param_count(cfg) * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream);
+    if (layered(cfg)) {  // the parameters as they are + W_l^T; the rest of ws is the layered path's chunk scratch
+        siren::layered_pack(siren::LayeredPlan(cfg->d_in, cfg->hidden, cfg->n_hidden, cfg->d_out, -1), params, ws,
+                            (hipStream_t)stream);
         return hip_status("siren_pack");
     }
     siren::launch_pack(params, ws, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden, small_pad(cfg), ws_floats(cfg),
@@ -232,7 +233,8 @@ int32_t siren_forward(const siren_cfg* cfg, const float* ws, const float* x, int
     const int64_t blocks = (n + siren::TILE - 1) / siren::TILE;
     if (blocks > 0x7fffffffll) return fail(SIREN_EINVAL, "n too large");
     const dim3 grid((unsigned)blocks);
-    if (layered(cfg)) return layered_call(0, cfg, ws, x, n, nullptr, y, nullptr, nullptr, stream, "siren_forward");
+    if (layered(cfg)) return layered_call(siren::LAY_FWD | siren::LAY_Y, cfg, ws, x, n, nullptr, y, nullptr, nullptr,
+                                          nullptr, stream, "siren_forward");
     siren::FusedArgs fa{ws, x, n, nullptr, y, nullptr, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first,
                         cfg->omega_hidden, cfg->outermost_linear ? 0 : 1, nullptr, nullptr, 0};
     if (wide(cfg))
@@ -264,7 +266,9 @@ int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
     if (n == 0) return SIREN_OK;
     if (ws == nullptr || x == nullptr || gx == nullptr) return fail(SIREN_EINVAL, "ws/x/gx is NULL");
-    if (layered(cfg)) return layered_call(1, cfg, ws, x, n, gy, y, gx, nullptr, stream, "siren_forward_grad");
+    if (layered(cfg))
+        return layered_call(siren::LAY_FWD | siren::LAY_Y | siren::LAY_GX, cfg, ws, x, n, gy, y, gx, nullptr, nullptr,
+                            stream, "siren_forward_grad");
     const int64_t blocks = (n + siren::TILE - 1) / siren::TILE;
     if (blocks > 0x7fffffffll) return fail(SIREN_EINVAL, "n too large");
     const dim3 grid((unsigned)blocks);
@@ -337,7 +341,8 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
         }
         if (ws == nullptr || x == nullptr || gy == nullptr || gx == nullptr || gparams == nullptr)
             return fail(SIREN_EINVAL, "ws/x/gy/gx/gparams is NULL");
-        return layered_call(2, cfg, ws, x, n, gy, nullptr, gx, gparams, stream, "siren_backward");
+        return layered_call(siren::LAY_FWD | siren::LAY_GX | siren::LAY_THETA, cfg, ws, x, n, gy, nullptr, gx,
+                            gparams, nullptr, stream, "siren_backward");
     }
     if (ws == nullptr || gy == nullptr || tws == nullptr || gx == nullptr || gparams == nullptr ||
         (n > 0 && x == nullptr))
@@ -378,11 +383,11 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
 
 // ---- stored-forward W2 split: the training forward keeps a_l and cos(w z_l) so the backward is reverse-only ----
 bool stored_ok(const siren_cfg* cfg) {
-    if (!cfg->outermost_linear || (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) != 0 || layered(cfg)) return false;
-    return wide(cfg) || (w1_ok(cfg) && cfg->n_hidden <= siren::MAX_LH_GRAD);
+    if (!cfg->outermost_linear || (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) != 0) return false;
+    return wide(cfg) || layered(cfg) || (w1_ok(cfg) && cfg->n_hidden <= siren::MAX_LH_GRAD);
 }
 // stored-split workspace: [a_l tiles][delta_l tiles][partial slabs][hidden 512: cos scratch of L + 1 layers]
-// [hidden 256: lane-major cos of L + 1 layers]
+// [hidden 256: lane-major cos of L + 1 layers]; layered path: [a_0..a_L][cos_0..cos_L], n x H rows each
 float* stored_cos(const siren_cfg* cfg, const TrainPlan& plan, float* tws) {
     return wide(cfg) ? tws + 2 * plan.act_floats + plan.partial_floats : tws + plan.total;
 }
@@ -393,6 +398,10 @@ int32_t siren_train_stored_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* c
         return fail(SIREN_EUNSUPPORTED, "the stored-forward W2 split needs a linear output layer (hidden 256: 1..3 "
                                         "hidden layers)");
     if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
+    if (layered(cfg)) {
+        *count = siren::layered_stored_floats(cfg->hidden, cfg->n_hidden, n);
+        return SIREN_OK;
+    }
     const TrainPlan plan(cfg, n);
     // hidden 256: + the lane-major cos buffer (L + 1 layers, the size of the a_l tiles); hidden 512: the cos
     // scratch grows from L to L + 1 layers
@@ -408,6 +417,9 @@ int32_t siren_forward_store(const siren_cfg* cfg, const float* ws, const float* 
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
     if (n == 0) return SIREN_OK;
     if (ws == nullptr || x == nullptr || y == nullptr || tws == nullptr) return fail(SIREN_EINVAL, "ws/x/y/tws is NULL");
+    if (layered(cfg))
+        return layered_call(siren::LAY_FWD | siren::LAY_Y | siren::LAY_TWS, cfg, ws, x, n, nullptr, y, nullptr,
+                            nullptr, tws, stream, "siren_forward_store");
     const TrainPlan plan(cfg, n);
     float* abuf = tws;
     float* cbuf = stored_cos(cfg, plan, tws);
@@ -430,9 +442,17 @@ int32_t siren_backward_stored(const siren_cfg* cfg, const float* ws, const float
     if (!stored_ok(cfg))
         return fail(SIREN_EUNSUPPORTED, "the stored-forward W2 split covers hidden 256, linear output, 1..3 hidden layers");
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    if (n == 0 && layered(cfg)) {  // empty tensors may carry NULL data pointers: only gparams is written
+        if (gparams == nullptr) return fail(SIREN_EINVAL, "gparams is NULL");
+        (void)hipMemsetAsync(gparams, 0, param_count(cfg) * sizeof(float), (hipStream_t)stream);
+        return hip_status("siren_backward_stored");
+    }
     if (ws == nullptr || gy == nullptr || tws == nullptr || gx == nullptr || gparams == nullptr ||
         (n > 0 && x == nullptr))
         return fail(SIREN_EINVAL, "ws/x/gy/tws/gx/gparams is NULL");
+    if (layered(cfg))
+        return layered_call(siren::LAY_GX | siren::LAY_THETA | siren::LAY_TWS, cfg, ws, x, n, gy, nullptr, gx, gparams,
+                            tws, stream, "siren_backward_stored");
     const TrainPlan plan(cfg, n);
     const hipStream_t st = (hipStream_t)stream;
     const int64_t P = param_count(cfg);
@@ -825,15 +845,17 @@ int32_t siren_second_order_ex(const siren_cfg* cfg, const float* ws, const float
 int32_t siren_second_order_kept(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* v,
                                 const float* gy, float* kept, float* tws, float* gx, float* gparams, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
-    if (!stored_ok(cfg) || wide(cfg)) return fail(SIREN_EUNSUPPORTED, "siren_second_order_kept covers hidden 256");
+    if (!stored_ok(cfg) || wide(cfg) || layered(cfg))
+        return fail(SIREN_EUNSUPPORTED, "siren_second_order_kept covers hidden 256");
     if (kept == nullptr) return fail(SIREN_EINVAL, "kept is NULL");
     return second_order_impl(cfg, ws, x, n, v, nullptr, gy, tws, gx, gparams, nullptr, kept, stream);
 }
 
 int32_t siren_forward_grad_store(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y,
                                  float* gx, float* tws, void* stream) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (wide(cfg) || layered(cfg)) return fail(SIREN_EUNSUPPORTED, "siren_forward_grad_store covers hidden 256");
     if (int rc = siren_forward_store(cfg, ws, x, n, y, tws, stream)) return rc;
-    if (wide(cfg)) return fail(SIREN_EUNSUPPORTED, "siren_forward_grad_store covers hidden 256");
     if (n == 0) return SIREN_OK;
     if (gx == nullptr) return fail(SIREN_EINVAL, "gx is NULL");
     const TrainPlan plan(cfg, n);

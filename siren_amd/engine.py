@@ -49,10 +49,10 @@ class SirenEngine:
         self.laplace_supported = (self.supported and int(hidden) == 256 and int(d_in) <= 2 and 1 <= n_hidden <= 5
                                   and bool(outermost_linear) and omega_first != 0 and omega_hidden != 0)
         # stored-forward W2 split: training forward keeps a_l / cos, backward is reverse-only
+        # (layered widths: a_l / cos_l of every layer over all n rows, see stored_for)
         self.stored_supported = (self.supported and bool(outermost_linear) and not (int(flags) & 1) and
-                                 not self.layered and
-                                 (int(hidden) == 512 or (1 <= n_hidden <= 3 and omega_first != 0
-                                                         and omega_hidden != 0)))
+                                 (int(hidden) == 512 or self.layered or (1 <= n_hidden <= 3 and omega_first != 0
+                                                                         and omega_hidden != 0)))
         # hidden 512: the two-stream jet kernel (wide_jet_kernel.hpp), 1..8 hidden layers
         self.second_order_supported = (self.supported and int(d_out) <= 4 and bool(outermost_linear)
                                        and ((int(hidden) == 256 and 1 <= n_hidden <= 3) or int(hidden) == 512))
@@ -60,6 +60,17 @@ class SirenEngine:
         # or hidden 512 (wide_jet_kernel<4>)
         self.hvp_backward_supported = (self.supported and bool(outermost_linear)
                                        and ((int(hidden) == 256 and 1 <= n_hidden <= 5) or int(hidden) == 512))
+
+    # the layered path's stored split keeps 2 (L + 1) n H floats; above this it recomputes the forward per chunk
+    STORED_LAYERED_MAX_BYTES = 64 << 30
+
+    def stored_for(self, n, batch=1):
+        """Whether a training forward over n coordinates (x batch elements) keeps its activations for the backward."""
+        if not self.stored_supported:
+            return False
+        if not self.layered:
+            return True
+        return 8 * (self.cfg.n_hidden + 1) * int(n) * self.cfg.hidden * int(batch) <= self.STORED_LAYERED_MAX_BYTES
 
     # ------------------------------------------------------------------------------------------------------
     def _require(self):

@@ -83,6 +83,14 @@ def test_layered_backward_vs_fp64(cuda, n, d, L, o, H):
     # deterministic (rocBLAS with atomics off, fixed chunk order)
     gx2, gp2 = eng.backward_params(ws, to_dev(x, cuda), to_dev(gy, cuda))
     assert torch.equal(gp, gp2) and torch.equal(gx, gx2)
+    # the stored split (training forward keeps a_l / cos_l of all n rows, the backward skips the forward GEMMs):
+    # the same per-chunk operations, so the same bits
+    assert eng.stored_for(n)
+    y, tws = eng.forward_store(ws, to_dev(x, cuda))
+    ry = O.forward(x, layers)
+    assert np.max(np.abs(y.cpu().numpy() - ry)) <= tol(ry)
+    gx3, gp3 = eng.backward_stored(ws, to_dev(x, cuda), to_dev(gy, cuda), tws)
+    assert torch.equal(gp, gp3) and torch.equal(gx, gx3)
 
 
 def test_layered_n0(cuda):
@@ -93,6 +101,9 @@ def test_layered_n0(cuda):
     assert eng.forward(ws, z).shape == (0, 1)
     gx, gp = eng.backward_params(ws, z, torch.empty(0, 1, device=cuda))
     assert gx.shape == (0, 2) and float(gp.abs().max()) == 0.
+    y, tws = eng.forward_store(ws, z)
+    gx, gp = eng.backward_stored(ws, z, torch.empty(0, 1, device=cuda), tws)
+    assert y.shape == (0, 1) and gx.shape == (0, 2) and float(gp.abs().max()) == 0.
 
 
 def test_reference_hidden1024_g10(cuda, g10):

@@ -57,7 +57,13 @@ def test_param_count_and_workspace(lib):
     assert lib.siren_param_count(ctypes.byref(big), ctypes.byref(c)) == 0
     P = c.value
     assert lib.siren_workspace_floats(ctypes.byref(big), ctypes.byref(c)) == 0
-    assert c.value == P + (2 * 4 + 2) * 16384 * 1024 + 16384
+    # [params, 256-byte aligned][W_l^T x 3][a_l, cos_l x 4 layers][u x 2] chunks of 16384 x 1024 + column-sum slabs
+    # (4 bias + 3 dWout + 3 dW0 matrices of 256 rows x 1024, dbout 256 x 3)
+    assert c.value == ((P + 63) // 64 * 64 + 3 * 1024 * 1024 + (2 * 4 + 2) * 16384 * 1024 + (4 + 3 + 3) * 256 * 1024
+                       + 256 * 3)
+    # the stored split keeps a_l / cos_l of every layer over all n rows
+    assert lib.siren_train_stored_ws_floats(ctypes.byref(big), 1000, ctypes.byref(c)) == 0
+    assert c.value == 2 * 4 * 1000 * 1024
     fs = _lib.SirenCfg(3, 1024, 3, 3, 30., 30., 0, 0)   # final sine: not on the layered path
     assert lib.siren_workspace_floats(ctypes.byref(fs), ctypes.byref(c)) == _lib.SIREN_EUNSUPPORTED
     assert lib.siren_second_order_ws_floats(ctypes.byref(big), 10, 1, ctypes.byref(c)) == _lib.SIREN_EUNSUPPORTED

@@ -22,7 +22,7 @@ PEAK_TF, HBM_GBS = 157.3, 8000.
 
 
 def short(name):
-    m = re.match(r'(?:void )?siren::(\w+)(<[^(]*>)?', name)
+    m = re.match(r'(?:void )?siren::(?:\(anonymous namespace\)::)?(\w+)(<[^(]*>)?', name)
     if not m:
         return name[:60]
     return m.group(1) + (m.group(2).replace(' ', '') if m.group(2) else '')
@@ -67,6 +67,11 @@ def io_bytes(path, k):
         return 2 * (L + 1) * cols * T
     if k.startswith('jet_store_kernel<0,true'):  # mixed jet (both phases): a-, z-, zb-jets
         return 3 * (L + 1) * cols * T + n * 3 * d * 4
+    if k.startswith('lay_'):  # layered path epilogues, per 16384-coordinate chunk (layered.hip)
+        C, tile = min(n, 16384), min(n, 16384) * H * 4
+        return {'lay_first_kernel': 2 * tile + C * d * 4, 'lay_sine_kernel': 3 * tile,
+                'lay_last_kernel': 3 * tile + C * o * 4, 'lay_rev_kernel<0>': 3 * tile,
+                'lay_rev_kernel<1>': 3 * tile + C * o * 4, 'lay_rev_kernel<2>': 3 * tile + C * d * 4}.get(k)
     if re.match(r'w1_kernel<\d+,4>', k) or (k.startswith('wide_kernel<4') and path == 'video'):
         return 2 * (L + 1) * n_pad * T + n * (d + o) * 4   # FWDS: a tiles + cos of L + 1 layers
     if re.match(r'w1_kernel<\d+,5>', k) or k.startswith('wide_kernel<5'):

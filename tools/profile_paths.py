@@ -36,6 +36,7 @@ PATHS = {  # name: (d, hidden, layers, o, n, work units of F)
     'w1': (2, 256, 3, 1, 1 << 20, 2),
     'w3_wide': (3, 512, 3, 1, 1 << 18, 6),
     'video1024': (3, 1024, 3, 3, 1 << 18, 3),   # the layered path (train_video.py's width)
+    'video1024_rc': (3, 1024, 3, 3, 1 << 18, 3),
     'fwd1024': (3, 1024, 3, 3, 1 << 18, 1),
 }
 
@@ -74,7 +75,12 @@ def build_step(name, dev):
         return lambda: eng.forward_grad(ws, x)
     if name == 'fwd1024':
         return lambda: eng.forward(ws, x)
-    if name == 'video1024':
+    if name == 'video1024':  # the training split the module runs: stored forward, reverse-only backward
+        def step():
+            _, tws = eng.forward_store(ws, x)
+            eng.backward_stored(ws, x, gy, tws)
+        return step
+    if name == 'video1024_rc':  # recompute backward (beyond SirenEngine.STORED_LAYERED_MAX_BYTES)
         def step():
             eng.forward(ws, x)
             eng.backward_params(ws, x, gy)

@@ -7,7 +7,7 @@
 set -o pipefail
 TAG=${1:-r02}
 shift
-PATHS_TO_RUN=${@:-"w1 image_w2 sdf w3_theta w3_wide video poisson poisson_ref hypernet"}
+PATHS_TO_RUN=${@:-"w1 image_w2 sdf w3_theta w3_wide video video1024 poisson poisson_ref hypernet"}
 R=$PWD
 O=$R/gpurun_out/prof_$TAG
 mkdir -p $O
