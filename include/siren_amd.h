@@ -209,6 +209,21 @@ int32_t siren_adam_step(float* params, const float* grads, float* exp_avg, float
                         float beta1, float beta2, float eps, int64_t step, float max_norm, float* scratch,
                         void* stream);
 
+/* ---- surface extraction: device marching cubes ------------------------------------------
+ * Replaces skimage.measure.marching_cubes_lewiner in convert_sdf_samples_to_ply (sdf_meshing.py:97-102) on the
+ * (X, Y, Z) fp32 volume create_mesh evaluated (row-major, axis 0 slowest; sdf_meshing.py:24-59). Cube-case
+ * marching cubes (table derived by tools/gen_mc_table.py: inside = value < level, inside corners separated on
+ * ambiguous faces, no triangle chord along a cube face), vertices welded per grid edge at the linear zero crossing,
+ * in index units * spacing, faces wound so normals point towards increasing value. Two calls: siren_mc_count
+ * (classification + scans; synchronises the stream to return the sizes), then siren_mc_emit into caller buffers
+ * verts (n_verts, 3) fp32 and faces (n_faces, 3) int32; spacing3 is a HOST pointer to 3 floats. ws:
+ * siren_mc_ws_bytes, 4-byte aligned, kept between the two calls. X * Y * Z < 2^32; volumes with an axis < 2 give an empty mesh. */
+int32_t siren_mc_ws_bytes(int64_t X, int64_t Y, int64_t Z, int64_t* bytes);
+int32_t siren_mc_count(const float* vol, int64_t X, int64_t Y, int64_t Z, float level, void* ws, int64_t* n_verts,
+                       int64_t* n_faces, void* stream);
+int32_t siren_mc_emit(const float* vol, int64_t X, int64_t Y, int64_t Z, float level, const float* spacing3,
+                      const void* ws, float* verts, int32_t* faces, void* stream);
+
 /* ---- batched (hypernetwork) weights ----------------------------------------------------
  * BatchLinear with per-element weights W (B, out, in), b (B, out) (modules.py:16-25; HyperNetwork.forward,
  * meta_modules.py:41-53) applied to coords (B, n, d_in). Element b reads params + b * param_count (state-dict

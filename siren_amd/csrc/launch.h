@@ -111,6 +111,13 @@ inline int64_t layered_stored_floats(int H, int lh, int64_t n) { return 2 * (int
 int layered_run(int mode, const LayeredPlan& plan, const float* ws, float w0, float w, const float* x, int64_t n,
                 const float* gy, float* y, float* gx, float* gparams, float* tws, hipStream_t st, std::string& err);
 
+// marching.hip: device marching cubes over an (X, Y, Z) volume; ws in uint32 words
+int64_t mc_ws_words(int64_t X, int64_t Y, int64_t Z);
+void mc_count(const float* vol, int64_t X, int64_t Y, int64_t Z, float level, uint32_t* ws, hipStream_t st);
+const uint32_t* mc_totals(const uint32_t* ws, int64_t X, int64_t Y, int64_t Z, int which);
+void mc_emit(const float* vol, int64_t X, int64_t Y, int64_t Z, float level, const float* spacing, const uint32_t* ws,
+             float* verts, int32_t* faces, hipStream_t st);
+
 constexpr int STEP_BLOCKS = 1024;  // partial sums of the clip-norm pass (4 workgroups per CU)
 // tu_step.hip: device point-cloud sampling (dataio.py:420-442), clip_grad_norm_ + Adam over the flat bucket
 void launch_sample_sdf(hipStream_t st, const float* pc, const float* pn, int64_t m, int64_t k, uint64_t seed,

@@ -1,0 +1,231 @@
+// marching.hip — device marching cubes for sdf_meshing.create_mesh (the reference: skimage
+// marching_cubes_lewiner on the host, sdf_meshing.py:97-102). The volume the W0 kernel just evaluated stays in HBM;
+// three passes over it build an indexed, welded, oriented mesh:
+//   mc_count_kernel   per grid point: crossings on its +x/+y/+z grid edges (popcount) and, per cell, the number of
+//                     triangles of its case (mc_table.h, tools/gen_mc_table.py)
+//   exclusive scans   of both counts (scan_*_kernel: 4096 items per workgroup, block sums scanned by one workgroup)
+//                     -> vertex and triangle offsets, totals
+//   mc_emit_kernel    vertices (linear interpolation along the grid edge, one per crossing: welded) and faces
+//                     (cube edges -> owning grid point + axis -> vertex number)
+// Everything is HBM-streaming integer / byte work on ~4 B per voxel per pass; no MFMA.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "launch.h"
+#include "mc_table.h"
+
+namespace siren {
+
+namespace {
+
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_PER_THREAD = 16;
+constexpr int SCAN_ITEMS = SCAN_THREADS * SCAN_PER_THREAD;
+
+struct Grid {
+    int64_t X, Y, Z;
+    __device__ __forceinline__ int64_t idx(int64_t i, int64_t j, int64_t k) const { return (i * Y + j) * Z + k; }
+};
+
+// crossing bits of the three grid edges leaving point (i, j, k) in +axis0 / +axis1 / +axis2
+__device__ __forceinline__ unsigned edge_bits(const float* __restrict__ v, const Grid& g, int64_t i, int64_t j,
+                                              int64_t k, float level) {
+    const bool in0 = v[g.idx(i, j, k)] < level;
+    unsigned b = 0;
+    if (i + 1 < g.X && (v[g.idx(i + 1, j, k)] < level) != in0) b |= 1u;
+    if (j + 1 < g.Y && (v[g.idx(i, j + 1, k)] < level) != in0) b |= 2u;
+    if (k + 1 < g.Z && (v[g.idx(i, j, k + 1)] < level) != in0) b |= 4u;
+    return b;
+}
+
+__device__ __forceinline__ int cell_case(const float* __restrict__ v, const Grid& g, int64_t i, int64_t j, int64_t k,
+                                         float level) {
+    int m = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+        if (v[g.idx(i + (c & 1), j + ((c >> 1) & 1), k + ((c >> 2) & 1))] < level) m |= 1 << c;
+    return m;
+}
+
+__global__ __launch_bounds__(256) void mc_count_kernel(const float* __restrict__ v, Grid g, float level,
+                                                       uint32_t* __restrict__ vcount, uint32_t* __restrict__ tcount) {
+    const int64_t total = g.X * g.Y * g.Z;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = p % g.Z, j = (p / g.Z) % g.Y, i = p / (g.Y * g.Z);
+        vcount[p] = __builtin_popcount(edge_bits(v, g, i, j, k, level));
+        tcount[p] = (i + 1 < g.X && j + 1 < g.Y && k + 1 < g.Z) ? kMcCount[cell_case(v, g, i, j, k, level)] : 0u;
+    }
+}
+
+__global__ __launch_bounds__(256) void mc_emit_kernel(const float* __restrict__ v, Grid g, float level, float sx,
+                                                      float sy, float sz, const uint32_t* __restrict__ voff,
+                                                      const uint32_t* __restrict__ toff, float* __restrict__ verts,
+                                                      int32_t* __restrict__ faces) {
+    const int64_t total = g.X * g.Y * g.Z;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = p % g.Z, j = (p / g.Z) % g.Y, i = p / (g.Y * g.Z);
+        const unsigned eb = edge_bits(v, g, i, j, k, level);
+        if (eb != 0) {
+            const float v0 = v[p];
+            uint32_t o = voff[p];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                if (!(eb >> a & 1u)) continue;
+                const float v1 = v[g.idx(i + (a == 0), j + (a == 1), k + (a == 2))];
+                const float t = (level - v0) / (v1 - v0);
+                float* q = verts + 3 * (int64_t)o;
+                q[0] = ((float)i + (a == 0 ? t : 0.f)) * sx;
+                q[1] = ((float)j + (a == 1 ? t : 0.f)) * sy;
+                q[2] = ((float)k + (a == 2 ? t : 0.f)) * sz;
+                ++o;
+            }
+        }
+        if (i + 1 < g.X && j + 1 < g.Y && k + 1 < g.Z) {
+            const int m = cell_case(v, g, i, j, k, level);
+            const int nt = kMcCount[m];
+            int32_t* f = faces + 3 * (int64_t)toff[p];
+            for (int s = 0; s < 3 * nt; ++s) {
+                const int e = kMcTri[m][s];
+                const int a = e >> 2, kk = e & 3;
+                // the edge's lower corner: bit (a+1)%3 = kk & 1, bit (a+2)%3 = kk >> 1
+                int64_t c[3] = {i, j, k};
+                c[(a + 1) % 3] += kk & 1;
+                c[(a + 2) % 3] += kk >> 1;
+                const int64_t q = g.idx(c[0], c[1], c[2]);
+                const unsigned qb = edge_bits(v, g, c[0], c[1], c[2], level);
+                f[s] = (int32_t)(voff[q] + __builtin_popcount(qb & ((1u << a) - 1u)));
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t* lds_waves, uint32_t& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t incl = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) lds_waves[wave] = incl;
+    __syncthreads();
+    uint32_t base = 0;
+    total = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+        const uint32_t s = lds_waves[w];
+        if (w < wave) base += s;
+        total += s;
+    }
+    __syncthreads();
+    return base + incl - x;
+}
+
+// per workgroup: sum of its SCAN_ITEMS items
+__global__ __launch_bounds__(SCAN_THREADS) void scan_reduce_kernel(const uint32_t* __restrict__ d, int64_t n,
+                                                                   uint32_t* __restrict__ bsum) {
+    __shared__ uint32_t w[SCAN_THREADS / 64];
+    const int64_t base = (int64_t)blockIdx.x * SCAN_ITEMS;
+    uint32_t s = 0;
+#pragma unroll
+    for (int r = 0; r < SCAN_PER_THREAD; ++r) {
+        const int64_t e = base + r * SCAN_THREADS + threadIdx.x;
+        if (e < n) s += d[e];
+    }
+    uint32_t total;
+    (void)block_exclusive_scan(s, w, total);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+// one workgroup: exclusive scan of the nb block sums in place, the grand total at bsum[nb]
+__global__ __launch_bounds__(1024) void scan_blocks_kernel(uint32_t* __restrict__ bsum, int64_t nb) {
+    __shared__ uint32_t w[16];
+    uint32_t carry = 0;
+    for (int64_t b0 = 0; b0 < nb; b0 += blockDim.x) {
+        const int64_t e = b0 + threadIdx.x;
+        const uint32_t x = e < nb ? bsum[e] : 0u;
+        uint32_t total;
+        const uint32_t ex = block_exclusive_scan(x, w, total);
+        if (e < nb) bsum[e] = carry + ex;
+        carry += total;
+    }
+    if (threadIdx.x == 0) bsum[nb] = carry;
+}
+
+// per workgroup: its items -> exclusive prefix (in place), offset by the scanned block sum
+__global__ __launch_bounds__(SCAN_THREADS) void scan_apply_kernel(uint32_t* __restrict__ d, int64_t n,
+                                                                  const uint32_t* __restrict__ bsum) {
+    __shared__ uint32_t tile[SCAN_ITEMS];
+    __shared__ uint32_t w[SCAN_THREADS / 64];
+    const int64_t base = (int64_t)blockIdx.x * SCAN_ITEMS;
+#pragma unroll
+    for (int r = 0; r < SCAN_PER_THREAD; ++r) {  // coalesced into LDS
+        const int64_t e = base + r * SCAN_THREADS + threadIdx.x;
+        tile[r * SCAN_THREADS + threadIdx.x] = e < n ? d[e] : 0u;
+    }
+    __syncthreads();
+    uint32_t loc[SCAN_PER_THREAD];
+    uint32_t s = 0;
+#pragma unroll
+    for (int r = 0; r < SCAN_PER_THREAD; ++r) {  // thread t owns items [16 t, 16 t + 16)
+        loc[r] = s;
+        s += tile[threadIdx.x * SCAN_PER_THREAD + r];
+    }
+    uint32_t total;
+    const uint32_t off = bsum[blockIdx.x] + block_exclusive_scan(s, w, total);
+#pragma unroll
+    for (int r = 0; r < SCAN_PER_THREAD; ++r) tile[threadIdx.x * SCAN_PER_THREAD + r] = off + loc[r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < SCAN_PER_THREAD; ++r) {
+        const int64_t e = base + r * SCAN_THREADS + threadIdx.x;
+        if (e < n) d[e] = tile[r * SCAN_THREADS + threadIdx.x];
+    }
+}
+
+int64_t scan_blocks(int64_t n) { return (n + SCAN_ITEMS - 1) / SCAN_ITEMS; }
+
+void scan_u32(uint32_t* d, int64_t n, uint32_t* bsum, hipStream_t st) {
+    const int64_t nb = scan_blocks(n);
+    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, st, d, n, bsum);
+    hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(1024), 0, st, bsum, nb);
+    hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, st, d, n, bsum);
+}
+
+dim3 grid_for(int64_t n) {
+    const int64_t b = (n + 255) / 256;
+    return dim3((unsigned)(b < 65536 ? (b > 0 ? b : 1) : 65536));
+}
+
+}  // namespace
+
+// workspace (uint32): [vertex counts -> offsets: P][triangle counts -> offsets: P][block sums x 2: nb + 1 each]
+int64_t mc_ws_words(int64_t X, int64_t Y, int64_t Z) {
+    const int64_t P = X * Y * Z;
+    return 2 * P + 2 * (scan_blocks(P) + 1);
+}
+
+void mc_count(const float* vol, int64_t X, int64_t Y, int64_t Z, float level, uint32_t* ws, hipStream_t st) {
+    const int64_t P = X * Y * Z, nb = scan_blocks(P);
+    uint32_t* vc = ws;
+    uint32_t* tc = ws + P;
+    uint32_t* vb = ws + 2 * P;
+    uint32_t* tb = vb + nb + 1;
+    hipLaunchKernelGGL(mc_count_kernel, grid_for(P), dim3(256), 0, st, vol, Grid{X, Y, Z}, level, vc, tc);
+    scan_u32(vc, P, vb, st);
+    scan_u32(tc, P, tb, st);
+}
+
+const uint32_t* mc_totals(const uint32_t* ws, int64_t X, int64_t Y, int64_t Z, int which) {
+    const int64_t P = X * Y * Z, nb = scan_blocks(P);
+    return ws + 2 * P + (which == 0 ? nb : 2 * nb + 1);
+}
+
+void mc_emit(const float* vol, int64_t X, int64_t Y, int64_t Z, float level, const float* spacing,
+             const uint32_t* ws, float* verts, int32_t* faces, hipStream_t st) {
+    const int64_t P = X * Y * Z;
+    hipLaunchKernelGGL(mc_emit_kernel, grid_for(P), dim3(256), 0, st, vol, Grid{X, Y, Z}, level, spacing[0],
+                       spacing[1], spacing[2], ws, ws + P, verts, faces);
+}
+
+}  // namespace siren

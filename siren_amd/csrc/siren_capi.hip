@@ -877,6 +877,56 @@ int32_t siren_sample_sdf(const float* pc_coords, const float* pc_normals, int64_
     return hip_status("siren_sample_sdf");
 }
 
+// ---- device marching cubes (sdf_meshing.py:97-102 replacement) ----
+static int mc_check(int64_t X, int64_t Y, int64_t Z, bool& empty) {
+    if (X < 0 || Y < 0 || Z < 0) return fail(SIREN_EINVAL, "volume dimensions must be >= 0");
+    empty = X < 2 || Y < 2 || Z < 2;
+    if (!empty && X * Y * Z >= (int64_t(1) << 32)) return fail(SIREN_EUNSUPPORTED, "marching cubes needs X*Y*Z < 2^32");
+    return SIREN_OK;
+}
+
+int32_t siren_mc_ws_bytes(int64_t X, int64_t Y, int64_t Z, int64_t* bytes) {
+    bool empty = false;
+    if (int rc = mc_check(X, Y, Z, empty)) return rc;
+    if (bytes == nullptr) return fail(SIREN_EINVAL, "bytes is NULL");
+    *bytes = empty ? 0 : 4 * siren::mc_ws_words(X, Y, Z);
+    return SIREN_OK;
+}
+
+int32_t siren_mc_count(const float* vol, int64_t X, int64_t Y, int64_t Z, float level, void* ws, int64_t* n_verts,
+                       int64_t* n_faces, void* stream) {
+    bool empty = false;
+    if (int rc = mc_check(X, Y, Z, empty)) return rc;
+    if (n_verts == nullptr || n_faces == nullptr) return fail(SIREN_EINVAL, "n_verts/n_faces is NULL");
+    *n_verts = *n_faces = 0;
+    if (empty) return SIREN_OK;
+    if (vol == nullptr || ws == nullptr) return fail(SIREN_EINVAL, "vol/ws is NULL");
+    if (!std::isfinite(level)) return fail(SIREN_EINVAL, "level must be finite");
+    const hipStream_t st = (hipStream_t)stream;
+    uint32_t* w = (uint32_t*)ws;
+    siren::mc_count(vol, X, Y, Z, level, w, st);
+    if (int rc = hip_status("siren_mc_count")) return rc;
+    uint32_t tv = 0, tf = 0;
+    if (hipMemcpyAsync(&tv, siren::mc_totals(w, X, Y, Z, 0), 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(&tf, siren::mc_totals(w, X, Y, Z, 1), 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return fail(SIREN_EHIP, "siren_mc_count: reading the totals failed");
+    *n_verts = tv;
+    *n_faces = tf;
+    return SIREN_OK;
+}
+
+int32_t siren_mc_emit(const float* vol, int64_t X, int64_t Y, int64_t Z, float level, const float* spacing3,
+                      const void* ws, float* verts, int32_t* faces, void* stream) {
+    bool empty = false;
+    if (int rc = mc_check(X, Y, Z, empty)) return rc;
+    if (empty) return SIREN_OK;
+    if (vol == nullptr || ws == nullptr || spacing3 == nullptr) return fail(SIREN_EINVAL, "vol/ws/spacing is NULL");
+    if (verts == nullptr || faces == nullptr) return fail(SIREN_EINVAL, "verts/faces is NULL");
+    siren::mc_emit(vol, X, Y, Z, level, spacing3, (const uint32_t*)ws, verts, faces, (hipStream_t)stream);
+    return hip_status("siren_mc_emit");
+}
+
 int32_t siren_adam_scratch_floats(int64_t* count) {
     if (count == nullptr) return fail(SIREN_EINVAL, "count is NULL");
     *count = siren::STEP_BLOCKS + 4;

@@ -12,10 +12,11 @@ What differs, and why:
     the default here is 2^22 coordinates per launch instead of 64^3);
   * surface extraction: the reference calls skimage.measure.marching_cubes_lewiner inside a bare try/except
     (sdf_meshing.py:97-102). skimage is not installed in this image; when it is importable its marching_cubes is
-    used, otherwise `marching_tetrahedra` below (Kuhn 6-tetrahedra split of every voxel, crack-free, vertices
-    welded per grid edge, faces oriented along the SDF gradient) runs vectorised in torch on the device. The
-    triangle sets of the two algorithms differ (tetrahedra make ~2x the faces); both interpolate the zero crossing
-    linearly along grid edges, so every vertex lies on the same piecewise-linear surface.
+    used, otherwise the device marching cubes (`marching_cubes` below: HIP kernels in marching.hip, cube-case
+    table from tools/gen_mc_table.py) meshes the volume where the W0 kernel left it. Both interpolate the zero
+    crossing linearly along grid edges (the same vertex set); Lewiner's variant resolves the interior ambiguity of
+    a few cube cases differently, so triangle lists can differ there — mesh parity vs the reference is unpinned
+    (no skimage here); tests pin the kernels to oracle/mc_oracle.py and check closedness / orientation.
   * plyfile is not installed either: write_ply writes the same binary_little_endian layout plyfile produces for
     the reference's element descriptions.
 """
@@ -65,132 +66,59 @@ def evaluate_sdf_grid(decoder, N=256, max_batch=1 << 22, device=None, out_device
 
 
 # --------------------------------------------------------------------------------------------------------
-# marching tetrahedra (stand-in for skimage.measure.marching_cubes, which this image lacks)
+# device marching cubes (stand-in for skimage.measure.marching_cubes_lewiner, which this image lacks)
 # --------------------------------------------------------------------------------------------------------
-_PERMS = ((0, 1, 2), (0, 2, 1), (1, 0, 2), (1, 2, 0), (2, 0, 1), (2, 1, 0))
-
-
-def _tet_offsets():
-    """The 6 Kuhn tetrahedra of the unit cube: vertices 0, e_a, e_a + e_b, (1, 1, 1) for every axis order."""
-    tets = []
-    for a, b, c in _PERMS:
-        v0 = (0, 0, 0)
-        v1 = tuple(1 if i == a else 0 for i in range(3))
-        v2 = tuple(1 if i in (a, b) else 0 for i in range(3))
-        tets.append((v0, v1, v2, (1, 1, 1)))
-    return tets
-
-
-def _case_table():
-    """For each 4-bit inside mask of a tetrahedron: triangles as triples of tet edges (i, j), unoriented."""
-    table = []
-    for mask in range(16):
-        ins = [v for v in range(4) if mask >> v & 1]
-        out = [v for v in range(4) if not mask >> v & 1]
-        if len(ins) in (0, 4):
-            table.append([])
-        elif len(ins) in (1, 3):
-            lone, rest = (ins[0], out) if len(ins) == 1 else (out[0], ins)
-            table.append([[(lone, r) for r in rest]])
-        else:
-            a, b = ins
-            c, d = out
-            table.append([[(a, c), (a, d), (b, d)], [(a, c), (b, d), (b, c)]])
-    return table
-
-
-def marching_tetrahedra(volume, level=0.0, spacing=(1., 1., 1.)):
-    """Zero level set of a (X, Y, Z) volume -> (verts (V, 3) float32 in index units * spacing, faces (F, 3)
-    int64), both on the volume's device. Faces are oriented so their normal points towards increasing value."""
-    vol = volume.float()
+def marching_cubes(volume, level=0.0, spacing=(1., 1., 1.)):
+    """Zero level set of an (X, Y, Z) volume on the device (siren_mc_count / siren_mc_emit, marching.hip) ->
+    (verts (V, 3) float32 in index units * spacing, faces (F, 3) int32), both on the volume's device. Cube-case
+    marching cubes: vertices welded per grid edge, crack-free on ambiguous faces, normals towards increasing value."""
+    import ctypes
+    from . import _lib
+    if not isinstance(volume, torch.Tensor) or volume.dim() != 3:
+        raise ValueError('volume must be an (X, Y, Z) tensor')
+    if volume.device.type != 'cuda':
+        raise RuntimeError('siren_amd marching cubes runs on ROCm devices (MI355X) only; got a %s tensor'
+                           % volume.device.type)
+    vol = volume.detach().float().contiguous()
     dev = vol.device
+    lib = _lib.load()
     X, Y, Z = vol.shape
-    if min(X, Y, Z) < 2:
-        return torch.zeros(0, 3, device=dev), torch.zeros(0, 3, dtype=torch.int64, device=dev)
-    f = vol - level
-    # active voxels: corner values straddle the level
-    corners = torch.stack([f[i:X - 1 + i, j:Y - 1 + j, k:Z - 1 + k]
-                           for i in (0, 1) for j in (0, 1) for k in (0, 1)], 0)
-    neg = (corners < 0)
-    active = neg.any(0) & (~neg).any(0)
-    cube = active.nonzero()  # (C, 3)
-    if cube.shape[0] == 0:
-        return torch.zeros(0, 3, device=dev), torch.zeros(0, 3, dtype=torch.int64, device=dev)
-    strides = torch.tensor([Y * Z, Z, 1], device=dev)
-    flatf = f.reshape(-1)
-    tets = torch.tensor(_tet_offsets(), device=dev)  # (6, 4, 3)
-    gv = cube[:, None, None, :] + tets[None]  # (C, 6, 4, 3) grid vertices of every tet
-    gid = (gv * strides).sum(-1)  # (C, 6, 4)
-    val = flatf[gid]  # (C, 6, 4)
-    mask = ((val < 0).long() * torch.tensor([1, 2, 4, 8], device=dev)).sum(-1)  # (C, 6)
-    table = _case_table()
-    tri_edges, tri_tet, tri_case = [], [], []
-    verts_key, faces = [], []
-    gv_flat = gv.reshape(-1, 4, 3)
-    gid_flat = gid.reshape(-1, 4)
-    val_flat = val.reshape(-1, 4)
-    mask_flat = mask.reshape(-1)
-    # edge id of a tet edge (i, j): the lower grid vertex * 7 + the offset code of the upper one
-    off_code = {(1, 0, 0): 0, (0, 1, 0): 1, (0, 0, 1): 2, (1, 1, 0): 3, (1, 0, 1): 4, (0, 1, 1): 5, (1, 1, 1): 6}
-    code_lut = torch.full((2, 2, 2), -1, dtype=torch.int64, device=dev)
-    for k, v in off_code.items():
-        code_lut[k] = v
-    all_p, all_key, all_tri = [], [], []
-    for case in range(1, 15):
-        sel = (mask_flat == case).nonzero().reshape(-1)
-        if sel.numel() == 0:
-            continue
-        for tri in table[case]:
-            corners_p, keys = [], []
-            for (i, j) in tri:
-                vi, vj = val_flat[sel, i], val_flat[sel, j]
-                pi, pj = gv_flat[sel, i].float(), gv_flat[sel, j].float()
-                t = (vi / (vi - vj)).unsqueeze(-1)
-                corners_p.append(pi + t * (pj - pi))
-                lo = torch.minimum(gid_flat[sel, i], gid_flat[sel, j])
-                d = (gv_flat[sel, j] - gv_flat[sel, i]).abs()
-                keys.append(lo * 7 + code_lut[d[:, 0], d[:, 1], d[:, 2]])
-            p = torch.stack(corners_p, 1)  # (T, 3 corners, 3)
-            key = torch.stack(keys, 1)  # (T, 3)
-            # orientation: the tet's linear interpolant gradient, from its values along the Kuhn path
-            v4 = val_flat[sel]
-            g4 = gv_flat[sel].float()
-            grad = torch.zeros(sel.numel(), 3, device=dev)
-            for e in range(3):  # edge e of the path v_e -> v_{e+1} moves along exactly one axis
-                axis = (g4[:, e + 1] - g4[:, e]).argmax(-1)
-                grad.scatter_(1, axis[:, None], (v4[:, e + 1] - v4[:, e])[:, None])
-            n = torch.cross(p[:, 1] - p[:, 0], p[:, 2] - p[:, 0], dim=-1)
-            flip = (n * grad).sum(-1) < 0
-            key = torch.where(flip[:, None], key[:, [0, 2, 1]], key)
-            p = torch.where(flip[:, None, None], p[:, [0, 2, 1]], p)
-            all_p.append(p.reshape(-1, 3))
-            all_key.append(key.reshape(-1))
-    if not all_key:
-        return torch.zeros(0, 3, device=dev), torch.zeros(0, 3, dtype=torch.int64, device=dev)
-    P = torch.cat(all_p, 0)
-    K = torch.cat(all_key, 0)
-    uniq, inv = torch.unique(K, return_inverse=True)
-    verts = torch.zeros(uniq.numel(), 3, device=dev)
-    verts[inv] = P  # every occurrence of an edge key interpolates the same two grid values: identical points
-    faces = inv.view(-1, 3)
-    # drop faces that collapsed onto one welded vertex (the level passing exactly through a grid vertex)
-    ok = (faces[:, 0] != faces[:, 1]) & (faces[:, 1] != faces[:, 2]) & (faces[:, 0] != faces[:, 2])
-    faces = faces[ok]
-    verts = verts * torch.tensor(spacing, device=dev, dtype=torch.float32)
+    nb = ctypes.c_int64()
+    _lib.check(lib.siren_mc_ws_bytes(X, Y, Z, ctypes.byref(nb)), 'siren_mc_ws_bytes')
+    ws = torch.empty(max(1, nb.value // 4), dtype=torch.int32, device=dev)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    nv, nf = ctypes.c_int64(), ctypes.c_int64()
+    _lib.check(lib.siren_mc_count(ctypes.c_void_p(vol.data_ptr()), X, Y, Z, ctypes.c_float(level),
+                                  ctypes.c_void_p(ws.data_ptr()), ctypes.byref(nv), ctypes.byref(nf), stream),
+               'siren_mc_count')
+    verts = torch.empty(nv.value, 3, dtype=torch.float32, device=dev)
+    faces = torch.empty(nf.value, 3, dtype=torch.int32, device=dev)
+    if nv.value == 0 and nf.value == 0:
+        return verts, faces
+    sp = (ctypes.c_float * 3)(*[float(t) for t in spacing])
+    _lib.check(lib.siren_mc_emit(ctypes.c_void_p(vol.data_ptr()), X, Y, Z, ctypes.c_float(level),
+                                 ctypes.cast(sp, ctypes.c_void_p),
+                                 ctypes.c_void_p(ws.data_ptr()), ctypes.c_void_p(verts.data_ptr()),
+                                 ctypes.c_void_p(faces.data_ptr()), stream), 'siren_mc_emit')
     return verts, faces
 
 
 def extract_surface(sdf_volume, voxel_size, level=0.0):
-    """(verts, faces) in voxel units * voxel_size: skimage's marching_cubes when importable, else
-    marching_tetrahedra on the volume's device."""
+    """(verts, faces) in voxel units * voxel_size: skimage's marching_cubes when importable, else the device
+    marching cubes (a host volume — the reference passes sdf_values.cpu() — is moved to the current device)."""
     try:
         import skimage.measure  # noqa: F401
         v = sdf_volume.detach().cpu().numpy()
         verts, faces, _, _ = skimage.measure.marching_cubes(v, level=level, spacing=[voxel_size] * 3)
         return np.asarray(verts, np.float64), np.asarray(faces, np.int64)
     except ImportError:
-        verts, faces = marching_tetrahedra(sdf_volume, level, (voxel_size,) * 3)
-        return verts.double().cpu().numpy(), faces.cpu().numpy()
+        vol = torch.as_tensor(sdf_volume)
+        if vol.device.type != 'cuda':
+            if not torch.cuda.is_available():
+                raise RuntimeError('siren_amd marching cubes needs a ROCm device (MI355X); there is no CPU path')
+            vol = vol.cuda()
+        verts, faces = marching_cubes(vol, level, (voxel_size,) * 3)
+        return verts.double().cpu().numpy(), faces.long().cpu().numpy()
 
 
 def write_ply(path, verts, faces):

@@ -43,30 +43,60 @@ def edge_counts(faces):
     return counts
 
 
-@pytest.mark.parametrize('N', [16, 33])
-def test_marching_tetrahedra_sphere_closed_oriented(N):
-    vol = sphere_volume(N)
-    h = 2.0 / (N - 1)
-    verts, faces = M.marching_tetrahedra(vol, 0.0, (h, h, h))
-    v = verts.double().numpy() - 1.0
-    f = faces.numpy()
+def closed_oriented(v, f, r=0.5, h=None):
+    """Every undirected edge in exactly two faces, the two uses opposite (consistent winding), enclosed volume
+    positive and close to the sphere's."""
     assert f.shape[0] > 0
-    # vertices on the sphere (linear interpolation of a smooth SDF: error O(h^2))
-    rad = np.linalg.norm(v, axis=1)
-    assert np.max(np.abs(rad - 0.5)) < 0.5 * h
-    # closed 2-manifold: every edge shared by exactly two faces
     assert np.all(edge_counts(f) == 2)
-    # consistently oriented outwards: positive enclosed volume close to 4/3 pi r^3
+    d = np.concatenate([f[:, [0, 1]], f[:, [1, 2]], f[:, [2, 0]]])
+    assert np.unique(d, axis=0).shape[0] == d.shape[0]  # no directed edge twice
     a, b, c = v[f[:, 0]], v[f[:, 1]], v[f[:, 2]]
     vol6 = np.einsum('ij,ij->i', a, np.cross(b, c)).sum()
-    assert abs(vol6 / 6 - 4 / 3 * np.pi * 0.125) < 0.05 * (4 / 3 * np.pi * 0.125)
+    assert abs(vol6 / 6 - 4 / 3 * np.pi * r ** 3) < 0.05 * (4 / 3 * np.pi * r ** 3)
 
 
-def test_marching_tetrahedra_empty_and_tiny():
-    v, f = M.marching_tetrahedra(torch.ones(5, 5, 5))
-    assert v.shape == (0, 3) and f.shape == (0, 3)
-    v, f = M.marching_tetrahedra(torch.ones(1, 5, 5))
-    assert f.shape == (0, 3)
+@pytest.mark.parametrize('N', [16, 25])
+def test_oracle_marching_cubes_sphere(N):
+    """The CPU restatement of the device marching cubes (oracle/mc_oracle.py): a sphere SDF gives a closed,
+    outward-oriented mesh whose vertices lie on the sphere to O(h^2)."""
+    from oracle import mc_oracle as MC
+    h = 2.0 / (N - 1)
+    v, f = MC.marching_cubes(sphere_volume(N).numpy(), 0.0, (h, h, h))
+    v = v - 1.0
+    assert np.max(np.abs(np.linalg.norm(v, axis=1) - 0.5)) < 0.5 * h
+    closed_oriented(v, f)
+
+
+def test_oracle_marching_cubes_noise_is_manifold():
+    """Random volumes (every ambiguous face and cube case): still a closed consistently wound 2-manifold inside
+    the volume — ambiguous faces are resolved identically by both cells, and no triangle chord lies on a face."""
+    from oracle import mc_oracle as MC
+    rng = np.random.default_rng(0)
+    for _ in range(6):
+        vol = rng.normal(size=(7, 6, 8))
+        vol[[0, -1]] = 1.
+        vol[:, [0, -1]] = 1.
+        vol[:, :, [0, -1]] = 1.
+        v, f = MC.marching_cubes(vol)
+        assert np.all(edge_counts(f) == 2)
+        d = np.concatenate([f[:, [0, 1]], f[:, [1, 2]], f[:, [2, 0]]])
+        assert np.unique(d, axis=0).shape[0] == d.shape[0]
+
+
+def test_mc_table_header_matches_derivation():
+    """siren_amd/csrc/mc_table.h (tools/gen_mc_table.py) == the oracle's independent derivation, case by case."""
+    import re
+    from oracle import mc_oracle as MC
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'siren_amd', 'csrc',
+                            'mc_table.h')).read()
+    counts = [int(t) for t in re.findall(r'-?\d+', src.split('kMcCount[256] = {')[1].split('};')[0])]
+    rows = re.findall(r'\{([-0-9, ]+)\},', src.split('kMcTri[256]')[1])
+    table = MC.case_table()
+    assert len(counts) == 256 and len(rows) == 256
+    for m in range(256):
+        got = [int(t) for t in rows[m].split(',') if int(t) >= 0]
+        assert got == [e for tri in table[m] for e in tri] and counts[m] == len(table[m]), m
+    assert max(counts) == 5 and counts[0] == 0 and counts[255] == 0
 
 
 def test_ply_roundtrip(tmp_path):
@@ -80,7 +110,9 @@ def test_ply_roundtrip(tmp_path):
     assert 'element vertex 10' in head and 'element face 7' in head and 'property list uchar int vertex_indices' in head
 
 
-def test_convert_sdf_samples_to_ply_offset_scale(tmp_path):
+@pytest.mark.gpu
+def test_convert_sdf_samples_to_ply_offset_scale(cuda, tmp_path):
+    """The reference passes a host tensor (sdf_values.cpu(), sdf_meshing.py:64-71): it is meshed on the device."""
     N = 17
     vol = sphere_volume(N)
     p = os.path.join(tmp_path, 's.ply')
@@ -126,3 +158,40 @@ def test_create_mesh_on_fused_kernel(cuda, tmp_path):
     pts_out, faces = M.create_mesh(dec2, os.path.join(tmp_path, 'mesh'), N=N, max_batch=1 << 16, log=None)
     v, f = M.read_ply(os.path.join(tmp_path, 'mesh.ply'))
     assert f.shape[0] > 0 and v.shape[0] > 0 and f.max() < v.shape[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('shape,seed', [((7, 6, 8), 0), ((2, 2, 2), 1), ((3, 9, 4), 2), ((11, 11, 11), 3)])
+def test_device_marching_cubes_matches_oracle(cuda, shape, seed):
+    """siren_mc_count / siren_mc_emit (marching.hip) == oracle/mc_oracle.py: the same vertex numbering (grid point,
+    axis), the same faces bit for bit, vertex positions to fp32 rounding — on noise volumes (every cube case)."""
+    from oracle import mc_oracle as MC
+    vol = np.random.default_rng(seed).normal(size=shape).astype(np.float32)
+    sp = (0.5, 1.0, 2.0)
+    v, f = M.marching_cubes(torch.tensor(vol, device=cuda), 0.1, sp)
+    rv, rf = MC.marching_cubes(vol.astype(np.float64), 0.1, sp)
+    assert f.shape == rf.shape and v.shape == rv.shape
+    assert np.array_equal(f.cpu().numpy(), rf)
+    assert np.max(np.abs(v.cpu().numpy() - rv), initial=0.) <= 1e-5
+
+
+@pytest.mark.gpu
+def test_device_marching_cubes_empty_and_tiny(cuda):
+    for shape in [(5, 5, 5), (1, 5, 5), (5, 0, 5)]:
+        v, f = M.marching_cubes(torch.ones(shape, device=cuda))
+        assert v.shape == (0, 3) and f.shape == (0, 3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('N', [33, 256])
+def test_device_marching_cubes_sphere(cuda, N):
+    """A sphere SDF at the reference's default resolution (create_mesh N = 256): closed, outward, on the sphere."""
+    h = 2.0 / (N - 1)
+    v, f = M.marching_cubes(sphere_volume(N).to(cuda), 0.0, (h, h, h))
+    v = v.double().cpu().numpy() - 1.0
+    f = f.long().cpu().numpy()
+    assert np.max(np.abs(np.linalg.norm(v, axis=1) - 0.5)) < 0.5 * h
+    closed_oriented(v, f)
+    # Euler characteristic of a sphere
+    e = np.unique(np.sort(np.concatenate([f[:, [0, 1]], f[:, [1, 2]], f[:, [2, 0]]]), axis=1), axis=0).shape[0]
+    assert v.shape[0] - e + f.shape[0] == 2
