@@ -217,7 +217,8 @@ int32_t siren_adam_step(float* params, const float* grads, float* exp_avg, float
  * in index units * spacing, faces wound so normals point towards increasing value. Two calls: siren_mc_count
  * (classification + scans; synchronises the stream to return the sizes), then siren_mc_emit into caller buffers
  * verts (n_verts, 3) fp32 and faces (n_faces, 3) int32; spacing3 is a HOST pointer to 3 floats. ws:
- * siren_mc_ws_bytes, 4-byte aligned, kept between the two calls. X * Y * Z < 2^32; volumes with an axis < 2 give an empty mesh. */
+ * siren_mc_ws_bytes, 4-byte aligned, kept between the two calls. X * Y * Z < 2^32, X, Y <= 65535; volumes
+ * with an axis < 2 give an empty mesh. */
 int32_t siren_mc_ws_bytes(int64_t X, int64_t Y, int64_t Z, int64_t* bytes);
 int32_t siren_mc_count(const float* vol, int64_t X, int64_t Y, int64_t Z, float level, void* ws, int64_t* n_verts,
                        int64_t* n_faces, void* stream);

@@ -31,72 +31,99 @@ struct Grid {
 // crossing bits of the three grid edges leaving point (i, j, k) in +axis0 / +axis1 / +axis2
 __device__ __forceinline__ unsigned edge_bits(const float* __restrict__ v, const Grid& g, int64_t i, int64_t j,
                                               int64_t k, float level) {
-    const bool in0 = v[g.idx(i, j, k)] < level;
+    const int64_t p = g.idx(i, j, k);
+    const bool in0 = v[p] < level;
     unsigned b = 0;
-    if (i + 1 < g.X && (v[g.idx(i + 1, j, k)] < level) != in0) b |= 1u;
-    if (j + 1 < g.Y && (v[g.idx(i, j + 1, k)] < level) != in0) b |= 2u;
-    if (k + 1 < g.Z && (v[g.idx(i, j, k + 1)] < level) != in0) b |= 4u;
+    if (i + 1 < g.X && (v[p + g.Y * g.Z] < level) != in0) b |= 1u;
+    if (j + 1 < g.Y && (v[p + g.Z] < level) != in0) b |= 2u;
+    if (k + 1 < g.Z && (v[p + 1] < level) != in0) b |= 4u;
     return b;
 }
 
-__device__ __forceinline__ int cell_case(const float* __restrict__ v, const Grid& g, int64_t i, int64_t j, int64_t k,
-                                         float level) {
-    int m = 0;
+// One thread per grid point: blockIdx.z = axis-0 index, blockIdx.y = axis-1 index, axis 2 across the workgroup
+// (coalesced rows, no index division). The 8 corner values of the point's cell are loaded once and give both the
+// point's edge crossings and the cell's case.
+struct Point {
+    int64_t i, j, k, p;
+    bool ok, cell;
+    unsigned eb;
+    int m;
+};
+
+__device__ __forceinline__ Point classify(const float* __restrict__ v, const Grid& g, float level) {
+    Point q;
+    q.k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    q.j = blockIdx.y;
+    q.i = blockIdx.z;
+    q.ok = q.k < g.Z;
+    q.eb = 0;
+    q.m = 0;
+    q.cell = false;
+    if (!q.ok) return q;
+    q.p = g.idx(q.i, q.j, q.k);
+    const int64_t si = g.Y * g.Z, sj = g.Z;
+    const bool hi = q.i + 1 < g.X, hj = q.j + 1 < g.Y, hk = q.k + 1 < g.Z;
+    q.cell = hi && hj && hk;
+    float c[8];
+    c[0] = v[q.p];
+    c[1] = hi ? v[q.p + si] : c[0];
+    c[2] = hj ? v[q.p + sj] : c[0];
+    c[4] = hk ? v[q.p + 1] : c[0];
+    const bool in0 = c[0] < level;
+    q.eb = ((c[1] < level) != in0 ? 1u : 0u) | ((c[2] < level) != in0 ? 2u : 0u) | ((c[4] < level) != in0 ? 4u : 0u);
+    if (q.cell) {
+        c[3] = v[q.p + si + sj];
+        c[5] = v[q.p + si + 1];
+        c[6] = v[q.p + sj + 1];
+        c[7] = v[q.p + si + sj + 1];
 #pragma unroll
-    for (int c = 0; c < 8; ++c)
-        if (v[g.idx(i + (c & 1), j + ((c >> 1) & 1), k + ((c >> 2) & 1))] < level) m |= 1 << c;
-    return m;
+        for (int t = 0; t < 8; ++t)
+            if (c[t] < level) q.m |= 1 << t;
+    }
+    return q;
 }
 
 __global__ __launch_bounds__(256) void mc_count_kernel(const float* __restrict__ v, Grid g, float level,
                                                        uint32_t* __restrict__ vcount, uint32_t* __restrict__ tcount) {
-    const int64_t total = g.X * g.Y * g.Z;
-    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t k = p % g.Z, j = (p / g.Z) % g.Y, i = p / (g.Y * g.Z);
-        vcount[p] = __builtin_popcount(edge_bits(v, g, i, j, k, level));
-        tcount[p] = (i + 1 < g.X && j + 1 < g.Y && k + 1 < g.Z) ? kMcCount[cell_case(v, g, i, j, k, level)] : 0u;
-    }
+    const Point q = classify(v, g, level);
+    if (!q.ok) return;
+    vcount[q.p] = __builtin_popcount(q.eb);
+    tcount[q.p] = q.cell ? (uint32_t)kMcCount[q.m] : 0u;
 }
 
 __global__ __launch_bounds__(256) void mc_emit_kernel(const float* __restrict__ v, Grid g, float level, float sx,
                                                       float sy, float sz, const uint32_t* __restrict__ voff,
                                                       const uint32_t* __restrict__ toff, float* __restrict__ verts,
                                                       int32_t* __restrict__ faces) {
-    const int64_t total = g.X * g.Y * g.Z;
-    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t k = p % g.Z, j = (p / g.Z) % g.Y, i = p / (g.Y * g.Z);
-        const unsigned eb = edge_bits(v, g, i, j, k, level);
-        if (eb != 0) {
-            const float v0 = v[p];
-            uint32_t o = voff[p];
+    const Point q = classify(v, g, level);
+    if (!q.ok) return;
+    if (q.eb != 0) {
+        const float v0 = v[q.p];
+        uint32_t o = voff[q.p];
+        const int64_t step[3] = {g.Y * g.Z, g.Z, 1};
 #pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                if (!(eb >> a & 1u)) continue;
-                const float v1 = v[g.idx(i + (a == 0), j + (a == 1), k + (a == 2))];
-                const float t = (level - v0) / (v1 - v0);
-                float* q = verts + 3 * (int64_t)o;
-                q[0] = ((float)i + (a == 0 ? t : 0.f)) * sx;
-                q[1] = ((float)j + (a == 1 ? t : 0.f)) * sy;
-                q[2] = ((float)k + (a == 2 ? t : 0.f)) * sz;
-                ++o;
-            }
+        for (int a = 0; a < 3; ++a) {
+            if (!(q.eb >> a & 1u)) continue;
+            const float t = (level - v0) / (v[q.p + step[a]] - v0);
+            float* w = verts + 3 * (int64_t)o;
+            w[0] = ((float)q.i + (a == 0 ? t : 0.f)) * sx;
+            w[1] = ((float)q.j + (a == 1 ? t : 0.f)) * sy;
+            w[2] = ((float)q.k + (a == 2 ? t : 0.f)) * sz;
+            ++o;
         }
-        if (i + 1 < g.X && j + 1 < g.Y && k + 1 < g.Z) {
-            const int m = cell_case(v, g, i, j, k, level);
-            const int nt = kMcCount[m];
-            int32_t* f = faces + 3 * (int64_t)toff[p];
-            for (int s = 0; s < 3 * nt; ++s) {
-                const int e = kMcTri[m][s];
-                const int a = e >> 2, kk = e & 3;
-                // the edge's lower corner: bit (a+1)%3 = kk & 1, bit (a+2)%3 = kk >> 1
-                int64_t c[3] = {i, j, k};
-                c[(a + 1) % 3] += kk & 1;
-                c[(a + 2) % 3] += kk >> 1;
-                const int64_t q = g.idx(c[0], c[1], c[2]);
-                const unsigned qb = edge_bits(v, g, c[0], c[1], c[2], level);
-                f[s] = (int32_t)(voff[q] + __builtin_popcount(qb & ((1u << a) - 1u)));
-            }
-        }
+    }
+    const int nt = q.cell ? kMcCount[q.m] : 0;
+    if (nt == 0) return;
+    int32_t* f = faces + 3 * (int64_t)toff[q.p];
+    for (int s = 0; s < 3 * nt; ++s) {
+        const int e = kMcTri[q.m][s];
+        const int a = e >> 2, kk = e & 3;
+        // the edge's lower corner: bit (a+1)%3 = kk & 1, bit (a+2)%3 = kk >> 1
+        int64_t c[3] = {q.i, q.j, q.k};
+        c[(a + 1) % 3] += kk & 1;
+        c[(a + 2) % 3] += kk >> 1;
+        const unsigned qb = edge_bits(v, g, c[0], c[1], c[2], level);
+        f[s] = (int32_t)(voff[g.idx(c[0], c[1], c[2])] + __builtin_popcount(qb & ((1u << a) - 1u)));
     }
 }
 
@@ -192,9 +219,8 @@ void scan_u32(uint32_t* d, int64_t n, uint32_t* bsum, hipStream_t st) {
     hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, st, d, n, bsum);
 }
 
-dim3 grid_for(int64_t n) {
-    const int64_t b = (n + 255) / 256;
-    return dim3((unsigned)(b < 65536 ? (b > 0 ? b : 1) : 65536));
+dim3 point_grid(int64_t X, int64_t Y, int64_t Z) {
+    return dim3((unsigned)((Z + 255) / 256), (unsigned)Y, (unsigned)X);
 }
 
 }  // namespace
@@ -211,7 +237,7 @@ void mc_count(const float* vol, int64_t X, int64_t Y, int64_t Z, float level, ui
     uint32_t* tc = ws + P;
     uint32_t* vb = ws + 2 * P;
     uint32_t* tb = vb + nb + 1;
-    hipLaunchKernelGGL(mc_count_kernel, grid_for(P), dim3(256), 0, st, vol, Grid{X, Y, Z}, level, vc, tc);
+    hipLaunchKernelGGL(mc_count_kernel, point_grid(X, Y, Z), dim3(256), 0, st, vol, Grid{X, Y, Z}, level, vc, tc);
     scan_u32(vc, P, vb, st);
     scan_u32(tc, P, tb, st);
 }
@@ -224,7 +250,7 @@ const uint32_t* mc_totals(const uint32_t* ws, int64_t X, int64_t Y, int64_t Z, i
 void mc_emit(const float* vol, int64_t X, int64_t Y, int64_t Z, float level, const float* spacing,
              const uint32_t* ws, float* verts, int32_t* faces, hipStream_t st) {
     const int64_t P = X * Y * Z;
-    hipLaunchKernelGGL(mc_emit_kernel, grid_for(P), dim3(256), 0, st, vol, Grid{X, Y, Z}, level, spacing[0],
+    hipLaunchKernelGGL(mc_emit_kernel, point_grid(X, Y, Z), dim3(256), 0, st, vol, Grid{X, Y, Z}, level, spacing[0],
                        spacing[1], spacing[2], ws, ws + P, verts, faces);
 }
 

@@ -881,7 +881,8 @@ int32_t siren_sample_sdf(const float* pc_coords, const float* pc_normals, int64_
 static int mc_check(int64_t X, int64_t Y, int64_t Z, bool& empty) {
     if (X < 0 || Y < 0 || Z < 0) return fail(SIREN_EINVAL, "volume dimensions must be >= 0");
     empty = X < 2 || Y < 2 || Z < 2;
-    if (!empty && X * Y * Z >= (int64_t(1) << 32)) return fail(SIREN_EUNSUPPORTED, "marching cubes needs X*Y*Z < 2^32");
+    if (!empty && (X * Y * Z >= (int64_t(1) << 32) || X > 65535 || Y > 65535))
+        return fail(SIREN_EUNSUPPORTED, "marching cubes needs X*Y*Z < 2^32 and X, Y <= 65535");
     return SIREN_OK;
 }
 
