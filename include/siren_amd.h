@@ -187,6 +187,10 @@ int32_t siren_hvp_backward(const siren_cfg* cfg, const float* ws, const float* x
  * unrecorded entries are left untouched. y / gx as siren_forward_grad with gy = ones. */
 int32_t siren_w1_phase_profile(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y, float* gx,
                                uint64_t* stamps, void* stream);
+/* Diagnostics: while stamps is non-NULL, every W3 (siren_second_order*) launch records s_memtime stamps of wave 0 of
+ * workgroups 0..255 after each phase (start, layer 0, forward GEMM / epilogue per layer, seed, reverse GEMM / epilogue
+ * per layer, end) into stamps[256][16] (device memory); NULL switches it off. */
+int32_t siren_w3_phase_profile(uint64_t* stamps);
 
 /* ---- per-step kernels around the network ---------------------------------------------
  * Device-side dataio.PointCloud.__getitem__ (dataio.py:420-442): from a resident point cloud pc_coords /

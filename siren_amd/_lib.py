@@ -62,6 +62,7 @@ _SIGS = {
     'siren_backward_batched': [_CFG, _P, _P, _I64, _I64, _P, _P, _P, _P, _P],
     'siren_sample_sdf': [_P, _P, _I64, _I64, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P],
     'siren_adam_scratch_floats': [ctypes.POINTER(_I64)],
+    'siren_w3_phase_profile': [_P],
     'siren_mc_ws_bytes': [_I64, _I64, _I64, ctypes.POINTER(_I64)],
     'siren_mc_count': [_P, _I64, _I64, _I64, ctypes.c_float, _P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), _P],
     'siren_mc_emit': [_P, _I64, _I64, _I64, ctypes.c_float, _P, _P, _P, _P, _P],

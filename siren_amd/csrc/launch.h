@@ -70,7 +70,7 @@ void launch_small_j2(dim3 grid, hipStream_t st, const float* abuf, const float* 
 void launch_w3(bool theta, dim3 grid, hipStream_t st, const float* ws, const float* x, const float* v, const float* gy,
                const float* u, float* ydot, int o, int64_t n, float* gx, float* spill, float* A, float* At, float* D,
                float* Dt, int64_t n_pad, int d, int lh, float w0, float w, const float* kA = nullptr,
-               const float* kC = nullptr);
+               const float* kC = nullptr, unsigned long long* prof = nullptr);
 void launch_small_w3(dim3 grid, hipStream_t st, const float* At, const float* D, const float* Dt, const float* AL,
                      const float* x, const float* v, const float* gy, const float* u, int64_t n, int64_t n_pad, int64_t tps,
                      float* eslab, int64_t E, int d, int o, int lh);

@@ -289,6 +289,13 @@ int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x
     return hip_status("siren_forward_grad");
 }
 
+// diagnostics: while set, W3 launches record s_memtime phase stamps (w3_kernel.hpp) into stamps[256][16]
+static unsigned long long* g_w3_prof = nullptr;
+int32_t siren_w3_phase_profile(uint64_t* stamps) {
+    g_w3_prof = (unsigned long long*)stamps;
+    return SIREN_OK;
+}
+
 int32_t siren_w1_phase_profile(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y, float* gx,
                                uint64_t* stamps, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
@@ -819,7 +826,7 @@ static int32_t second_order_impl(const siren_cfg* cfg, const float* ws, const fl
     }
     const dim3 grid((unsigned)(plan.n_pad / siren::TILE));
     siren::launch_w3(theta, grid, st, ws, x, v, gy, u, ydot, cfg->d_out, n, gx, spill, A, At, D, Dt, plan.n_pad,
-                     cfg->d_in, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, kA, kC);
+                     cfg->d_in, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, kA, kC, g_w3_prof);
     if (int rc = hip_status("siren_second_order (w3)")) return rc;
     if (!theta) return SIREN_OK;
     const dim3 wgrid((unsigned)plan.splits, (unsigned)cfg->n_hidden);

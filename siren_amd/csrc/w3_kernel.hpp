@@ -86,7 +86,8 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
                                                         float* __restrict__ At, float* __restrict__ D,
                                                         float* __restrict__ Dt, int64_t n_pad, int d, float w0,
                                                         float w, const float* __restrict__ kA,
-                                                        const float* __restrict__ kC) {
+                                                        const float* __restrict__ kC,
+                                                        unsigned long long* __restrict__ prof = nullptr) {
     __shared__ __attribute__((aligned(16))) float lds[NBUF * SLICE + SMALL_MAX];
     float* ring = lds;
     float* sm = lds + NBUF * SLICE;
@@ -95,6 +96,17 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
     const int nslices = 2 * LH * NB;
     const float* stream = ws + small_pad(LH);
     const int64_t tile = (int64_t)blockIdx.x * WAVES + wave;
+    // diagnostics (siren_w3_phase_profile): s_memtime after each phase, workgroups < 256, wave 0
+    const bool rec = prof != nullptr && blockIdx.x < 256 && wave == 0;
+    int ev = 0;
+    auto mark = [&]() {
+        if (rec) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (lane == 0) prof[blockIdx.x * 16 + ev] = t;
+        }
+        ++ev;
+    };
+    mark();
     float* wsp = spill + tile * (int64_t)(LH + 1) * 3 * NB * 256;
     const int64_t lstride = n_pad * H;
     const int64_t toff = tile * (H * 16) + 4 * g * 16 + c;
@@ -148,7 +160,7 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
         *spill_at(wsp, 0, 1, rb, lane) = zd;
         if (!KEPT) {
             *spill_at(wsp, 0, 0, rb, lane) = cs;
-            *spill_at(wsp, 0, 2, rb, lane) = sn;
+            if (!THETA) *spill_at(wsp, 0, 2, rb, lane) = sn;  // THETA: a_l comes back from the A tiles
         }
         if (THETA) {
             if (!KEPT) store_block(A + toff, rb, actp[rb]);
@@ -156,6 +168,7 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
         }
     }
 
+    mark();
     // ---- hidden layers: primal + tangent GEMMs ------------------------------------------------------------
     int s = 0;
 #pragma unroll 1
@@ -163,6 +176,7 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
         if constexpr (KEPT) {
             // primal from the stored forward: tangent GEMM only, zdot_l = W_l adot_{l-1}, adot_l = w cos_l zdot_l
             layer_mma1(stream, ring, s, nslices, wave, lane, actt, acct);
+            mark();
 #pragma unroll
             for (int rb = 0; rb < NB; ++rb) {
                 const f32x4 zd = acct[rb];
@@ -170,9 +184,11 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
                 *spill_at(wsp, l, 1, rb, lane) = zd;
                 if (THETA) store_block(At + l * lstride + toff, rb, actt[rb]);
             }
+            mark();
             continue;
         }
         layer_mma2(stream, ring, s, nslices, wave, lane, actp, actt, accp, acct);
+        mark();
         const float* bl = sm + SM_BIAS + l * H + 4 * g;
 #pragma unroll
         for (int rb = 0; rb < NB; ++rb) {
@@ -190,12 +206,13 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
             actt[rb] = (w * cs) * zd;
             *spill_at(wsp, l, 0, rb, lane) = cs;
             *spill_at(wsp, l, 1, rb, lane) = zd;
-            *spill_at(wsp, l, 2, rb, lane) = sn;
+            if (!THETA) *spill_at(wsp, l, 2, rb, lane) = sn;
             if (THETA) {
                 store_block(A + l * lstride + toff, rb, actp[rb]);
                 store_block(At + l * lstride + toff, rb, actt[rb]);
             }
         }
+        mark();
     }
 
     // ---- ydot = Wout ad_L (the forward tangent of y along v) ---------------------------------------------------
@@ -231,7 +248,8 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
         }
         const f32x4 cs = KEPT ? kept_c(LH, rb) : *spill_at(wsp, LH, 0, rb, lane);
         const f32x4 zd = *spill_at(wsp, LH, 1, rb, lane);
-        const f32x4 sn = KEPT ? kept_a(kA, lstride, toff, LH, rb) : *spill_at(wsp, LH, 2, rb, lane);
+        const f32x4 sn = KEPT ? kept_a(kA, lstride, toff, LH, rb)
+                              : (THETA ? kept_a(A, lstride, toff, LH, rb) : *spill_at(wsp, LH, 2, rb, lane));
         actt[rb] = (w * cs) * adb;
         actp[rb] = (w * cs) * abseed - (w * w) * sn * zd * adb;
         if (THETA) {
@@ -239,15 +257,18 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
             store_block(Dt + LH * lstride + toff, rb, actt[rb]);
         }
     }
+    mark();
 #pragma unroll 1
     for (int l = LH; l >= 1; --l) {
         layer_mma2(stream, ring, s, nslices, wave, lane, actp, actt, accp, acct);  // accp = ab, acct = adb (l-1)
+        mark();
         const float wl = (l == 1) ? w0 : w;
 #pragma unroll
         for (int rb = 0; rb < NB; ++rb) {
             const f32x4 cs = KEPT ? kept_c(l - 1, rb) : *spill_at(wsp, l - 1, 0, rb, lane);
             const f32x4 zd = *spill_at(wsp, l - 1, 1, rb, lane);
-            const f32x4 sn = KEPT ? kept_a(kA, lstride, toff, l - 1, rb) : *spill_at(wsp, l - 1, 2, rb, lane);
+            const f32x4 sn = KEPT ? kept_a(kA, lstride, toff, l - 1, rb)
+                                  : (THETA ? kept_a(A, lstride, toff, l - 1, rb) : *spill_at(wsp, l - 1, 2, rb, lane));
             const f32x4 wc = wl * cs;
             actt[rb] = wc * acct[rb];
             actp[rb] = wc * accp[rb] - (wl * wl) * sn * zd * acct[rb];
@@ -256,6 +277,7 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
                 store_block(Dt + (l - 1) * lstride + toff, rb, actt[rb]);
             }
         }
+        mark();
     }
     // ---- gx = W0^T zb_0 ------------------------------------------------------------------------------------
 #pragma unroll
@@ -271,6 +293,7 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
             if (valid && g == 0) gx[coord * d + k] = p;
         }
     }
+    mark();
 }
 
 }  // namespace siren
