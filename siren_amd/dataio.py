@@ -23,6 +23,16 @@ def get_mgrid(sidelen, dim=2):
     return torch.Tensor(pc).view(-1, dim)
 
 
+def lin2img(tensor, image_resolution=None):
+    """(B, N, C) -> (B, C, H, W), square when no resolution is given (dataio.py:43-52)."""
+    batch_size, num_samples, channels = tensor.shape
+    if image_resolution is None:
+        height = width = int(np.sqrt(num_samples))
+    else:
+        height, width = image_resolution[0], image_resolution[1]
+    return tensor.permute(0, 2, 1).reshape(batch_size, channels, height, width)
+
+
 def synthetic_image(coords):
     """0.6 (sin 8x cos 5y + 0.5 sign(sin 20xy)): the closed-form stand-in for the camera image."""
     x, y = coords[..., 0:1], coords[..., 1:2]
