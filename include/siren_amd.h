@@ -76,7 +76,9 @@ const char* siren_last_error(void);
 /* Number of fp32 values in the flat parameter buffer. */
 int32_t siren_param_count(const siren_cfg* cfg, int64_t* count);
 
-/* Number of fp32 values of packed-weight workspace that siren_pack() fills. */
+/* Number of fp32 values of packed-weight workspace that siren_pack() fills. Hidden widths other than 256 / 512 (the
+ * layered path: rocBLAS layer GEMMs + HIP epilogues over 16384-coordinate chunks) add the chunk scratch to it: the
+ * entry points then write into ws beyond the parameters, so calls sharing one ws must be ordered on one stream. */
 int32_t siren_workspace_floats(const siren_cfg* cfg, int64_t* count);
 
 /* Repack params into the kernels' LDS-slice layout (workspace ws, siren_workspace_floats() floats). */
