@@ -13,10 +13,10 @@ fi
 timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -30 $O/bench.err; exit 1; }
 cat $O/bench.json
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --no-cpu --no-extra --steps 10 > $O/prof.log 2>&1 || { echo "rocprof failed"; tail -20 $O/prof.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --no-cpu --no-extra --no-dp --steps 10 > $O/prof.log 2>&1 || { echo "rocprof failed"; tail -20 $O/prof.log; exit 1; }
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $O/pmc/pass$i -o pmc -- python3 $R/bench.py --no-cpu --no-extra --steps 5 > $O/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $O/pmc/pass$i -o pmc -- python3 $R/bench.py --no-cpu --no-extra --no-dp --steps 5 > $O/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; exit 1; }
 done
 cd $R && python tools/pmc_summary.py $O/pmc 1048576 $O/pmc.json && echo done
