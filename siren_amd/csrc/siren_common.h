@@ -240,6 +240,21 @@ __device__ __forceinline__ void store_block(float* p, int rb, const f32x4& v) {
     p[32] = v[2];
     p[48] = v[3];
 }
+// The same block as ONE coalesced global_store_dwordx4 per lane (1 KiB per instruction instead of four scattered
+// dword stores: epilogue store tails are store-ISSUE-bound, MI355X_MICROARCH.md), transposed through a per-wave LDS
+// scratch of STB_SCRATCH floats (rows padded to 20 floats: conflict-free b32 writes, 16 B-aligned b128 reads). LDS
+// operations of one wave execute in order, so back-to-back blocks may reuse the scratch. tile points at the
+// wave's tile (no lane offset).
+constexpr int STB_ROW = 20;
+constexpr int STB_SCRATCH = 16 * STB_ROW;
+__device__ __forceinline__ void store_block4(float* tile, int rb, const f32x4& v, float* scr, int lane) {
+    const int g = lane >> 4, c = lane & 15;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) scr[(4 * g + r) * STB_ROW + c] = v[r];
+    const int n = lane >> 2, q = lane & 3;
+    const f32x4 w = *(const f32x4*)(scr + n * STB_ROW + 4 * q);
+    *(f32x4*)(tile + rb * 256 + n * 16 + 4 * q) = w;
+}
 __device__ __forceinline__ void store_tile(float* p, const f32x4 (&v)[NB]) {
 #pragma unroll
     for (int rb = 0; rb < NB; ++rb) store_block(p, rb, v[rb]);

@@ -88,7 +88,7 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
                                                         float w, const float* __restrict__ kA,
                                                         const float* __restrict__ kC,
                                                         unsigned long long* __restrict__ prof = nullptr) {
-    __shared__ __attribute__((aligned(16))) float lds[NBUF * SLICE + SMALL_MAX];
+    __shared__ __attribute__((aligned(16))) float lds[NBUF * SLICE + SMALL_MAX + WAVES * STB_SCRATCH];
     float* ring = lds;
     float* sm = lds + NBUF * SLICE;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -110,6 +110,8 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
     float* wsp = spill + tile * (int64_t)(LH + 1) * 3 * NB * 256;
     const int64_t lstride = n_pad * H;
     const int64_t toff = tile * (H * 16) + 4 * g * 16 + c;
+    const int64_t tbase = tile * (H * 16);  // the wave's tile (store_block4)
+    float* stb = lds + NBUF * SLICE + SMALL_MAX + wave * STB_SCRATCH;
     auto kept_c = [&](int l, int rb) -> f32x4 {
         return *(const f32x4*)(kC + cos_off(blockIdx.x, wave, LH, l, rb, lane));
     };
@@ -163,8 +165,8 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
             if (!THETA) *spill_at(wsp, 0, 2, rb, lane) = sn;  // THETA: a_l comes back from the A tiles
         }
         if (THETA) {
-            if (!KEPT) store_block(A + toff, rb, actp[rb]);
-            store_block(At + toff, rb, actt[rb]);
+            if (!KEPT) store_block4(A + tbase, rb, actp[rb], stb, lane);
+            store_block4(At + tbase, rb, actt[rb], stb, lane);
         }
     }
 
@@ -182,7 +184,7 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
                 const f32x4 zd = acct[rb];
                 actt[rb] = (w * kept_c(l, rb)) * zd;
                 *spill_at(wsp, l, 1, rb, lane) = zd;
-                if (THETA) store_block(At + l * lstride + toff, rb, actt[rb]);
+                if (THETA) store_block4(At + l * lstride + tbase, rb, actt[rb], stb, lane);
             }
             mark();
             continue;
@@ -208,8 +210,8 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
             *spill_at(wsp, l, 1, rb, lane) = zd;
             if (!THETA) *spill_at(wsp, l, 2, rb, lane) = sn;
             if (THETA) {
-                store_block(A + l * lstride + toff, rb, actp[rb]);
-                store_block(At + l * lstride + toff, rb, actt[rb]);
+                store_block4(A + l * lstride + tbase, rb, actp[rb], stb, lane);
+                store_block4(At + l * lstride + tbase, rb, actt[rb], stb, lane);
             }
         }
         mark();
@@ -253,8 +255,8 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
         actt[rb] = (w * cs) * adb;
         actp[rb] = (w * cs) * abseed - (w * w) * sn * zd * adb;
         if (THETA) {
-            store_block(D + LH * lstride + toff, rb, actp[rb]);
-            store_block(Dt + LH * lstride + toff, rb, actt[rb]);
+            store_block4(D + LH * lstride + tbase, rb, actp[rb], stb, lane);
+            store_block4(Dt + LH * lstride + tbase, rb, actt[rb], stb, lane);
         }
     }
     mark();
@@ -273,8 +275,8 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
             actt[rb] = wc * acct[rb];
             actp[rb] = wc * accp[rb] - (wl * wl) * sn * zd * acct[rb];
             if (THETA) {
-                store_block(D + (l - 1) * lstride + toff, rb, actp[rb]);
-                store_block(Dt + (l - 1) * lstride + toff, rb, actt[rb]);
+                store_block4(D + (l - 1) * lstride + tbase, rb, actp[rb], stb, lane);
+                store_block4(Dt + (l - 1) * lstride + tbase, rb, actt[rb], stb, lane);
             }
         }
         mark();
