@@ -8,8 +8,11 @@
 //   wgrad_kernel : dW_l = delta_l^T a_{l-1}, db_l = sum delta_l   (l = 1..LH), v_mfma_f32_16x16x4_f32, split-K
 //   small_kernel : dW_0 = delta_0^T x, db_0, dW_out = gy^T a_LH, db_out  (VALU; K = d_in / d_out <= 4)
 //   reduce_kernel: deterministic sum of the per-split partial slabs into the flat gradient (param order)
+#include <type_traits>
+
 #include "siren_common.h"
 #include "siren_params.h"
+#include "lds_ops.h"
 
 namespace siren {
 
@@ -17,17 +20,25 @@ constexpr int WG_TILE_FLOATS = H * 16;          // 256 neurons of one 16-coordin
 constexpr int WG_SLOT = 2 * WG_TILE_FLOATS;     // delta (half-)tile + activation (half-)tile
 constexpr int WG_NBUF = 3;
 
+// Ring layout: a staged 1 KiB chunk is 16 neuron rows of 64 B (16 coordinates); row r keeps its coordinate quad c
+// at 16 B position (c + (r >> 1)) & 3. The swizzle is applied by the global side of the load (lane L fills LDS
+// position L & 3 of row L >> 2, so it fetches quad ((L & 3) - (L >> 3)) & 3 of that row), and with it the operand
+// reads (lane (g, i) reads quad g of row i) put every 16-lane ds_read_b128 group on 16 distinct 16 B slots of the
+// 256 B bank row: conflict-free (the linear layout was 2-way, 5.6 conflict cycles per LDS instruction).
+__device__ __forceinline__ unsigned wg_swz_off(int lane) {
+    const int rr = lane >> 2, p = lane & 3;
+    return (unsigned)(rr * 64 + (((p - (rr >> 1)) & 3) * 16));
+}
+
 __device__ __forceinline__ void wg_issue(const float* __restrict__ dsrc, const float* __restrict__ asrc, float* ring,
-                                         int64_t t, int64_t t1, int k, int wave, int lane, int64_t tstride) {
+                                         int64_t t, int64_t t1, int k, int wave, unsigned swz, int64_t tstride) {
     if (t < t1) {
         float* slot = ring + (k % WG_NBUF) * WG_SLOT;
         const int wu = __builtin_amdgcn_readfirstlane(wave);
+        // wave wu stages 8 chunks of 1 KiB: waves 0, 1 the delta tile, waves 2, 3 the activation tile
+        const float* src = (wu < 2 ? dsrc + wu * 2048 : asrc + (wu - 2) * 2048) + t * tstride;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int chunk = wu * 8 + q;  // 32 chunks of 1 KiB: 0..15 delta tile, 16..31 activation tile
-            const float* src = chunk < 16 ? dsrc + t * tstride + chunk * 256 : asrc + t * tstride + (chunk - 16) * 256;
-            glds_x4(src, 16u * lane, lds_addr(slot + chunk * 256));
-        }
+        for (int q = 0; q < 8; ++q) glds_x4(src + q * 256, swz, lds_addr(slot + (wu * 8 + q) * 256));
     }
 }
 
@@ -35,6 +46,9 @@ __device__ __forceinline__ void wg_issue(const float* __restrict__ dsrc, const f
 // into the 256x256 block q = (qr, qc) of dW_l (the whole dW_l for h = 256; a quadrant for h = 512, staging
 // only the 256-neuron halves of the delta and activation tiles it needs).
 // Wave w owns the 128x128 sub-block (rows 128*(w>>1), cols 128*(w&1)).
+// Software-pipelined: a tile's 16 operand reads are issued into the second register set while the previous tile's
+// 256 MFMAs run (the first version waited lgkmcnt(0) on them at the top of every tile, behind the barrier), and
+// the bias gradient accumulates from the delta operands already in registers (no extra LDS row reads).
 __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restrict__ abuf,
                                                           const float* __restrict__ dbuf, int64_t n_pad,
                                                           int64_t tps, float* __restrict__ partial, int64_t P,
@@ -58,50 +72,122 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
     const int64_t t0 = (int64_t)s * tps, t1 = t0 + tps < T ? t0 + tps : T;
     const float* dsrc = dbuf + (int64_t)l * n_pad * h + qr * WG_TILE_FLOATS;
     const float* asrc = abuf + (int64_t)(l - 1) * n_pad * h + qc * WG_TILE_FLOATS;
+    const unsigned swz = wg_swz_off(lane);
+    // byte offsets of this lane's operand reads inside a ring slot (block rb / cb adds 1 KiB)
+    const unsigned rd = (unsigned)(i * 64 + ((g + (i >> 1)) & 3) * 16);
+    const unsigned ring_base = lds_addr(ring);
+    const unsigned ra = ring_base + rd + 128 * wr * 64;
+    const unsigned rbv = ring_base + rd + (unsigned)WG_TILE_FLOATS * 4 + 128 * wc * 64;
 
     f32x4 acc[8][8];
 #pragma unroll
     for (int a = 0; a < 8; ++a)
 #pragma unroll
         for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float bsum = 0.f;
+    // bias partial sums: lane (g, i) accumulates the value columns of delta row 128 wr + 16 rb + i among
+    // coordinates 4g..4g+3 (jet tiles: column 4g only; two-stream tiles: 4g, 4g + 2) -- m1..m3 are exact 0/1 masks
+    float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const float m1 = jet_bias ? 0.f : 1.f, m2 = jet_bias == 1 ? 0.f : 1.f, m3 = m1;
 
-    wg_issue(dsrc, asrc, ring, t0, t1, 0, wave, lane, tstride);
-    wg_issue(dsrc, asrc, ring, t0 + 1, t1, 1, wave, lane, tstride);
-    int k = 0;
-    for (int64_t t = t0; t < t1; ++t, ++k) {
-        if (t + 1 < t1)
+    f32x4 av[8], bv[8];
+    // Operands are reloaded for the next tile as soon as their last MFMA of this tile has issued: A block rb after
+    // its 32 MFMAs, B block cb inside the last A block (cb pairs outermost there). One register set, one loop body
+    // (a double-buffered B set with a two-body loop spilled: the 256 accumulators fill the AGPR file). The reads
+    // are inline-asm ds_read_b128 at immediate offsets (a C++ f32x4 load from a runtime slot lost the 16 B
+    // alignment and split into ds_read2_b32 pairs); they read slot (k + 1) % 3 unconditionally (stale data after
+    // the last tile is never used), and the closing wait ties every operand register so no MFMA of the next tile
+    // can be scheduled above it.
+    auto lgkm_all = [&]() {
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(av[0]), "+v"(av[1]), "+v"(av[2]), "+v"(av[3]), "+v"(av[4]), "+v"(av[5]), "+v"(av[6]),
+                       "+v"(av[7]), "+v"(bv[0]), "+v"(bv[1]), "+v"(bv[2]), "+v"(bv[3]), "+v"(bv[4]), "+v"(bv[5]),
+                       "+v"(bv[6]), "+v"(bv[7])::"memory");
+    };
+    auto block = [&](auto RB, unsigned va_next) {
+        constexpr int rb = decltype(RB)::value;
+        const f32x4 v = av[rb];
+        bs[rb] += (v[0] + m2 * v[2]) + (m1 * v[1] + m3 * v[3]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int cb = 0; cb < 8; ++cb) acc[rb][cb] = mfma4(v[r], bv[cb][r], acc[rb][cb]);
+        av[rb] = lds_read4<rb * 1024>(va_next);
+        __builtin_amdgcn_sched_barrier(0);  // keep the reload between its block's MFMAs and the next block's
+    };
+    auto last_block = [&](unsigned va_next, unsigned vb_next) {
+        const f32x4 v = av[7];
+        bs[7] += (v[0] + m2 * v[2]) + (m1 * v[1] + m3 * v[3]);
+        av[7] = lds_read4<7 * 1024>(va_next);
+        __builtin_amdgcn_sched_barrier(0);
+        // cb pairs outermost (a dependent MFMA two issues behind clears the 16x16x4 f32 latency); B block cb is
+        // reloaded after its pair
+#define WG_PAIR(CB)                                                                    \
+    {                                                                                  \
+        _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                \
+            acc[7][CB] = mfma4(v[r], bv[CB][r], acc[7][CB]);                           \
+            acc[7][CB + 1] = mfma4(v[r], bv[CB + 1][r], acc[7][CB + 1]);               \
+        }                                                                              \
+        bv[CB] = lds_read4<CB * 1024>(vb_next);                                        \
+        bv[CB + 1] = lds_read4<(CB + 1) * 1024>(vb_next);                              \
+        __builtin_amdgcn_sched_barrier(0);                                             \
+    }
+        WG_PAIR(0)
+        WG_PAIR(2)
+        WG_PAIR(4)
+        WG_PAIR(6)
+#undef WG_PAIR
+    };
+
+    wg_issue(dsrc, asrc, ring, t0, t1, 0, wave, swz, tstride);
+    wg_issue(dsrc, asrc, ring, t0 + 1, t1, 1, wave, swz, tstride);
+    wg_issue(dsrc, asrc, ring, t0 + 2, t1, 2, wave, swz, tstride);
+    if (t0 < t1) {
+        if (t0 + 2 < t1)
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else if (t0 + 1 < t1)
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        wg_issue(dsrc, asrc, ring, t + 2, t1, k + 2, wave, lane, tstride);
-        const float* sd = ring + (k % WG_NBUF) * WG_SLOT;
-        const float* sa = sd + WG_TILE_FLOATS;
-        // bias gradient: thread t owns neuron t (jet tiles: the bias only enters the value columns 0, 4, 8, 12)
-        {
-            const f32x4* row = (const f32x4*)(sd + threadIdx.x * 16);
-            if (jet_bias == 2) {  // two-stream jet tiles (wide_jet_kernel.hpp): value columns 0, 2, ..., 14
-                bsum += ((row[0][0] + row[0][2]) + (row[1][0] + row[1][2])) +
-                        ((row[2][0] + row[2][2]) + (row[3][0] + row[3][2]));
-            } else if (jet_bias) {
-                bsum += (row[0][0] + row[1][0]) + (row[2][0] + row[3][0]);
-            } else {
-                const f32x4 v = row[0] + row[1] + row[2] + row[3];
-                bsum += (v[0] + v[1]) + (v[2] + v[3]);
-            }
-        }
-        f32x4 av[8], bv[8];
-#pragma unroll
-        for (int rb = 0; rb < 8; ++rb) av[rb] = *(const f32x4*)(sd + (128 * wr + 16 * rb + i) * 16 + 4 * g);
-#pragma unroll
-        for (int cb = 0; cb < 8; ++cb) bv[cb] = *(const f32x4*)(sa + (128 * wc + 16 * cb + i) * 16 + 4 * g);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int rb = 0; rb < 8; ++rb)
-#pragma unroll
-                for (int cb = 0; cb < 8; ++cb) acc[rb][cb] = mfma4(av[rb][r], bv[cb][r], acc[rb][cb]);
+        av[0] = lds_read4<0>(ra);
+        av[1] = lds_read4<1024>(ra);
+        av[2] = lds_read4<2048>(ra);
+        av[3] = lds_read4<3072>(ra);
+        av[4] = lds_read4<4096>(ra);
+        av[5] = lds_read4<5120>(ra);
+        av[6] = lds_read4<6144>(ra);
+        av[7] = lds_read4<7168>(ra);
+        bv[0] = lds_read4<0>(rbv);
+        bv[1] = lds_read4<1024>(rbv);
+        bv[2] = lds_read4<2048>(rbv);
+        bv[3] = lds_read4<3072>(rbv);
+        bv[4] = lds_read4<4096>(rbv);
+        bv[5] = lds_read4<5120>(rbv);
+        bv[6] = lds_read4<6144>(rbv);
+        bv[7] = lds_read4<7168>(rbv);
+        lgkm_all();
+    }
+    int k = 0;
+    for (int64_t t = t0; t < t1; ++t, ++k) {
+        // tile t + 1 has landed (tile t + 2 may still be in flight); the barrier also retires every wave's reads of
+        // slot k % 3 (tile t, in registers), which the issue of tile t + 3 overwrites
+        if (t + 2 < t1)
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        wg_issue(dsrc, asrc, ring, t + 3, t1, k + 3, wave, swz, tstride);
+        const unsigned so = (unsigned)(((k + 1) % WG_NBUF) * WG_SLOT * 4);
+        const unsigned va_next = ra + so, vb_next = rbv + so;
+        block(std::integral_constant<int, 0>{}, va_next);
+        block(std::integral_constant<int, 1>{}, va_next);
+        block(std::integral_constant<int, 2>{}, va_next);
+        block(std::integral_constant<int, 3>{}, va_next);
+        block(std::integral_constant<int, 4>{}, va_next);
+        block(std::integral_constant<int, 5>{}, va_next);
+        block(std::integral_constant<int, 6>{}, va_next);
+        last_block(va_next, vb_next);
+        lgkm_all();
     }
 
     float* out = partial + (int64_t)s * P;
@@ -114,7 +200,18 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
             for (int q = 0; q < 4; ++q)
                 dW[(int64_t)(256 * qr + 128 * wr + 16 * rb + 4 * g + q) * h + 256 * qc + 128 * wc + 16 * cb + i] =
                     acc[rb][cb][q];
-    if (qc == 0) out[off.b(l) + 256 * qr + threadIdx.x] = with_bias ? bsum : 0.f;
+    // bias: the value columns of lane group g (jet tiles: columns 0, 4, 8, 12; two-stream tiles: 0, 2, ..., 14),
+    // then the four groups of each row combined in a fixed order through the (now idle) ring
+    __syncthreads();
+    if (wc == 0) {
+#pragma unroll
+        for (int rb = 0; rb < 8; ++rb) ring[(128 * wr + 16 * rb + i) * 4 + g] = bs[rb];
+    }
+    __syncthreads();
+    if (qc == 0) {
+        const float* rw = ring + threadIdx.x * 4;
+        out[off.b(l) + 256 * qr + threadIdx.x] = with_bias ? (rw[0] + rw[1]) + (rw[2] + rw[3]) : 0.f;
+    }
 }
 
 // ---- first / output layer gradients ("edge" layers: K = d_in or d_out, VALU) ------------------------------------
