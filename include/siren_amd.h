@@ -184,6 +184,18 @@ int32_t siren_hvp_backward(const siren_cfg* cfg, const float* ws, const float* x
                            const float* u, const float* g, float* tws, float* gx, float* gparams, float* gv,
                            float* gu, void* stream);
 
+/* Split-bf16 W1 (precision mode "bf16x6"): siren_forward_grad with gy = ones for the headline network (hidden 256,
+ * 3 hidden layers, d_in 2 / 3, d_out 1, linear output) with the layer GEMMs on the bf16 matrix pipe. Every fp32
+ * weight and activation is split exactly into three bf16 pieces (hi + mid + lo) and each K-step sums the six products
+ * down to 2^-16 of the leading one, accumulated in fp32: the error against the fp64 reference is that of the fp32
+ * kernel. siren_pack_split fills wsx (siren_split_ws_floats floats) from the flat parameters, once
+ * per weight update; siren_forward_grad_split replaces siren_forward_grad(cfg, ws, x, n, NULL, y, gx, NULL, stream)
+ * (diff_operators.gradient, diff_operators.py:39-43; y nullable). */
+int32_t siren_split_ws_floats(const siren_cfg* cfg, int64_t* count);
+int32_t siren_pack_split(const siren_cfg* cfg, const float* params, float* wsx, void* stream);
+int32_t siren_forward_grad_split(const siren_cfg* cfg, const float* wsx, const float* x, int64_t n, float* y,
+                                 float* gx, void* stream);
+
 /* Diagnostics: the W1 kernel (hidden 256, 3 hidden layers) with s_memtime stamps. stamps receives
  * 256 workgroups x 4 tiles x 4 waves x 8 events (uint64; event 0 tile start, 1..6 after GEMM 0..5, 7 tile end);
  * unrecorded entries are left untouched. y / gx as siren_forward_grad with gy = ones. */

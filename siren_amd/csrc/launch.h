@@ -33,6 +33,12 @@ void launch_legacy_grad(bool store, dim3 grid, hipStream_t st, const FusedArgs& 
 void launch_w1(int mode, dim3 grid, hipStream_t st, const FusedArgs& a);
 void launch_w0(dim3 grid, hipStream_t st, const FusedArgs& a);
 void launch_w0s(dim3 grid, hipStream_t st, const FusedArgs& a);
+// tu_w1x.hip: split-bf16 W1 (bf16x6 products on the bf16 matrix pipe; 3 hidden layers, d_in 2 / 3, d_out 1,
+// gy = ones); the stream holds split_stream_words(lh) 32-bit words
+int64_t split_stream_words(int lh);
+void launch_pack_split(const float* p, unsigned* stream, int d, int o, int lh, float s, hipStream_t st);
+void launch_w1x(dim3 grid, hipStream_t st, const float* ws_small, const unsigned* stream, const float* x, int64_t n,
+                float* y, float* gx, int d, float w0, float w);
 // tu_w4.hip: JET mode (16 coordinates per workgroup); lap (n) = sum_j Laplacian(y_j), gx (n, d) = sum_j grad y_j
 void launch_w4(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, float* y, float* gx, float* lap,
                int d, int o, int lh, float w0, float w);

@@ -289,6 +289,49 @@ int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x
     return hip_status("siren_forward_grad");
 }
 
+// ---- split-bf16 W1 (w1x_kernel.hpp): workspace [unscaled small block | phase-scaled small block | bf16 stream] ----
+static int split_ok(const siren_cfg* cfg) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (cfg->hidden != siren::H || cfg->n_hidden != 3 || cfg->d_out != 1 || (cfg->d_in != 2 && cfg->d_in != 3) ||
+        !cfg->outermost_linear || cfg->omega_first == 0.f || cfg->omega_hidden == 0.f)
+        return fail(SIREN_EUNSUPPORTED, "the split-bf16 W1 covers hidden 256, 3 hidden layers, in_features 2 / 3, "
+                                        "out_features 1, linear output, nonzero omegas");
+    return SIREN_OK;
+}
+
+int32_t siren_split_ws_floats(const siren_cfg* cfg, int64_t* count) {
+    if (int rc = split_ok(cfg)) return rc;
+    if (count == nullptr) return fail(SIREN_EINVAL, "count is NULL");
+    *count = 2 * small_pad(cfg) + siren::split_stream_words(cfg->n_hidden);
+    return SIREN_OK;
+}
+
+int32_t siren_pack_split(const siren_cfg* cfg, const float* params, float* wsx, void* stream) {
+    if (int rc = split_ok(cfg)) return rc;
+    if (params == nullptr || wsx == nullptr) return fail(SIREN_EINVAL, "params/wsx is NULL");
+    const int64_t spad = small_pad(cfg);
+    // small blocks: pack_kernel over [0, 2 spad) with the scaled copy starting at spad (the stream part is empty)
+    siren::launch_pack(params, wsx, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden, spad, 2 * spad, spad,
+                       cfg->omega_first * kInv2Pi, cfg->omega_hidden * kInv2Pi, (hipStream_t)stream);
+    siren::launch_pack_split(params, (unsigned*)(wsx + 2 * spad), cfg->d_in, cfg->d_out, cfg->n_hidden,
+                             cfg->omega_hidden * kInv2Pi, (hipStream_t)stream);
+    return hip_status("siren_pack_split");
+}
+
+int32_t siren_forward_grad_split(const siren_cfg* cfg, const float* wsx, const float* x, int64_t n, float* y,
+                                 float* gx, void* stream) {
+    if (int rc = split_ok(cfg)) return rc;
+    if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    if (n == 0) return SIREN_OK;
+    if (wsx == nullptr || x == nullptr || gx == nullptr) return fail(SIREN_EINVAL, "wsx/x/gx is NULL");
+    const int64_t blocks = (n + siren::TILE - 1) / siren::TILE;
+    if (blocks > 0x7fffffffll) return fail(SIREN_EINVAL, "n too large");
+    const int64_t spad = small_pad(cfg);
+    siren::launch_w1x(tile_grid(cfg, blocks, 1), (hipStream_t)stream, wsx + spad, (const unsigned*)(wsx + 2 * spad), x,
+                      n, y, gx, cfg->d_in, cfg->omega_first, cfg->omega_hidden);
+    return hip_status("siren_forward_grad_split");
+}
+
 // diagnostics: while set, W3 launches record s_memtime phase stamps (w3_kernel.hpp) into stamps[256][16]
 static unsigned long long* g_w3_prof = nullptr;
 int32_t siren_w3_phase_profile(uint64_t* stamps) {

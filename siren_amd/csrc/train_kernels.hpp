@@ -73,11 +73,11 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
     const float* dsrc = dbuf + (int64_t)l * n_pad * h + qr * WG_TILE_FLOATS;
     const float* asrc = abuf + (int64_t)(l - 1) * n_pad * h + qc * WG_TILE_FLOATS;
     const unsigned swz = wg_swz_off(lane);
-    // byte offsets of this lane's operand reads inside a ring slot (block rb / cb adds 1 KiB)
-    const unsigned rd = (unsigned)(i * 64 + ((g + (i >> 1)) & 3) * 16);
-    const unsigned ring_base = lds_addr(ring);
-    const unsigned ra = ring_base + rd + 128 * wr * 64;
-    const unsigned rbv = ring_base + rd + (unsigned)WG_TILE_FLOATS * 4 + 128 * wc * 64;
+    // f32x4 index of this lane's operand reads inside a ring slot (block rb / cb adds 64, 1 KiB)
+    const int rd = i * 4 + ((g + (i >> 1)) & 3);
+    const int ra = rd + 512 * wr;
+    const int rbv = rd + WG_TILE_FLOATS / 4 + 512 * wc;
+    const f32x4* rv = (const f32x4*)ring;
 
     f32x4 acc[8][8];
 #pragma unroll
@@ -92,18 +92,12 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
     f32x4 av[8], bv[8];
     // Operands are reloaded for the next tile as soon as their last MFMA of this tile has issued: A block rb after
     // its 32 MFMAs, B block cb inside the last A block (cb pairs outermost there). One register set, one loop body
-    // (a double-buffered B set with a two-body loop spilled: the 256 accumulators fill the AGPR file). The reads
-    // are inline-asm ds_read_b128 at immediate offsets (a C++ f32x4 load from a runtime slot lost the 16 B
-    // alignment and split into ds_read2_b32 pairs); they read slot (k + 1) % 3 unconditionally (stale data after
-    // the last tile is never used), and the closing wait ties every operand register so no MFMA of the next tile
-    // can be scheduled above it.
-    auto lgkm_all = [&]() {
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(av[0]), "+v"(av[1]), "+v"(av[2]), "+v"(av[3]), "+v"(av[4]), "+v"(av[5]), "+v"(av[6]),
-                       "+v"(av[7]), "+v"(bv[0]), "+v"(bv[1]), "+v"(bv[2]), "+v"(bv[3]), "+v"(bv[4]), "+v"(bv[5]),
-                       "+v"(bv[6]), "+v"(bv[7])::"memory");
-    };
-    auto block = [&](auto RB, unsigned va_next) {
+    // (a double-buffered B set with a two-body loop spilled: the 256 accumulators fill the AGPR file). The reads are
+    // plain LDS loads through an f32x4 pointer (ds_read_b128; hipcc counts and places their waits itself, so no
+    // register of an in-flight load is ever copied -- inline-asm reads are invisible to its bookkeeping,
+    // tools/check_asm_waits.py), read slot (k + 1) % 3 unconditionally (stale data after the last tile is never
+    // used), and sched_barrier(0) keeps each reload between its block's MFMAs and the next block's.
+    auto block = [&](auto RB, int vn) {
         constexpr int rb = decltype(RB)::value;
         const f32x4 v = av[rb];
         bs[rb] += (v[0] + m2 * v[2]) + (m1 * v[1] + m3 * v[3]);
@@ -111,13 +105,13 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int cb = 0; cb < 8; ++cb) acc[rb][cb] = mfma4(v[r], bv[cb][r], acc[rb][cb]);
-        av[rb] = lds_read4<rb * 1024>(va_next);
-        __builtin_amdgcn_sched_barrier(0);  // keep the reload between its block's MFMAs and the next block's
+        av[rb] = rv[vn + ra + rb * 64];
+        __builtin_amdgcn_sched_barrier(0);
     };
-    auto last_block = [&](unsigned va_next, unsigned vb_next) {
+    auto last_block = [&](int vn) {
         const f32x4 v = av[7];
         bs[7] += (v[0] + m2 * v[2]) + (m1 * v[1] + m3 * v[3]);
-        av[7] = lds_read4<7 * 1024>(va_next);
+        av[7] = rv[vn + ra + 7 * 64];
         __builtin_amdgcn_sched_barrier(0);
         // cb pairs outermost (a dependent MFMA two issues behind clears the 16x16x4 f32 latency); B block cb is
         // reloaded after its pair
@@ -127,8 +121,8 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
             acc[7][CB] = mfma4(v[r], bv[CB][r], acc[7][CB]);                           \
             acc[7][CB + 1] = mfma4(v[r], bv[CB + 1][r], acc[7][CB + 1]);               \
         }                                                                              \
-        bv[CB] = lds_read4<CB * 1024>(vb_next);                                        \
-        bv[CB + 1] = lds_read4<(CB + 1) * 1024>(vb_next);                              \
+        bv[CB] = rv[vn + rbv + (CB) * 64];                                             \
+        bv[CB + 1] = rv[vn + rbv + (CB + 1) * 64];                                     \
         __builtin_amdgcn_sched_barrier(0);                                             \
     }
         WG_PAIR(0)
@@ -148,24 +142,12 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        av[0] = lds_read4<0>(ra);
-        av[1] = lds_read4<1024>(ra);
-        av[2] = lds_read4<2048>(ra);
-        av[3] = lds_read4<3072>(ra);
-        av[4] = lds_read4<4096>(ra);
-        av[5] = lds_read4<5120>(ra);
-        av[6] = lds_read4<6144>(ra);
-        av[7] = lds_read4<7168>(ra);
-        bv[0] = lds_read4<0>(rbv);
-        bv[1] = lds_read4<1024>(rbv);
-        bv[2] = lds_read4<2048>(rbv);
-        bv[3] = lds_read4<3072>(rbv);
-        bv[4] = lds_read4<4096>(rbv);
-        bv[5] = lds_read4<5120>(rbv);
-        bv[6] = lds_read4<6144>(rbv);
-        bv[7] = lds_read4<7168>(rbv);
-        lgkm_all();
+        asm volatile("s_barrier" ::: "memory");  // also a compiler barrier for the LDS loads
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            av[q] = rv[ra + q * 64];
+            bv[q] = rv[rbv + q * 64];
+        }
     }
     int k = 0;
     for (int64_t t = t0; t < t1; ++t, ++k) {
@@ -175,19 +157,19 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        asm volatile("s_barrier" ::: "memory");  // also a compiler barrier for the LDS loads
         wg_issue(dsrc, asrc, ring, t + 3, t1, k + 3, wave, swz, tstride);
-        const unsigned so = (unsigned)(((k + 1) % WG_NBUF) * WG_SLOT * 4);
-        const unsigned va_next = ra + so, vb_next = rbv + so;
-        block(std::integral_constant<int, 0>{}, va_next);
-        block(std::integral_constant<int, 1>{}, va_next);
-        block(std::integral_constant<int, 2>{}, va_next);
-        block(std::integral_constant<int, 3>{}, va_next);
-        block(std::integral_constant<int, 4>{}, va_next);
-        block(std::integral_constant<int, 5>{}, va_next);
-        block(std::integral_constant<int, 6>{}, va_next);
-        last_block(va_next, vb_next);
-        lgkm_all();
+        const int vn = ((k + 1) % WG_NBUF) * (WG_SLOT / 4);
+        block(std::integral_constant<int, 0>{}, vn);
+        block(std::integral_constant<int, 1>{}, vn);
+        block(std::integral_constant<int, 2>{}, vn);
+        block(std::integral_constant<int, 3>{}, vn);
+        block(std::integral_constant<int, 4>{}, vn);
+        block(std::integral_constant<int, 5>{}, vn);
+        block(std::integral_constant<int, 6>{}, vn);
+        last_block(vn);
+        // every read of this tile's slot is retired before the next barrier (the next issue overwrites it)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
 
     float* out = partial + (int64_t)s * P;

@@ -1,0 +1,23 @@
+// tu_w1x.hip — the split-bf16 W1 kernel (w1x_kernel.hpp) and its weight pack.
+#include "launch.h"
+#include "w1x_kernel.hpp"
+
+namespace siren {
+
+int64_t split_stream_words(int lh) { return (int64_t)x_slices(lh) * X_SLICE; }
+
+void launch_pack_split(const float* p, unsigned* stream, int d, int o, int lh, float s, hipStream_t st) {
+    const int64_t total = (int64_t)x_slices(lh) * 3 * X_OBS * 64;
+    hipLaunchKernelGGL(pack_split_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, p, stream, d, o, lh,
+                       s);
+}
+
+void launch_w1x(dim3 grid, hipStream_t st, const float* ws_small, const unsigned* stream, const float* x, int64_t n,
+                float* y, float* gx, int d, float w0, float w) {
+    if (d == 2)
+        hipLaunchKernelGGL((w1x_kernel<3, 2>), grid, dim3(THREADS), 0, st, ws_small, stream, x, n, y, gx, w0, w);
+    else
+        hipLaunchKernelGGL((w1x_kernel<3, 3>), grid, dim3(THREADS), 0, st, ws_small, stream, x, n, y, gx, w0, w);
+}
+
+}  // namespace siren

@@ -1,0 +1,395 @@
+// w1x_kernel.hpp — W1 (fused SIREN forward + coordinate vector-Jacobian product, gy = ones) with the hidden-layer
+// GEMMs on the bf16 matrix pipe in fp32-equivalent precision ("bf16x6").
+//
+// Every fp32 operand is split exactly into three bf16 pieces by truncation, v = hi + mid + lo (hi = the top 8
+// significand bits, mid the next 8, lo the last 8; both subtractions are exact), and each K-step of a layer GEMM
+// sums the six products whose magnitude is at or above 2^-16 of hi*hi:
+//     lo(W) hi(a) + mid(W) mid(a) + hi(W) lo(a) + mid(W) hi(a) + hi(W) mid(a) + hi(W) hi(a)
+// in fp32 on v_mfma_f32_16x16x32_bf16 (bf16 x bf16 products are exact in fp32). The dropped terms are 2^-24 of the
+// leading one, the fp32 rounding level: against the fp64 goldens this matches the fp32 kernel (G1 gradient
+// 1.4e-6 vs 2.0e-6, G2 8.6e-6 vs 8.3e-6 relative; a three-product split lands at 9e-5 / 2.2e-4 and is not used).
+// The bf16 pipe issues a 16x16x32 MFMA every 16 cycles against 32 cycles for the fp32 16x16x4, i.e. 8x the K per
+// cycle, so six of them cost 2.67x less matrix time than the fp32 K-step.
+//
+// Tiling (one wave = 16 coordinates = the MFMA columns, as in w1_kernel.hpp):
+//   * A = weights. The pack (pack_split_kernel) pre-splits the phase-scaled weights of the 2 L layer GEMMs into
+//     slices of half a K-step: 8 output blocks x (hi, mid, lo) x 1 KiB, lane (g, m) holding the 8 bf16 of row
+//     16 ob + m at K positions kn(s, g, j) = 32 s + 16 (j >> 2) + 4 g + (j & 3), j = 0..7.
+//   * B = activations. After a layer's epilogue, lane (g, c) holds rows 16 b + 4 g + r of column c (the C/D layout);
+//     blocks 2s and 2s+1 give exactly the 8 values kn(s, g, 0..7) of K-step s, so the split pieces of the next
+//     layer's B operand are built in place (v_perm of the upper halves), with no lane exchange.
+//   * A 4-slot LDS ring of 24 KiB slices (global_load_lds), one barrier per slice placed mid-slice (it publishes
+//     slice S+1 and frees slot S-1 for slice S+3); the A pieces of the next output block are read one block ahead
+//     with a counted lgkmcnt.
+//   * The epilogue producing K-step s+1's B operand (two blocks) runs in the MFMA shadow of K-step s; cos(w z_l)
+//     of the forward layers is parked in AGPRs for the reverse sweep; the ring streams across the coordinate tiles
+//     of a persistent grid.
+// Epilogues (phase-scaled pack, as w1_kernel.hpp): FIRST a_0 = sin(x W0^T + b0), SINCOS a_G, SEED (y partials and
+// delta_L = seed . cos . w), DELTA delta_l = u_l . cos_l . 2 pi; then delta_0 and gx = delta_0 W0 (VALU).
+#pragma once
+#include <type_traits>
+
+#include "lds_ops.h"
+#include "siren_common.h"
+
+namespace siren {
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int X_OBS = 8;                            // output blocks per slice (half a K-step)
+constexpr int X_SLICE = 3 * X_OBS * 256;            // 32-bit words per slice: 8 blocks x (hi, mid, lo) x 1 KiB
+constexpr int X_NBUF = 4;                           // ring slots (96 KiB)
+constexpr int X_KSTEPS = H / 32;                    // K-steps of one 256-wide GEMM
+constexpr int X_SPG = 2 * X_KSTEPS;                 // slices per GEMM
+constexpr int x_slices(int lh) { return 2 * lh * X_SPG; }  // slices per coordinate tile
+
+__device__ __forceinline__ f32x4 mfma_x(const u32x4& a, const u32x4& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                    0, 0, 0);
+}
+
+// exact 3-way bf16 split of two values into the (lo half, hi half) of one word per piece
+__device__ __forceinline__ void split_pair(float v0, float v1, unsigned& h, unsigned& m, unsigned& l) {
+    const unsigned b0 = __float_as_uint(v0), b1 = __float_as_uint(v1);
+    h = __builtin_amdgcn_perm(b1, b0, 0x07060302u);
+    const float r0 = v0 - __uint_as_float(b0 & 0xffff0000u), r1 = v1 - __uint_as_float(b1 & 0xffff0000u);
+    const unsigned c0 = __float_as_uint(r0), c1 = __float_as_uint(r1);
+    m = __builtin_amdgcn_perm(c1, c0, 0x07060302u);
+    const float q0 = r0 - __uint_as_float(c0 & 0xffff0000u), q1 = r1 - __uint_as_float(c1 & 0xffff0000u);
+    l = __builtin_amdgcn_perm(__float_as_uint(q1), __float_as_uint(q0), 0x07060302u);
+}
+
+// block b of a layer's output (lane: rows 16 b + 4 g + r) -> words 2 (b & 1), 2 (b & 1) + 1 of the K-step's pieces
+template <int HALF>
+__device__ __forceinline__ void split_block(const f32x4& v, u32x4 (&p)[3]) {
+    unsigned h0, m0, l0, h1, m1, l1;
+    split_pair(v[0], v[1], h0, m0, l0);
+    split_pair(v[2], v[3], h1, m1, l1);
+    p[0][2 * HALF] = h0;
+    p[0][2 * HALF + 1] = h1;
+    p[1][2 * HALF] = m0;
+    p[1][2 * HALF + 1] = m1;
+    p[2][2 * HALF] = l0;
+    p[2][2 * HALF + 1] = l1;
+}
+
+template <int LH>
+struct XState {
+    u32x4 bx[2][3];    // B operand pieces (hi, mid, lo) of K-step s in bx[s & 1]
+    f32x4 acc[2][NB];  // ping-pong accumulators (GEMM G in acc[G & 1])
+    f32x4 C[LH][NB];   // cos(w z_l), l < LH
+    u32x4 pa[3];       // A pieces of the next output block
+    float xv[4];
+    float yp;
+};
+
+struct XCtx {
+    const unsigned* stream;
+    float* ring;
+    const float* sm;
+    int d, wave, lane, g;
+    float w0, w, wsd, inv_s0;
+    bool more;
+};
+
+// A piece at ring byte offset OFF (compile time) for this lane: a plain LDS load (ds_read_b128), so hipcc counts and
+// places its wait itself -- an inline-asm read is invisible to that bookkeeping and its destination may be copied
+// before the data lands (tools/check_asm_waits.py)
+template <int OFF>
+__device__ __forceinline__ u32x4 xread(const XCtx& cx) {
+    return ((const u32x4*)cx.ring)[OFF / 16 + cx.lane];
+}
+
+// six 1 KiB global->LDS pieces of slice s for this wave (saddr form, as ring_issue4)
+__device__ __forceinline__ void xring_issue(const unsigned* __restrict__ stream, float* ring, int s, int wave,
+                                            unsigned lane_off) {
+    const char* src = (const char*)(stream + (int64_t)s * X_SLICE + wave * 6 * 256);
+    const unsigned dst = lds_addr(ring + (s % X_NBUF) * X_SLICE + wave * 6 * 256);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) glds_x4(src + q * 1024, lane_off, dst + q * 1024);
+}
+
+template <int I, int N, typename F>
+__device__ __forceinline__ void xstatic_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        xstatic_for<I + 1, N>(f);
+    }
+}
+
+__device__ __forceinline__ f32x4 x_to_agpr(f32x4 v) {
+    f32x4 r;
+    asm("; park in agpr" : "=a"(r) : "0"(v));
+    return r;
+}
+__device__ __forceinline__ f32x4 x_from_agpr(f32x4 v) {
+    f32x4 r;
+    asm("; unpark" : "=v"(r) : "0"(v));
+    return r;
+}
+__device__ __forceinline__ f32x4 x_pin(f32x4 v) {
+    asm("; pin" : "+v"(v));
+    return v;
+}
+
+// Epilogue of block B producing the B operand of GEMM E (see the table at the top; the previous GEMM's output is
+// acc[(E + 1) & 1]).
+template <int E, int B, int LH, int D>
+__device__ __forceinline__ void x_epilogue(XState<LH>& st, const XCtx& cx) {
+    constexpr int KS = B >> 1, HALF = B & 1;
+    const int nb = 16 * B + 4 * cx.g;
+    u32x4(&p)[3] = st.bx[KS & 1];
+    if constexpr (E == 0) {
+        f32x4 z = *(const f32x4*)(cx.sm + SM_BIAS + nb);
+#pragma unroll
+        for (int k = 0; k < D; ++k) z += st.xv[k] * *(const f32x4*)(cx.sm + SM_W0 + k * H + nb);
+        f32x4 sn, cs;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float a_, c_;
+            sincos_rev(z[r], a_, c_);
+            sn[r] = a_;
+            cs[r] = c_;
+        }
+        st.C[0][B] = x_pin(cs);
+        split_block<HALF>(sn, p);
+    } else if constexpr (E < LH) {
+        const f32x4 z = st.acc[(E + 1) & 1][B] + *(const f32x4*)(cx.sm + SM_BIAS + E * H + nb);
+        f32x4 sn, cs;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float a_, c_;
+            sincos_rev(z[r], a_, c_);
+            sn[r] = a_;
+            cs[r] = c_;
+        }
+        st.C[E][B] = x_to_agpr(cs);
+        split_block<HALF>(sn, p);
+    } else if constexpr (E == LH) {
+        const f32x4 z = st.acc[(E + 1) & 1][B] + *(const f32x4*)(cx.sm + SM_BIAS + LH * H + nb);
+        f32x4 sn, cs;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float a_, c_;
+            sincos_rev(z[r], a_, c_);
+            sn[r] = a_;
+            cs[r] = c_;
+        }
+        const f32x4 wo = *(const f32x4*)(cx.sm + SM_WO + nb);
+        st.yp += wo[0] * sn[0] + wo[1] * sn[1] + wo[2] * sn[2] + wo[3] * sn[3];
+        const f32x4 dl = (*(const f32x4*)(cx.sm + SM_SEED + nb) * cs) * cx.wsd;
+        split_block<HALF>(dl, p);
+    } else {
+        constexpr int L = 2 * LH - E;  // delta_L = u_L . cos(w z_L) . w, 1 <= L < LH
+        const f32x4 dl = (st.acc[(E + 1) & 1][B] * x_from_agpr(st.C[L][B])) * cx.w;
+        split_block<HALF>(dl, p);
+    }
+}
+
+// Slice (G, KS, HALF): the output blocks ob = 8 HALF .. 8 HALF + 7 of K-step KS, six MFMAs each; the mid-slice ring
+// barrier after block 3; the next block's (or the next slice's first block's) A pieces read one block ahead; then
+// the epilogue block of K-step KS + 1 (block 2 (KS + 1) + HALF) of the previous GEMM's output.
+template <int G, int KS, int HALF, int LH, int D>
+__device__ __forceinline__ void x_slice(XState<LH>& st, const XCtx& cx) {
+    constexpr int NS = x_slices(LH);
+    constexpr int S = G * X_SPG + 2 * KS + HALF;
+    constexpr int SLOT = (S % X_NBUF) * X_SLICE * 4;
+    constexpr int NSLOT = ((S + 1) % X_NBUF) * X_SLICE * 4;
+    f32x4(&acc)[NB] = st.acc[G & 1];
+    const u32x4(&b)[3] = st.bx[KS & 1];
+    xstatic_for<0, X_OBS>([&](auto OBL) {
+        constexpr int obl = decltype(OBL)::value;
+        constexpr int ob = X_OBS * HALF + obl;
+        if constexpr (obl == 4) {
+            if (S + 1 < NS || cx.more) {
+                if (S + 2 < NS || cx.more)
+                    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                asm volatile("s_barrier" ::: "memory");  // also orders the next slice's LDS loads after it
+                if (S + 3 < NS || cx.more) {
+                    const unsigned* sp = cx.stream;
+                    asm volatile("" : "+s"(sp));
+                    xring_issue(sp, cx.ring, (S + 3) % NS, cx.wave, 16u * cx.lane);
+                }
+            }
+        }
+        u32x4 a[3] = {st.pa[0], st.pa[1], st.pa[2]};
+        constexpr bool NEXT_IN_SLICE = obl + 1 < X_OBS;
+        constexpr bool NEXT_SLICE = !NEXT_IN_SLICE && S + 1 < NS;
+        if constexpr (NEXT_IN_SLICE) {
+            st.pa[0] = xread<SLOT + (3 * (obl + 1) + 0) * 1024>(cx);
+            st.pa[1] = xread<SLOT + (3 * (obl + 1) + 1) * 1024>(cx);
+            st.pa[2] = xread<SLOT + (3 * (obl + 1) + 2) * 1024>(cx);
+        } else if constexpr (NEXT_SLICE) {
+            st.pa[0] = xread<NSLOT>(cx);
+            st.pa[1] = xread<NSLOT + 1024>(cx);
+            st.pa[2] = xread<NSLOT + 2048>(cx);
+        } else {  // last slice of the tile: the next tile's slice 0 (published by this slice's barrier) if any
+            if (cx.more) {
+                st.pa[0] = xread<NSLOT>(cx);
+                st.pa[1] = xread<NSLOT + 1024>(cx);
+                st.pa[2] = xread<NSLOT + 2048>(cx);
+                }
+        }
+        // smallest products first
+        acc[ob] = mfma_x(a[2], b[0], acc[ob]);
+        acc[ob] = mfma_x(a[1], b[1], acc[ob]);
+        acc[ob] = mfma_x(a[0], b[2], acc[ob]);
+        acc[ob] = mfma_x(a[1], b[0], acc[ob]);
+        acc[ob] = mfma_x(a[0], b[1], acc[ob]);
+        acc[ob] = mfma_x(a[0], b[0], acc[ob]);
+    });
+    if constexpr (KS + 1 < X_KSTEPS) x_epilogue<G, 2 * (KS + 1) + HALF, LH, D>(st, cx);
+}
+
+template <int G, int LH, int D>
+__device__ __forceinline__ void x_gemm(XState<LH>& st, const XCtx& cx) {
+#pragma unroll
+    for (int ob = 0; ob < NB; ++ob) st.acc[G & 1][ob] = f32x4{0.f, 0.f, 0.f, 0.f};
+    x_epilogue<G, 0, LH, D>(st, cx);
+    x_epilogue<G, 1, LH, D>(st, cx);
+    xstatic_for<0, X_KSTEPS>([&](auto KS) {
+        x_slice<G, decltype(KS)::value, 0, LH, D>(st, cx);
+        x_slice<G, decltype(KS)::value, 1, LH, D>(st, cx);
+    });
+}
+
+template <int G, int LH, int D>
+__device__ __forceinline__ void x_run(XState<LH>& st, const XCtx& cx) {
+    if constexpr (G < 2 * LH) {
+        x_gemm<G, LH, D>(st, cx);
+        x_run<G + 1, LH, D>(st, cx);
+    }
+}
+
+// ws: the split image of siren_pack_split (small block at ws_small, bf16 stream at stream); x (n, D); y (n) / gx
+// (n, D) (y nullable). w0 / w as the fp32 kernel (phase-scaled pack).
+template <int LH, int D>
+__global__ __launch_bounds__(THREADS, 1) void w1x_kernel(const float* __restrict__ ws_small,
+                                                         const unsigned* __restrict__ stream,
+                                                         const float* __restrict__ x, int64_t n,
+                                                         float* __restrict__ y, float* __restrict__ gx, float w0,
+                                                         float w) {
+    constexpr int NS = x_slices(LH);
+    static_assert(NS % X_NBUF == 0, "the ring must wrap onto slot 0 at a tile boundary");
+    __shared__ __attribute__((aligned(16))) float lds[X_NBUF * X_SLICE + SM_BIAS + (LH + 1) * H];
+    XCtx cx;
+    XState<LH> st;
+    cx.ring = lds;
+    float* sm = lds + X_NBUF * X_SLICE;
+    cx.sm = sm;
+    cx.stream = stream;
+    cx.lane = threadIdx.x & 63;
+    cx.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    cx.g = cx.lane >> 4;
+    cx.d = D;
+    const int c = cx.lane & 15;
+    {
+        constexpr float two_pi = 6.28318530717958648f;
+        const float s = w * 0.159154943091895336f;
+        cx.w0 = w0 / s;
+        cx.w = two_pi;
+        cx.wsd = w;
+        cx.inv_s0 = two_pi / w0;
+    }
+    cx.more = false;
+    {
+        const int nf4 = (SM_BIAS + (LH + 1) * H + 3) / 4;
+        for (int e = threadIdx.x; e < nf4; e += THREADS) ((f32x4*)sm)[e] = ((const f32x4*)ws_small)[e];
+    }
+    const int64_t tiles = (n + TILE - 1) / TILE;
+    float xn[4];
+    auto load_inputs = [&](int64_t tile) {
+        const int64_t cd = tile * TILE + cx.wave * 16 + c;
+        const bool ok = tile < tiles && cd < n;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) xn[k] = (ok && k < D) ? x[cd * D + k] : 0.f;
+    };
+    load_inputs(blockIdx.x);
+    __syncthreads();
+    xring_issue(stream, cx.ring, 0, cx.wave, 16u * cx.lane);
+    xring_issue(stream, cx.ring, 1, cx.wave, 16u * cx.lane);
+    xring_issue(stream, cx.ring, 2, cx.wave, 16u * cx.lane);
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
+    st.pa[0] = xread<0>(cx);
+    st.pa[1] = xread<1024>(cx);
+    st.pa[2] = xread<2048>(cx);
+
+#pragma unroll 1
+    for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+        cx.more = tile + gridDim.x < tiles;
+        const int64_t coord = tile * TILE + cx.wave * 16 + c;
+        const bool valid = coord < n;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) st.xv[k] = xn[k];
+        st.yp = 0.f;
+        load_inputs(tile + gridDim.x);
+        x_run<0, LH, D>(st, cx);
+        {
+            const float yv = sum_groups(st.yp) + sm[SM_BOUT];
+            if (y != nullptr && valid && cx.g == 0) y[coord] = yv;
+        }
+        // delta_0 = u_0 . cos(w0 z_0) . w0 (cx.w0 = w0 / s undoes the pack scale); gx = delta_0 W0 (cx.inv_s0)
+        constexpr int GL = (2 * LH - 1) & 1;
+        float q[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int rb = 0; rb < NB; ++rb) {
+            const f32x4 dl = (st.acc[GL][rb] * st.C[0][rb]) * cx.w0;
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                const f32x4 wk = *(const f32x4*)(sm + SM_W0 + k * H + 16 * rb + 4 * cx.g);
+                q[k] += wk[0] * dl[0] + wk[1] * dl[1] + wk[2] * dl[2] + wk[3] * dl[3];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            const float qk = sum_groups(q[k]) * cx.inv_s0;
+            if (valid && cx.g == 0) gx[coord * D + k] = qk;
+        }
+    }
+}
+
+// The split image's bf16 stream from the flat parameters (state-dict order): slice (G, s, half), output block
+// ob = 8 half + obl, piece p: lane (g, m) holds 8 bf16 of A row 16 ob + m at K positions kn(s, g, j), where A is
+// s_scale W_{G+1} for the forward GEMMs G < LH and s_scale W_{2LH-G}^T for the reverse ones (s_scale = w / 2 pi, the
+// phase-scaled pack). One thread per (slice, chunk, lane) word quad.
+__global__ void pack_split_kernel(const float* __restrict__ p, unsigned* __restrict__ stream, int d, int o, int lh,
+                                  float s_scale) {
+    const int64_t total = (int64_t)x_slices(lh) * 3 * X_OBS * 64;
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= total) return;
+    const int lane = (int)(q & 63), chunk = (int)((q >> 6) % (3 * X_OBS));
+    const int64_t slice = (q >> 6) / (3 * X_OBS);
+    const int G = (int)(slice / X_SPG), ks = (int)((slice % X_SPG) >> 1), half = (int)(slice & 1);
+    const int obl = chunk / 3, piece = chunk % 3;
+    const int g = lane >> 4, m = lane & 15;
+    const int row = 16 * (X_OBS * half + obl) + m;
+    // W_l offset in the flat buffer: W0 (H, d), b0, then (W_l, b_l) for l = 1..lh
+    const int layer = G < lh ? G + 1 : 2 * lh - G;
+    const int64_t wl = (int64_t)H * d + H + (int64_t)(layer - 1) * (H * H + H);
+    unsigned out[4];
+#pragma unroll
+    for (int w2 = 0; w2 < 4; ++w2) {
+        unsigned half16[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int j = 2 * w2 + e;
+            const int kn = 32 * ks + 16 * (j >> 2) + 4 * g + (j & 3);
+            const float v = s_scale * (G < lh ? p[wl + (int64_t)row * H + kn] : p[wl + (int64_t)kn * H + row]);
+            const unsigned bv = __float_as_uint(v);
+            const float r = v - __uint_as_float(bv & 0xffff0000u);
+            const unsigned br = __float_as_uint(r);
+            const float r2 = r - __uint_as_float(br & 0xffff0000u);
+            const unsigned pc = piece == 0 ? bv : (piece == 1 ? br : __float_as_uint(r2));
+            half16[e] = pc >> 16;
+        }
+        out[w2] = half16[0] | (half16[1] << 16);
+    }
+    (void)o;
+    *(u32x4*)(stream + ((slice * (3 * X_OBS) + chunk) * 64 + lane) * 4) = u32x4{out[0], out[1], out[2], out[3]};
+}
+
+}  // namespace siren

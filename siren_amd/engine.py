@@ -141,6 +141,47 @@ class SirenEngine:
                                                _ptr(gx), _ptr(tws), _stream(x.device)), 'siren_forward_grad')
         return y, gx
 
+    # ---- split-bf16 W1 (precision mode "bf16x6", w1x_kernel.hpp) ----------------------------------------
+    @property
+    def split_supported(self):
+        """Whether siren_forward_grad_split covers this network (hidden 256, 3 hidden layers, d_in 2 / 3, d_out 1,
+        linear output)."""
+        c = self.cfg
+        return (self.supported and c.hidden == 256 and c.n_hidden == 3 and c.d_out == 1 and c.d_in in (2, 3)
+                and bool(c.outermost_linear) and c.omega_first != 0 and c.omega_hidden != 0)
+
+    def pack_split(self, flat):
+        """The split-bf16 weight image (siren_pack_split) from the flat parameters: once per weight update."""
+        self._require()
+        if not self.split_supported:
+            raise _lib.SirenUnsupported('the split-bf16 W1 covers hidden 256, 3 hidden layers, in_features 2 / 3, '
+                                        'out_features 1, linear output')
+        if flat.device.type != 'cuda':
+            raise RuntimeError('siren_amd: parameters must live on a ROCm device')
+        flat = self._check_params(flat, flat.device)
+        cnt = ctypes.c_int64()
+        _lib.check(self.lib.siren_split_ws_floats(ctypes.byref(self.cfg), ctypes.byref(cnt)), 'siren_split_ws_floats')
+        wsx = torch.empty(cnt.value, dtype=torch.float32, device=flat.device)
+        _lib.check(self.lib.siren_pack_split(ctypes.byref(self.cfg), _ptr(flat), _ptr(wsx), _stream(flat.device)),
+                   'siren_pack_split')
+        return wsx
+
+    def forward_grad_split(self, wsx, x, want_y=True, out_y=None, out_gx=None):
+        """W1 with gy = ones (diff_operators.gradient) on the split-bf16 kernel: (y, gx) as forward_grad(ws, x)."""
+        self._require()
+        if not self.split_supported:
+            raise _lib.SirenUnsupported('the split-bf16 W1 covers hidden 256, 3 hidden layers, in_features 2 / 3, '
+                                        'out_features 1, linear output')
+        x = self._check_x(x)
+        n = x.shape[0]
+        y = None
+        if want_y:
+            y = out_y if out_y is not None else torch.empty(n, 1, dtype=torch.float32, device=x.device)
+        gx = out_gx if out_gx is not None else torch.empty(n, self.cfg.d_in, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_forward_grad_split(ctypes.byref(self.cfg), _ptr(wsx), _ptr(x), n, _ptr(y), _ptr(gx),
+                                                     _stream(x.device)), 'siren_forward_grad_split')
+        return y, gx
+
     def _fg_workspace(self, n, device):
         """siren_forward_grad's caller-owned scratch (hidden 512: the cos spill; hidden 256: none)."""
         cnt = ctypes.c_int64()

@@ -1,0 +1,121 @@
+"""Parity of the split-bf16 W1 kernel (siren_forward_grad_split, w1x_kernel.hpp: bf16 hi/mid/lo pieces, six
+products per K-step, fp32 accumulation) against the fp64 oracle and the reference's golden vectors, with the same
+tolerances as the fp32 kernel and the extra requirement that its error stays at the fp32 kernel's
+level (the split is an fp32-equivalent precision mode, not a reduced one). Needs an MI355X."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import siren_oracle as O
+from conftest import weights_of
+
+pytestmark = pytest.mark.gpu
+
+
+def tol_rel(ref, rel=1e-4):
+    return rel * max(1., float(np.max(np.abs(ref))))
+
+
+def engine(d=2):
+    from siren_amd.engine import SirenEngine
+    return SirenEngine(d, 256, 3, 1, 30., 30., True)
+
+
+def random_layers(d, seed=0):
+    rng = np.random.default_rng(seed)
+    dims = [d] + [256] * 4 + [1]
+    layers = []
+    for i, (fi, fo) in enumerate(zip(dims[:-1], dims[1:])):
+        bound = 1. / fi if i == 0 else np.sqrt(6. / fi) / 30.
+        layers.append((rng.uniform(-bound, bound, (fo, fi)).astype(np.float32),
+                       (rng.uniform(-1, 1, fo) / np.sqrt(fi)).astype(np.float32)))
+    return layers
+
+
+def to_dev(a, dev):
+    return torch.tensor(np.asarray(a, np.float32), device=dev)
+
+
+@pytest.mark.parametrize('name', ['g1', 'g2'])
+def test_split_vs_reference_golden(cuda, name, request):
+    fx = request.getfixturevalue(name)
+    g1 = request.getfixturevalue('g1')
+    tag = name.upper()
+    flat, _ = weights_of(fx)
+    eng = engine()
+    fdev = to_dev(flat, cuda)
+    ws, wsx = eng.pack(fdev), eng.pack_split(fdev)
+    x = to_dev(g1['coords'][0], cuda)
+    y, gx = eng.forward_grad_split(wsx, x)
+    y32, gx32 = eng.forward_grad(ws, x)
+    ry, rg = fx[tag + '_model_out_f64'][0], fx[tag + '_gradient_f64'][0]
+    ey, eg = np.max(np.abs(y.cpu().numpy() - ry)), np.max(np.abs(gx.cpu().numpy() - rg))
+    ey32, eg32 = np.max(np.abs(y32.cpu().numpy() - ry)), np.max(np.abs(gx32.cpu().numpy() - rg))
+    print('%s split: |dy| %.2e |dg| %.2e   fp32 kernel: |dy| %.2e |dg| %.2e' % (name, ey, eg, ey32, eg32))
+    assert ey <= 1e-4 and eg <= tol_rel(rg)
+    # fp32-equivalent: within 2x of the fp32 kernel's own error (and of the reference's fp32 autograd, x4 margin)
+    assert eg <= 2 * eg32 + 1e-6
+    assert ey <= 2 * ey32 + 1e-7
+    own = np.max(np.abs(fx[tag + '_gradient_f32'][0] - rg))
+    assert eg <= 4 * own + 1e-6
+
+
+@pytest.mark.parametrize('d', [2, 3])
+@pytest.mark.parametrize('n', [1, 15, 63, 64, 65, 1000, 4097])
+def test_split_ragged_sizes(cuda, n, d):
+    layers = random_layers(d, seed=n + d)
+    eng = engine(d)
+    wsx = eng.pack_split(to_dev(O.flatten(layers), cuda))
+    x = np.random.default_rng(n).uniform(-1, 1, (n, d)).astype(np.float32)
+    y, gx = eng.forward_grad_split(wsx, to_dev(x, cuda))
+    ry, rg = O.forward_grad(x, layers)
+    assert y.shape == (n, 1) and gx.shape == (n, d)
+    assert np.max(np.abs(y.cpu().numpy() - ry)) <= 1e-4
+    assert np.max(np.abs(gx.cpu().numpy() - rg)) <= tol_rel(rg)
+
+
+def test_split_zero_coords_and_no_y(cuda):
+    eng = engine()
+    wsx = eng.pack_split(to_dev(O.flatten(random_layers(2)), cuda))
+    y, gx = eng.forward_grad_split(wsx, torch.empty(0, 2, device=cuda))
+    assert y.shape == (0, 1) and gx.shape == (0, 2)
+    x = torch.rand(300, 2, device=cuda) * 2 - 1
+    y1, g1 = eng.forward_grad_split(wsx, x)
+    y2, g2 = eng.forward_grad_split(wsx, x, want_y=False)
+    assert y2 is None and torch.equal(g1, g2)
+
+
+def test_split_full_size_vs_fp32_kernel_and_oracle(cuda):
+    """N = 2^20 (the bench workload): a 4096-coordinate subset against the fp64 oracle, the whole batch against the
+    fp32 kernel (both fp32-level, so their difference is at the fp32 rounding level), determinism."""
+    layers = random_layers(2, seed=7)
+    eng = engine()
+    fdev = to_dev(O.flatten(layers), cuda)
+    ws, wsx = eng.pack(fdev), eng.pack_split(fdev)
+    g = torch.Generator(device=cuda).manual_seed(1000)
+    x = torch.rand(1 << 20, 2, device=cuda, generator=g) * 2 - 1
+    y, gx = eng.forward_grad_split(wsx, x)
+    y2, gx2 = eng.forward_grad_split(wsx, x)
+    assert torch.equal(y, y2) and torch.equal(gx, gx2)
+    y32, gx32 = eng.forward_grad(ws, x)
+    sc = max(1., float(gx32.abs().max()))
+    assert float((y - y32).abs().max()) <= 1e-5
+    assert float((gx - gx32).abs().max()) <= 1e-5 * sc
+    idx = torch.arange(0, 1 << 20, 256, device=cuda)
+    ry, rg = O.forward_grad(x[idx].cpu().numpy(), layers)
+    assert np.max(np.abs(y[idx].cpu().numpy() - ry)) <= 1e-4
+    assert np.max(np.abs(gx[idx].cpu().numpy() - rg)) <= tol_rel(rg)
+
+
+def test_split_pack_tracks_weight_updates(cuda):
+    """The split image is a function of the current weights (repacked per optimizer step)."""
+    la, lb = random_layers(2, seed=1), random_layers(2, seed=2)
+    eng = engine()
+    x = torch.rand(2048, 2, device=cuda) * 2 - 1
+    wa = eng.pack_split(to_dev(O.flatten(la), cuda))
+    wb = eng.pack_split(to_dev(O.flatten(lb), cuda))
+    _, ga = eng.forward_grad_split(wa, x)
+    _, gb = eng.forward_grad_split(wb, x)
+    _, rb = O.forward_grad(x.cpu().numpy(), lb)
+    assert not torch.equal(ga, gb)
+    assert np.max(np.abs(gb.cpu().numpy() - rb)) <= tol_rel(rb)

@@ -1,0 +1,96 @@
+"""Static check of a kernel's ISA for reads of in-flight LDS-load destinations.
+
+hipcc does not count inline-asm ds_read loads: their destination VGPRs count as written at the asm statement, so the
+compiler may copy, spill or reuse them before the data lands (cdna_hip_programming.md 'What hipcc does not do').
+This walks each kernel's straight-line ISA, tracks the destinations of every ds_read in issue order and the
+s_waitcnt lgkmcnt(N) that retires them (LDS loads complete in order), and reports any instruction that reads or
+overwrites a register of a load that is still outstanding.
+
+python tools/check_asm_waits.py <file.s> [kernel-substring]   (hipcc --cuda-device-only -S output)
+"""
+import re
+import sys
+
+REG = re.compile(r'\b([va])(\d+)\b|\b([va])\[(\d+):(\d+)\]')
+
+
+def regs(text):
+    out = set()
+    for m in REG.finditer(text):
+        if m.group(1):
+            out.add((m.group(1), int(m.group(2))))
+        else:
+            for r in range(int(m.group(4)), int(m.group(5)) + 1):
+                out.add((m.group(3), r))
+    return out
+
+
+def check(body, name):
+    pending = []  # list of (line_no, set of regs) for outstanding LDS loads, oldest first
+    problems = []
+    for no, line in enumerate(body):
+        t = line.split(';')[0].strip()
+        if not t or t.endswith(':') or t.startswith('.'):
+            if t.endswith(':'):
+                pending = []  # a label: control-flow join; be conservative and reset (loop heads wait themselves)
+            continue
+        op = t.split()[0]
+        if op == 's_waitcnt':
+            m = re.search(r'lgkmcnt\((\d+)\)', t)
+            if m:
+                keep = int(m.group(1))
+                pending = pending[len(pending) - keep:] if keep < len(pending) else pending
+                if keep == 0:
+                    pending = []
+            continue
+        if op.startswith('s_load') or op.startswith('s_buffer_load'):
+            pending.append((no, set()))  # counted in lgkmcnt too
+            continue
+        if op.startswith('s_') and 'barrier' not in op:
+            continue
+        operands = t[len(op):]
+        if op.startswith('ds_') and not op.startswith('ds_read'):
+            used = regs(operands)
+            for ln, rs in pending:
+                if rs & used:
+                    problems.append((no, t, ln))
+            pending.append((no, set()))  # LDS writes / other LDS ops count in lgkmcnt
+            continue
+        if op.startswith('ds_read'):
+            parts = operands.split(',')
+            dst = regs(parts[0])
+            src = regs(','.join(parts[1:]))
+            for ln, rs in pending:
+                if rs & (dst | src):
+                    problems.append((no, t, ln))
+            pending.append((no, dst))
+            continue
+        used = regs(operands)
+        for ln, rs in pending:
+            if rs & used:
+                problems.append((no, t, ln))
+    return problems
+
+
+def main():
+    path = sys.argv[1]
+    want = sys.argv[2] if len(sys.argv) > 2 else ''
+    s = open(path).read()
+    names = re.findall(r'\n(_Z\w+):', s)
+    bad = 0
+    for nm in names:
+        if want and want not in nm:
+            continue
+        i = s.find('\n' + nm + ':')
+        j = s.find('.Lfunc_end', i)
+        body = s[i:j].split('\n')
+        probs = check(body, nm)
+        print('%-70s %d reads of in-flight LDS-load registers' % (nm[:70], len(probs)))
+        for no, t, ln in probs[:8]:
+            print('    line %d: %s   (load at line %d: %s)' % (no, t, ln, body[ln].strip()))
+        bad += len(probs)
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == '__main__':
+    main()
