@@ -19,6 +19,16 @@ __device__ __forceinline__ f32x4 lds_read4(unsigned vaddr) {
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(vaddr), "i"(OFF));
     return r;
 }
+// two ds_read_b128 and their wait in ONE statement: the outputs are valid when the statement ends, so the compiler may
+// copy them freely (the loop-carried operands at a persistent tile seam; an asm read's destination counts as written
+// at its own ASMEND and was copied before the data landed, tools/check_asm_waits.py)
+template <int OFF>
+__device__ __forceinline__ void lds_read4x2_wait(unsigned vaddr, f32x4& a, f32x4& b) {
+    static_assert(OFF >= 0 && OFF + 1024 < 65536, "ds offset field is 16 bits");
+    asm volatile("ds_read_b128 %0, %2 offset:%3\n\tds_read_b128 %1, %2 offset:%4\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(a), "=&v"(b)
+                 : "v"(vaddr), "i"(OFF), "i"(OFF + 1024));
+}
 template <int N>
 __device__ __forceinline__ void lgkm_wait(f32x4& a, f32x4& b) {
     asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N));

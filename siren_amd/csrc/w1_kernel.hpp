@@ -335,14 +335,8 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
         if constexpr (NEXT_IN_SLICE || NEXT_SLICE) {
             lgkm_wait<2>(a0, a1);
         } else if constexpr (NEXT_TILE) {
-            if (cx.more) {
-                n0 = lds_read4<NSLOT>(cx.ring_vaddr);
-                n1 = lds_read4<NSLOT + 1024>(cx.ring_vaddr);
-                lgkm_wait<2>(a0, a1);
-                next = true;
-            } else {
-                lgkm_wait<0>(a0, a1);
-            }
+            // the next tile's first pair is read after this pair's MFMAs, read and wait in one statement (below)
+            lgkm_wait<0>(a0, a1);
         } else {
             lgkm_wait<0>(a0, a1);
         }
@@ -356,7 +350,9 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
             acc[2 * p] = mfma4(a0[r], bop[r], acc[2 * p]);
             acc[2 * p + 1] = mfma4(a1[r], bop[r], acc[2 * p + 1]);
         }
-        if (next) {
+        if constexpr (NEXT_TILE) {
+            if (cx.more) lds_read4x2_wait<NSLOT>(cx.ring_vaddr, a0, a1);
+        } else if (next) {
             a0 = n0;
             a1 = n1;
         }

@@ -78,8 +78,8 @@ template <int LH>
 struct XState {
     u32x4 bx[2][3];    // B operand pieces (hi, mid, lo) of K-step s in bx[s & 1]
     f32x4 acc[2][NB];  // ping-pong accumulators (GEMM G in acc[G & 1])
-    f32x4 C[LH][NB];   // cos(w z_l), l < LH
-    u32x4 pa[3];       // A pieces of the next output block
+    f32x4 C[LH][NB];   // cos(w z_l), 1 <= l < LH (layer 0's is recomputed at the end: 64 fewer live registers)
+    u32x4 pa[3][3];    // A pieces of output blocks b, b + 1, b + 2 of the tile's block sequence (b % 3)
     float xv[4];
     float yp;
 };
@@ -91,14 +91,45 @@ struct XCtx {
     int d, wave, lane, g;
     float w0, w, wsd, inv_s0;
     bool more;
+    unsigned ring_vaddr;   // LDS byte address of this lane's 16 B in slot 0
+    unsigned ring_vaddr2;  // ... in slot 2
 };
 
-// A piece at ring byte offset OFF (compile time) for this lane: a plain LDS load (ds_read_b128), so hipcc counts and
-// places its wait itself -- an inline-asm read is invisible to that bookkeeping and its destination may be copied
-// before the data lands (tools/check_asm_waits.py)
+// A pieces of block-sequence index BI (compile time) for this lane: three inline-asm ds_read_b128 into pa[BI % 3],
+// retired by a counted wait that names exactly those registers (x_wait). The buffers are a static ring with no C++
+// copies, so nothing reads a destination before its wait (tools/check_asm_waits.py checks the ISA); the loop-carried
+// pieces of the next tile are read and waited in ONE statement (x_read_wait).
 template <int OFF>
-__device__ __forceinline__ u32x4 xread(const XCtx& cx) {
-    return ((const u32x4*)cx.ring)[OFF / 16 + cx.lane];
+__device__ __forceinline__ u32x4 xread1(const XCtx& cx) {
+    constexpr int HALFRING = 2 * X_SLICE * 4;  // ds offsets are 16-bit: slots 2, 3 use the second base
+    if constexpr (OFF < HALFRING)
+        return __builtin_bit_cast(u32x4, lds_read4<OFF>(cx.ring_vaddr));
+    else
+        return __builtin_bit_cast(u32x4, lds_read4<OFF - HALFRING>(cx.ring_vaddr2));
+}
+// ring byte offset of piece P of block-sequence index BI (slice BI / 8 of the tile in slot (BI / 8) % 4)
+template <int BI, int P>
+constexpr int xoff() {
+    return ((BI / X_OBS) % X_NBUF) * X_SLICE * 4 + (3 * (BI % X_OBS) + P) * 1024;
+}
+template <int BI, int LH>
+__device__ __forceinline__ void x_issue(XState<LH>& st, const XCtx& cx) {
+    st.pa[BI % 3][0] = xread1<xoff<BI, 0>()>(cx);
+    st.pa[BI % 3][1] = xread1<xoff<BI, 1>()>(cx);
+    st.pa[BI % 3][2] = xread1<xoff<BI, 2>()>(cx);
+}
+template <int N>
+__device__ __forceinline__ void x_wait(u32x4 (&a)[3]) {
+    asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]) : "i"(N));
+}
+// blocks 0 and 1 of a tile (slot 0): six reads and their wait in one statement
+__device__ __forceinline__ void x_read_wait01(u32x4 (&a)[3], u32x4 (&b)[3], unsigned vaddr) {
+    asm volatile(
+        "ds_read_b128 %0, %6\n\tds_read_b128 %1, %6 offset:1024\n\tds_read_b128 %2, %6 offset:2048\n\t"
+        "ds_read_b128 %3, %6 offset:3072\n\tds_read_b128 %4, %6 offset:4096\n\tds_read_b128 %5, %6 offset:5120\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(a[0]), "=&v"(a[1]), "=&v"(a[2]), "=&v"(b[0]), "=&v"(b[1]), "=&v"(b[2])
+        : "v"(vaddr));
 }
 
 // six 1 KiB global->LDS pieces of slice s for this wave (saddr form, as ring_issue4)
@@ -152,7 +183,6 @@ __device__ __forceinline__ void x_epilogue(XState<LH>& st, const XCtx& cx) {
             sn[r] = a_;
             cs[r] = c_;
         }
-        st.C[0][B] = x_pin(cs);
         split_block<HALF>(sn, p);
     } else if constexpr (E < LH) {
         const f32x4 z = st.acc[(E + 1) & 1][B] + *(const f32x4*)(cx.sm + SM_BIAS + E * H + nb);
@@ -201,13 +231,15 @@ __device__ __forceinline__ void x_slice(XState<LH>& st, const XCtx& cx) {
     xstatic_for<0, X_OBS>([&](auto OBL) {
         constexpr int obl = decltype(OBL)::value;
         constexpr int ob = X_OBS * HALF + obl;
+        constexpr int BI = S * X_OBS + obl;  // block-sequence index in the tile (NS * 8 blocks, a multiple of 3)
+        constexpr int NBI = NS * X_OBS;
         if constexpr (obl == 4) {
             if (S + 1 < NS || cx.more) {
                 if (S + 2 < NS || cx.more)
                     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
                 else
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                asm volatile("s_barrier" ::: "memory");  // also orders the next slice's LDS loads after it
+                __builtin_amdgcn_s_barrier();
                 if (S + 3 < NS || cx.more) {
                     const unsigned* sp = cx.stream;
                     asm volatile("" : "+s"(sp));
@@ -215,24 +247,16 @@ __device__ __forceinline__ void x_slice(XState<LH>& st, const XCtx& cx) {
                 }
             }
         }
-        u32x4 a[3] = {st.pa[0], st.pa[1], st.pa[2]};
-        constexpr bool NEXT_IN_SLICE = obl + 1 < X_OBS;
-        constexpr bool NEXT_SLICE = !NEXT_IN_SLICE && S + 1 < NS;
-        if constexpr (NEXT_IN_SLICE) {
-            st.pa[0] = xread<SLOT + (3 * (obl + 1) + 0) * 1024>(cx);
-            st.pa[1] = xread<SLOT + (3 * (obl + 1) + 1) * 1024>(cx);
-            st.pa[2] = xread<SLOT + (3 * (obl + 1) + 2) * 1024>(cx);
-        } else if constexpr (NEXT_SLICE) {
-            st.pa[0] = xread<NSLOT>(cx);
-            st.pa[1] = xread<NSLOT + 1024>(cx);
-            st.pa[2] = xread<NSLOT + 2048>(cx);
-        } else {  // last slice of the tile: the next tile's slice 0 (published by this slice's barrier) if any
-            if (cx.more) {
-                st.pa[0] = xread<NSLOT>(cx);
-                st.pa[1] = xread<NSLOT + 1024>(cx);
-                st.pa[2] = xread<NSLOT + 2048>(cx);
-                }
+        // pieces of block BI + 2 (its slice is published: the next slice's, by this slice's mid barrier)
+        if constexpr (BI + 2 < NBI) {
+            x_issue<BI + 2, LH>(st, cx);
+            x_wait<6>(st.pa[BI % 3]);
+        } else if constexpr (BI + 1 < NBI) {
+            x_wait<3>(st.pa[BI % 3]);
+        } else {
+            x_wait<0>(st.pa[BI % 3]);
         }
+        const u32x4(&a)[3] = st.pa[BI % 3];
         // smallest products first
         acc[ob] = mfma_x(a[2], b[0], acc[ob]);
         acc[ob] = mfma_x(a[1], b[1], acc[ob]);
@@ -240,6 +264,10 @@ __device__ __forceinline__ void x_slice(XState<LH>& st, const XCtx& cx) {
         acc[ob] = mfma_x(a[1], b[0], acc[ob]);
         acc[ob] = mfma_x(a[0], b[1], acc[ob]);
         acc[ob] = mfma_x(a[0], b[0], acc[ob]);
+        // the next tile's blocks 0, 1 (slot 0, published by this slice's barrier), read and waited at once
+        if constexpr (BI + 1 == NBI) {
+            if (cx.more) x_read_wait01(st.pa[0], st.pa[1], cx.ring_vaddr);
+        }
     });
     if constexpr (KS + 1 < X_KSTEPS) x_epilogue<G, 2 * (KS + 1) + HALF, LH, D>(st, cx);
 }
@@ -295,6 +323,8 @@ __global__ __launch_bounds__(THREADS, 1) void w1x_kernel(const float* __restrict
         cx.inv_s0 = two_pi / w0;
     }
     cx.more = false;
+    cx.ring_vaddr = lds_addr(lds) + cx.lane * 16;
+    cx.ring_vaddr2 = cx.ring_vaddr + 2 * X_SLICE * 4;
     {
         const int nf4 = (SM_BIAS + (LH + 1) * H + 3) / 4;
         for (int e = threadIdx.x; e < nf4; e += THREADS) ((f32x4*)sm)[e] = ((const f32x4*)ws_small)[e];
@@ -313,10 +343,8 @@ __global__ __launch_bounds__(THREADS, 1) void w1x_kernel(const float* __restrict
     xring_issue(stream, cx.ring, 1, cx.wave, 16u * cx.lane);
     xring_issue(stream, cx.ring, 2, cx.wave, 16u * cx.lane);
     asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    asm volatile("s_barrier" ::: "memory");
-    st.pa[0] = xread<0>(cx);
-    st.pa[1] = xread<1024>(cx);
-    st.pa[2] = xread<2048>(cx);
+    __builtin_amdgcn_s_barrier();
+    x_read_wait01(st.pa[0], st.pa[1], cx.ring_vaddr);
 
 #pragma unroll 1
     for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
@@ -337,7 +365,18 @@ __global__ __launch_bounds__(THREADS, 1) void w1x_kernel(const float* __restrict
         float q[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int rb = 0; rb < NB; ++rb) {
-            const f32x4 dl = (st.acc[GL][rb] * st.C[0][rb]) * cx.w0;
+            const int nb = 16 * rb + 4 * cx.g;
+            f32x4 z = *(const f32x4*)(sm + SM_BIAS + nb);
+#pragma unroll
+            for (int k = 0; k < D; ++k) z += st.xv[k] * *(const f32x4*)(sm + SM_W0 + k * H + nb);
+            f32x4 c0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float sn_, cs_;
+                sincos_rev(z[r], sn_, cs_);
+                c0[r] = cs_;
+            }
+            const f32x4 dl = (st.acc[GL][rb] * c0) * cx.w0;
 #pragma unroll
             for (int k = 0; k < D; ++k) {
                 const f32x4 wk = *(const f32x4*)(sm + SM_W0 + k * H + 16 * rb + 4 * cx.g);
