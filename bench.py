@@ -127,6 +127,58 @@ def kernel_roofline(eng, ws, x, reps=10):
     return ms, achieved
 
 
+PEAK_BF16_MFMA_TFLOPS = 2516.6     # MI355X dense bf16 MFMA peak (MI355X_MICROARCH.md; 16x the fp32 matrix rate)
+# split-bf16 W1 (w1x_kernel.hpp): per coordinate, the 2 L hidden GEMMs (forward + reverse) run six bf16 products per
+# fp32 K-step: 6 x 2 x (2 LH H^2) bf16 MFMA flops; the d_in / d_out layers are VALU
+SPLIT_MFMA_FLOP = 6 * 2 * 2 * 3 * 256 * 256
+
+
+def split_leg(eng, flat, x, steps, warmup):
+    """The split-bf16 W1 (siren_pack_split + siren_forward_grad_split) on the headline workload: the same step (pack +
+    one fused launch per step) timed the same way, its kernel duration from HIP events, its roofline against the
+    dense bf16 MFMA peak, and its largest difference from the fp32 kernel on this batch. The headline value stays the
+    fp32 kernel's (compute dtype >= the reference's fp32); this is the precision-mode alternative."""
+    if not eng.split_supported:
+        return None
+    y = torch.empty(x.shape[0], 1, device=x.device)
+    gx = torch.empty_like(x)
+
+    def step():
+        wsx = eng.pack_split(flat)
+        eng.forward_grad_split(wsx, x, out_y=y, out_gx=gx)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    wsx = eng.pack_split(flat)
+    st = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+    for a, b in ev:
+        a.record(st)
+        eng.forward_grad_split(wsx, x, out_y=y, out_gx=gx)
+        b.record(st)
+    torch.cuda.synchronize()
+    kms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    ws = eng.pack(flat)
+    y32, g32 = eng.forward_grad(ws, x)
+    achieved_bf16 = SPLIT_MFMA_FLOP * x.shape[0] / (kms * 1e-3) / 1e12
+    return {'value': round(x.shape[0] * steps / el / 1e6, 3), 'unit': 'Mcoords/s',
+            'ms_per_step': round(el / steps * 1e3, 4), 'kernel_ms': round(kms, 4),
+            'dtype': 'bf16x6 (fp32 operands split exactly into bf16 hi/mid/lo, 6 products per K-step, fp32 accumulate)',
+            'fp32_equiv_tflops': round(W1_FLOP * x.shape[0] / (kms * 1e-3) / 1e12, 2),
+            'roofline': {'bound': 'mfma', 'achieved': round(achieved_bf16, 2), 'peak': PEAK_BF16_MFMA_TFLOPS,
+                         'unit': 'TFLOP/s', 'frac': round(achieved_bf16 / PEAK_BF16_MFMA_TFLOPS, 4),
+                         'flop_per_coord': SPLIT_MFMA_FLOP},
+            'max_abs_dy_vs_fp32_kernel': float((y - y32).abs().max()),
+            'max_abs_dgrad_vs_fp32_kernel': float((gx - g32).abs().max()),
+            'parity': 'tests/test_gpu_split.py: G1/G2 reference goldens vs fp64 within the fp32 kernel\'s error'}
+
+
 HEADLINE_KERNEL = 'w1_kernel<3,640>'   # MODE_W1 | MODE_O1S | MODE_D(2), as tools/pmc_summary.py shortens it
 PMC_FILE = os.path.join(ROOT, 'profiles', 'pmc_headline.json')
 
@@ -537,6 +589,7 @@ def main():
     kms, achieved = kernel_roofline(eng, ws, x)
     n_ranks = dist.get_world_size() if world > 1 else 1  # ranks the process group (RCCL) initialised
     del y, gx, ws
+    split = split_leg(eng, flat, x, args.steps, args.warmup) if rank == 0 else None
     dp = None if args.no_dp else dp_train_rates(device, n_ranks, rank)
     extra = {}
     if rank == 0 and not args.no_extra:
@@ -573,6 +626,7 @@ def main():
                          'traffic': traffic, 'kernel_ms': round(kms, 4),
                          'flop_per_coord': W1_FLOP},
             'cpu_baseline': cpu,
+            'split_bf16x6': split,
             'dp_train': dp,
         }
         line.update(extra)
