@@ -40,6 +40,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int X_OBS = 8;                            // output blocks per slice (half a K-step)
 constexpr int X_SLICE = 3 * X_OBS * 256;            // 32-bit words per slice: 8 blocks x (hi, mid, lo) x 1 KiB
 constexpr int X_NBUF = 4;                           // ring slots (96 KiB)
+#ifndef X_EPI_AT
+#define X_EPI_AT 7                                  // slice block after which the slice's epilogue block is issued
+#endif
 constexpr int X_KSTEPS = H / 32;                    // K-steps of one 256-wide GEMM
 constexpr int X_SPG = 2 * X_KSTEPS;                 // slices per GEMM
 constexpr int x_slices(int lh) { return 2 * lh * X_SPG; }  // slices per coordinate tile
@@ -268,8 +271,10 @@ __device__ __forceinline__ void x_slice(XState<LH>& st, const XCtx& cx) {
         if constexpr (BI + 1 == NBI) {
             if (cx.more) x_read_wait01(st.pa[0], st.pa[1], cx.ring_vaddr);
         }
+        // the epilogue block of K-step KS + 1, placed early in the slice so its VALU spreads over the remaining
+        // blocks' MFMAs (after the last block it ran as a cluster with the matrix pipe idle)
+        if constexpr (obl == X_EPI_AT && KS + 1 < X_KSTEPS) x_epilogue<G, 2 * (KS + 1) + HALF, LH, D>(st, cx);
     });
-    if constexpr (KS + 1 < X_KSTEPS) x_epilogue<G, 2 * (KS + 1) + HALF, LH, D>(st, cx);
 }
 
 template <int G, int LH, int D>

@@ -14,6 +14,7 @@ Paths (BASELINE.json configs; F = 2 sum fan_in fan_out FLOP per coordinate, SURV
   hypernet     32 x 4096 coords, 5x256 d2 o1 per-element weights: grouped stored forward + grouped reverse-only W2
                (the hypernetwork training kernels, W2 = 3F)
   w1           5x256 d2 o1, 2^20 coords: the headline W1 launch (2F)
+  w1x          the same on the split-bf16 kernel (w1x_kernel.hpp, precision mode bf16x6)
   w3_wide      5x512 d3 o1, 2^18 coords: W3 H v + theta-grads at hidden 512 (two-stream jet + wgrad, 6F)
 """
 import argparse
@@ -34,6 +35,7 @@ PATHS = {  # name: (d, hidden, layers, o, n, work units of F)
     'w3_theta': (2, 256, 3, 1, 1 << 19, 6),
     'hypernet': (2, 256, 3, 1, 32 * 4096, 3),
     'w1': (2, 256, 3, 1, 1 << 20, 2),
+    'w1x': (2, 256, 3, 1, 1 << 20, 2),      # the split-bf16 W1 (precision mode bf16x6), same workload as w1
     'w3_wide': (3, 512, 3, 1, 1 << 18, 6),
     'video1024': (3, 1024, 3, 3, 1 << 18, 3),   # the layered path (train_video.py's width)
     'video1024_rc': (3, 1024, 3, 3, 1 << 18, 3),
@@ -73,6 +75,9 @@ def build_step(name, dev):
     gy = torch.randn(n, o, device=dev, generator=g)
     if name == 'w1':
         return lambda: eng.forward_grad(ws, x)
+    if name == 'w1x':
+        wsx = eng.pack_split(flat)
+        return lambda: eng.forward_grad_split(wsx, x)
     if name == 'fwd1024':
         return lambda: eng.forward(ws, x)
     if name == 'video1024':  # the training split the module runs: stored forward, reverse-only backward
