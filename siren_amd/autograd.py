@@ -114,10 +114,13 @@ class SirenJetFunction(torch.autograd.Function):
     for the gradient terms)."""
 
     @staticmethod
-    def forward(ctx, engine, x, flat, store=False):
+    def forward(ctx, engine, x, flat, store=False, split=False):
         ws = engine.pack(flat)
         ctx.tws = None
-        if store and engine.stored_supported and engine.cfg.hidden == 256 and STORED_FORWARD:
+        if split and engine.split_supported:
+            # precision 'bf16x6': the split-bf16 W1 kernel (fp32-level error); a backward recomputes from the fp32 ws
+            y, J = engine.forward_grad_split(engine.pack_split(flat), x)
+        elif store and engine.stored_supported and engine.cfg.hidden == 256 and STORED_FORWARD:
             # training: keep a_l / cos so the backward (seeded W3) skips the primal forward GEMMs
             y, J, ctx.tws = engine.forward_grad_store(ws, x)
         else:
@@ -135,7 +138,7 @@ class SirenJetFunction(torch.autograd.Function):
         need_x = ctx.needs_input_grad[1] and _will_execute(ctx, 0)
         need_p = ctx.needs_input_grad[2] and _will_execute(ctx, 1)
         if (gy is None and gJ is None) or not (need_x or need_p):
-            return None, None, None, None
+            return None, None, None, None, None
         gy = gy.contiguous() if gy is not None else None
         gJ = gJ.contiguous() if gJ is not None else None
         gx = gp = None
@@ -156,7 +159,7 @@ class SirenJetFunction(torch.autograd.Function):
                     gx = gx + gy * J
                     if need_p:
                         gp = gp + engine.backward_params(ws, x, gy)[1]
-            return None, (gx if need_x else None), (gp if need_p else None), None
+            return None, (gx if need_x else None), (gp if need_p else None), None, None
         # create_graph=True: differentiable in (x, theta, gy, gJ); J here is this node's own output 1
         if need_x:
             gx = gy * J if gy is not None else None
@@ -172,7 +175,7 @@ class SirenJetFunction(torch.autograd.Function):
             if gJ is not None:
                 _, gpj = _torch_path.jacobian_vjp(engine.cfg, x, flat, gJ, create_graph=True)
                 gp = gpj if gp is None else gp + gpj
-        return None, gx, gp, None
+        return None, gx, gp, None, None
 
 
 class SirenHVP(torch.autograd.Function):

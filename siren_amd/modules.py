@@ -157,8 +157,13 @@ def get_engine(d_in, hidden, n_hidden, d_out, omega_first=30., omega_hidden=30.,
     return eng
 
 
-def _fused_apply(engine, jet, coords, weights_biases):
-    """Run the fused SIREN on coords (..., d_in) with [(W, b), ...]; returns (..., d_out)."""
+PRECISIONS = ('fp32', 'bf16x6')
+
+
+def _fused_apply(engine, jet, coords, weights_biases, precision='fp32'):
+    """Run the fused SIREN on coords (..., d_in) with [(W, b), ...]; returns (..., d_out). precision 'bf16x6' runs
+    the jet forward (y and dPhi/dx in one launch) on the split-bf16 kernel where it covers the network
+    (DESIGN.md §3.13); everything else stays on the fp32 kernels."""
     if coords.device.type != 'cuda':
         raise RuntimeError('siren_amd runs on ROCm devices (MI355X) only; move the model and coords to "cuda". '
                            'The CPU restatement of the reference lives in oracle/ (test infrastructure).')
@@ -180,7 +185,8 @@ def _fused_apply(engine, jet, coords, weights_biases):
         x2d = coords.view(coords.shape)
     if (jet is not None and jet.active and engine.cfg.d_out == 1 and engine.grad_supported
             and torch.is_grad_enabled() and x2d.requires_grad):
-        y, _ = SirenJetFunction.apply(engine, x2d, flat, flat.requires_grad)  # J: the node's second output
+        y, _ = SirenJetFunction.apply(engine, x2d, flat, flat.requires_grad,
+                                      precision == 'bf16x6')  # J: the node's second output
     else:
         # a graph that will want parameter gradients: the forward keeps a_l / cos for a reverse-only backward
         y = SirenFunction.apply(engine, jet, x2d, flat, torch.is_grad_enabled() and flat.requires_grad)
@@ -215,8 +221,11 @@ class FCBlock(MetaModule):
     """Fully connected block; with nonlinearity='sine' it is evaluated by the fused engine."""
 
     def __init__(self, in_features, out_features, num_hidden_layers, hidden_features, outermost_linear=False,
-                 nonlinearity='relu', weight_init=None, jet='auto'):
+                 nonlinearity='relu', weight_init=None, jet='auto', precision='fp32'):
         super().__init__()
+        if precision not in PRECISIONS:
+            raise ValueError('precision must be one of %s; got %r' % (PRECISIONS, precision))
+        self.precision = precision
         self.first_layer_init = None
         table = {'sine': (Sine(), sine_init, first_layer_sine_init),
                  'relu': (nn.ReLU(inplace=True), init_weights_normal, None),
@@ -257,7 +266,7 @@ class FCBlock(MetaModule):
         if self.nonlinearity != 'sine':
             return self.net(coords, params=params)
         wb = [(params['%d.0.weight' % i], params.get('%d.0.bias' % i)) for i in range(len(self.net))]
-        return _fused_apply(self._engine(), self._jet, coords, wb)
+        return _fused_apply(self._engine(), self._jet, coords, wb, self.precision)
 
     def forward_with_activations(self, coords, params=None, retain_grad=False):
         """Per-layer activations (modules.py:96-116): a visualisation API, evaluated layer by layer in torch."""
@@ -286,6 +295,10 @@ class SingleBVPNet(MetaModule):
     requires_grad, 'model_out': (B, N, out_features)}; 'coords' is an alias of 'model_in'.
     Extra keyword `jet` ('auto' | True | False): compute dPhi/dx in the forward launch (W1 kernel) so that
     diff_operators.gradient costs no second sweep; 'auto' switches it on after the first such request.
+    Extra keyword `precision` ('fp32' | 'bf16x6'): 'bf16x6' evaluates that jet forward on the split-bf16 kernel
+    (fp32 operands split exactly into bf16 hi/mid/lo, fp32-level error, 1.48x the fp32 kernel at 5x256 d2/d3 o1)
+    where it covers the network; a backward through it recomputes on the fp32 kernels, so it is an evaluation mode
+    (gradient fields, summaries) -- training is faster with the default (its stored forward feeds the backward).
     """
 
     def __init__(self, out_features=1, type='sine', in_features=2, mode='mlp', hidden_features=256,
@@ -298,7 +311,7 @@ class SingleBVPNet(MetaModule):
             raise _lib.SirenUnsupported('ImageDownsampling jitter (downsample=True) is out of scope')
         self.net = FCBlock(in_features=in_features, out_features=out_features, num_hidden_layers=num_hidden_layers,
                            hidden_features=hidden_features, outermost_linear=True, nonlinearity=type,
-                           jet=kwargs.get('jet', 'auto'))
+                           jet=kwargs.get('jet', 'auto'), precision=kwargs.get('precision', 'fp32'))
         if kwargs.get('verbose', True):
             print(self)
 

@@ -119,3 +119,31 @@ def test_split_pack_tracks_weight_updates(cuda):
     _, rb = O.forward_grad(x.cpu().numpy(), lb)
     assert not torch.equal(ga, gb)
     assert np.max(np.abs(gb.cpu().numpy() - rb)) <= tol_rel(rb)
+
+
+def test_module_precision_bf16x6(cuda, g1):
+    """SingleBVPNet(precision='bf16x6') through the drop-in API: diff_operators.gradient on the jet node served by
+    the split kernel matches the fp64 golden like the fp32 module, and a backward through it (fp32 recompute) agrees
+    with the fp32 module's."""
+    from siren_amd import diff_operators, modules
+    sd = {k[2:]: np.asarray(g1[k]) for k in g1.keys() if k.startswith('w_net.')}
+    ref = g1['G1_gradient_f64'][0]
+    outs = {}
+    for prec in ('fp32', 'bf16x6'):
+        m = modules.SingleBVPNet(in_features=2, verbose=False, jet=True, precision=prec).to(cuda)
+        m.load_state_dict({k: torch.tensor(v) for k, v in sd.items()})
+        x = to_dev(g1['coords'], cuda)
+        out = m({'coords': x})
+        gr = diff_operators.gradient(out['model_out'], out['model_in'])
+        loss = (gr ** 2).sum()
+        loss.backward()
+        outs[prec] = (out['model_out'].detach().cpu().numpy()[0], gr.detach().cpu().numpy()[0],
+                      m.net.net[1][0].weight.grad.detach().cpu().numpy())
+    y_s, g_s, w_s = outs['bf16x6']
+    y_f, g_f, w_f = outs['fp32']
+    assert np.max(np.abs(g_s - ref)) <= tol_rel(ref)
+    assert np.max(np.abs(y_s - g1['G1_model_out_f64'][0])) <= 1e-4
+    assert np.max(np.abs(g_s - g_f)) <= 1e-5 * max(1., np.max(np.abs(g_f)))
+    assert np.max(np.abs(w_s - w_f)) <= 1e-4 * np.max(np.abs(w_f))
+    with pytest.raises(ValueError):
+        modules.SingleBVPNet(in_features=2, verbose=False, precision='bf16')
