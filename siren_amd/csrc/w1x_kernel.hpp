@@ -307,11 +307,14 @@ __global__ __launch_bounds__(THREADS, 1) void w1x_kernel(const float* __restrict
                                                          float w) {
     constexpr int NS = x_slices(LH);
     static_assert(NS % X_NBUF == 0, "the ring must wrap onto slot 0 at a tile boundary");
-    __shared__ __attribute__((aligned(16))) float lds[X_NBUF * X_SLICE + SM_BIAS + (LH + 1) * H];
+    // the small-parameter block FIRST: its epilogue reads are then one base register + immediate offsets (after the
+    // 96 KiB ring they were out of ds offset range, and the compiler kept ~50 per-block addresses live and spilled them)
+    constexpr int SMALL = (SM_BIAS + (LH + 1) * H + 255) / 256 * 256;
+    __shared__ __attribute__((aligned(16))) float lds[SMALL + X_NBUF * X_SLICE];
     XCtx cx;
     XState<LH> st;
-    cx.ring = lds;
-    float* sm = lds + X_NBUF * X_SLICE;
+    cx.ring = lds + SMALL;
+    float* sm = lds;
     cx.sm = sm;
     cx.stream = stream;
     cx.lane = threadIdx.x & 63;
@@ -328,7 +331,7 @@ __global__ __launch_bounds__(THREADS, 1) void w1x_kernel(const float* __restrict
         cx.inv_s0 = two_pi / w0;
     }
     cx.more = false;
-    cx.ring_vaddr = lds_addr(lds) + cx.lane * 16;
+    cx.ring_vaddr = lds_addr(cx.ring) + cx.lane * 16;
     cx.ring_vaddr2 = cx.ring_vaddr + 2 * X_SLICE * 4;
     {
         const int nf4 = (SM_BIAS + (LH + 1) * H + 3) / 4;
