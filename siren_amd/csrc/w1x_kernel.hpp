@@ -52,15 +52,20 @@ __device__ __forceinline__ f32x4 mfma_x(const u32x4& a, const u32x4& b, f32x4 c)
                                                     0, 0, 0);
 }
 
-// exact 3-way bf16 split of two values into the (lo half, hi half) of one word per piece
+// exact 3-way bf16 split of two values into the (lo half, hi half) of one word per piece; the subtractions run as
+// one packed v_pk_add_f32 per pair
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 trunc_bf16x2(f32x2 v) {
+    return f32x2{__uint_as_float(__float_as_uint(v[0]) & 0xffff0000u),
+                 __uint_as_float(__float_as_uint(v[1]) & 0xffff0000u)};
+}
 __device__ __forceinline__ void split_pair(float v0, float v1, unsigned& h, unsigned& m, unsigned& l) {
-    const unsigned b0 = __float_as_uint(v0), b1 = __float_as_uint(v1);
-    h = __builtin_amdgcn_perm(b1, b0, 0x07060302u);
-    const float r0 = v0 - __uint_as_float(b0 & 0xffff0000u), r1 = v1 - __uint_as_float(b1 & 0xffff0000u);
-    const unsigned c0 = __float_as_uint(r0), c1 = __float_as_uint(r1);
-    m = __builtin_amdgcn_perm(c1, c0, 0x07060302u);
-    const float q0 = r0 - __uint_as_float(c0 & 0xffff0000u), q1 = r1 - __uint_as_float(c1 & 0xffff0000u);
-    l = __builtin_amdgcn_perm(__float_as_uint(q1), __float_as_uint(q0), 0x07060302u);
+    const f32x2 v = {v0, v1};
+    h = __builtin_amdgcn_perm(__float_as_uint(v1), __float_as_uint(v0), 0x07060302u);
+    const f32x2 r = v - trunc_bf16x2(v);
+    m = __builtin_amdgcn_perm(__float_as_uint(r[1]), __float_as_uint(r[0]), 0x07060302u);
+    const f32x2 q = r - trunc_bf16x2(r);
+    l = __builtin_amdgcn_perm(__float_as_uint(q[1]), __float_as_uint(q[0]), 0x07060302u);
 }
 
 // block b of a layer's output (lane: rows 16 b + 4 g + r) -> words 2 (b & 1), 2 (b & 1) + 1 of the K-step's pieces
