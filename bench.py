@@ -322,12 +322,14 @@ def config_rates(device, steps=5):
         eng_b.forward_grad_batched(wsb, xb)
     torch.cuda.synchronize()
     res['hypernet_b32x4096_grouped_w1_mcoords_s'] = round(32 * 4096 * steps / (time.perf_counter() - t0) / 1e6, 3)
-    # the hypernetwork training kernels: grouped stored forward + grouped reverse-only W2 (3F per coordinate)
+    # the hypernetwork training kernels: the per-step batched pack (the hypernetwork predicts new weights every step),
+    # grouped stored forward + grouped reverse-only W2 (3F per coordinate)
     gyb = torch.randn(32, 4096, 1, device=device)
 
     def hyper_w2():
-        _, tws = eng_b.forward_store_batched(wsb, xb)
-        eng_b.backward_stored_batched(wsb, xb, gyb, tws)
+        ws_step = eng_b.pack_batched(flat_b)
+        _, tws = eng_b.forward_store_batched(ws_step, xb)
+        eng_b.backward_stored_batched(ws_step, xb, gyb, tws)
     hyper_w2()
     torch.cuda.synchronize()
     t0 = time.perf_counter()

@@ -248,6 +248,9 @@ int32_t siren_mc_emit(const float* vol, int64_t X, int64_t Y, int64_t Z, float l
  * meta_modules.py:41-53) applied to coords (B, n, d_in). Element b reads params + b * param_count (state-dict
  * order, as siren_pack), ws + b * workspace_floats, x + b * n * d_in, and writes y + b * n * d_out, gx + b * n * d_in,
  * gparams + b * param_count. batch <= 65535. */
+/* siren_pack_batched fills what the batched entry points read: for a linear-output hidden-256 network only the
+ * phase-scaled half of each element's workspace (run siren_pack on an element before passing its workspace to the
+ * single-network second / third-order or Laplacian entry points). */
 int32_t siren_pack_batched(const siren_cfg* cfg, const float* params, int64_t batch, float* ws, void* stream);
 /* W0 for every element in ONE grouped launch (grid.y = element) at hidden 256, linear output, 1..5 hidden layers;
  * other configurations run siren_forward element by element. */

@@ -29,28 +29,33 @@ namespace siren {
 // kernel's accumulators are phases in revolutions (sincos_rev) and its reverse GEMMs return s W^T delta.
 __global__ void pack_kernel(const float* __restrict__ p, float* __restrict__ ws, int d, int o, int lh,
                             int64_t spad, int64_t total, int h, int64_t base, float s0, float s,
-                            int64_t p_bstride) {
-    // grouped over batched weights (grid.y = batch element): params rows of p_bstride, workspaces of total floats
+                            int64_t p_bstride, int64_t begin) {
+    // grouped over batched weights (grid.y = batch element): params rows of p_bstride, workspaces of total floats;
+    // elements [begin, total) of each workspace are written (the batched pack skips the unscaled copy)
     p += (int64_t)blockIdx.y * p_bstride;
     ws += (int64_t)blockIdx.y * total;
-    // h = hidden width (256: the H kernels, 512: wide_kernel.hpp); a slice is 16 K-rows x h out-neurons
+    // h = hidden width (256: the H kernels, 512: wide_kernel.hpp); a slice is 16 K-rows x h out-neurons. All
+    // per-element index math is 32-bit shifts and masks (h is a power of two; one workspace < 2^31 floats): the
+    // 64-bit divisions of the first version made the batched pack instruction-bound (98 us for 32 x 3.2 MB)
     const ParamOffsets off(d, o, lh, h);
     const SmallLayout sl(h);
     const int nb = h / 16;
-    const int64_t slice_floats = 16 * (int64_t)h;
-    for (int64_t gidx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; gidx < total;
+    const int lsf = 4 + __builtin_ctz((unsigned)h);  // log2(slice floats)
+    const unsigned sfm = (1u << lsf) - 1u;
+    const unsigned hm = (unsigned)h - 1u, lh2 = (unsigned)__builtin_ctz((unsigned)h);
+    for (int64_t gidx = begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; gidx < total;
          gidx += (int64_t)gridDim.x * blockDim.x) {
         const bool scaled = base > 0 && gidx >= base;
-        const int64_t idx = scaled ? gidx - base : gidx;
+        const unsigned idx = (unsigned)(scaled ? gidx - base : gidx);
         float v = 0.f, sc = 1.f;
-        if (idx < spad) {
+        if (idx < (unsigned)spad) {
             const int e = (int)idx;
             if (e < sl.wo) {
-                const int k = e / h, n = e % h;
+                const int k = e >> lh2, n = e & hm;
                 v = k < d ? p[off.w0 + (int64_t)n * d + k] : 0.f;
                 sc = s0;
             } else if (e < sl.seed) {
-                const int j = (e - sl.wo) / h, n = (e - sl.wo) % h;
+                const int j = (e - sl.wo) >> lh2, n = (e - sl.wo) & hm;
                 v = j < o ? p[off.wout + (int64_t)j * h + n] : 0.f;
             } else if (e < sl.bout) {
                 const int n = e - sl.seed;
@@ -61,21 +66,21 @@ __global__ void pack_kernel(const float* __restrict__ p, float* __restrict__ ws,
                 const int j = e - sl.bout;
                 v = j < o ? p[off.bout + j] : 0.f;
             } else if (e < sl.floats(lh)) {
-                const int l = (e - sl.bias) / h, n = (e - sl.bias) % h;
+                const int l = (e - sl.bias) >> lh2, n = (e - sl.bias) & hm;
                 v = p[off.b(l) + n];
                 sc = l == 0 ? s0 : s;
             }
         } else {
-            const int64_t e = idx - spad;
-            const int64_t slice = e / slice_floats;
-            const int w = (int)(e % slice_floats);
+            const unsigned e = idx - (unsigned)spad;
+            const unsigned slice = e >> lsf;
+            const unsigned w = e & sfm;
             const int r = w & 3, i = (w >> 2) & 15, g = (w >> 6) & 3, blk = w >> 8;
-            if (slice < (int64_t)lh * nb) {
+            if (slice < (unsigned)(lh * nb)) {
                 const int l = (int)(slice / nb) + 1, kb = (int)(slice % nb);
                 v = p[off.w(l) + (int64_t)(16 * blk + i) * h + 16 * kb + 4 * g + r];
             } else {
-                const int64_t s2 = slice - (int64_t)lh * nb;
-                const int l = lh - (int)(s2 / nb), kb = (int)(s2 % nb);
+                const int s2 = (int)slice - lh * nb;
+                const int l = lh - s2 / nb, kb = s2 % nb;
                 v = p[off.w(l) + (int64_t)(16 * kb + 4 * g + r) * h + 16 * blk + i];
             }
             sc = s;

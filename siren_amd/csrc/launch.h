@@ -25,7 +25,7 @@ struct FusedArgs {
 
 // tu_legacy.hip
 void launch_pack(const float* p, float* ws, int d, int o, int lh, int h, int64_t spad, int64_t total, int64_t base,
-                 float s0, float s, hipStream_t st, int batch = 1, int64_t p_bstride = 0);
+                 float s0, float s, hipStream_t st, int batch = 1, int64_t p_bstride = 0, int64_t begin = 0);
 void launch_legacy_fwd(dim3 grid, hipStream_t st, const FusedArgs& a);
 void launch_legacy_grad(bool store, dim3 grid, hipStream_t st, const FusedArgs& a);
 // tu_w1.hip: mode 0 = W1, 1 = STORE (W2 stage 1), MODE_REV (stored-forward W2 reverse); tu_w0.hip: forward only,

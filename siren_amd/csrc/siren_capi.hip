@@ -1019,9 +1019,12 @@ int32_t siren_pack_batched(const siren_cfg* cfg, const float* params, int64_t ba
             if (int rc = siren_pack(cfg, params + b * param_count(cfg), ws + b * ws_floats(cfg), stream)) return rc;
         return SIREN_OK;
     }
+    // every batched entry point reads only the phase-scaled copy when the W1-family kernels cover the network
+    // (linear output, hidden 256, no legacy flag): the unscaled half is not written (half the per-step pack)
+    const bool scaled_only = w1_ok(cfg) && cfg->outermost_linear && (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0;
     siren::launch_pack(params, ws, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden, small_pad(cfg), ws_floats(cfg),
                        wide(cfg) ? 0 : ws_base(cfg), cfg->omega_first * kInv2Pi, cfg->omega_hidden * kInv2Pi,
-                       (hipStream_t)stream, (int)batch, param_count(cfg));
+                       (hipStream_t)stream, (int)batch, param_count(cfg), scaled_only ? ws_base(cfg) : 0);
     return hip_status("siren_pack_batched");
 }
 
