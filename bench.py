@@ -167,6 +167,18 @@ def split_leg(eng, flat, x, steps, warmup):
     ws = eng.pack(flat)
     y32, g32 = eng.forward_grad(ws, x)
     achieved_bf16 = SPLIT_MFMA_FLOP * x.shape[0] / (kms * 1e-3) / 1e12
+    # the forward-only W0 on the same image (dense evaluation), beside the fp32 W0 kernel
+    yf = torch.empty(x.shape[0], 1, device=x.device)
+    fwd = {}
+    for name, fn in (('fp32', lambda: eng.forward(ws, x, out=yf)), ('split', lambda: eng.forward_split(wsx, x, out=yf))):
+        fn()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+        for a, b in ev:
+            a.record(st)
+            fn()
+            b.record(st)
+        torch.cuda.synchronize()
+        fwd[name] = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     return {'value': round(x.shape[0] * steps / el / 1e6, 3), 'unit': 'Mcoords/s',
             'ms_per_step': round(el / steps * 1e3, 4), 'kernel_ms': round(kms, 4),
             'dtype': 'bf16x6 (fp32 operands split exactly into bf16 hi/mid/lo, 6 products per K-step, fp32 accumulate)',
@@ -174,6 +186,11 @@ def split_leg(eng, flat, x, steps, warmup):
             'roofline': {'bound': 'mfma', 'achieved': round(achieved_bf16, 2), 'peak': PEAK_BF16_MFMA_TFLOPS,
                          'unit': 'TFLOP/s', 'frac': round(achieved_bf16 / PEAK_BF16_MFMA_TFLOPS, 4),
                          'flop_per_coord': SPLIT_MFMA_FLOP},
+            'forward_w0': {'split_mcoords_s': round(x.shape[0] / fwd['split'] / 1e3, 2),
+                           'fp32_mcoords_s': round(x.shape[0] / fwd['fp32'] / 1e3, 2),
+                           'split_kernel_ms': round(fwd['split'], 4), 'fp32_kernel_ms': round(fwd['fp32'], 4),
+                           'bf16_frac': round(SPLIT_MFMA_FLOP / 2 * x.shape[0] / (fwd['split'] * 1e-3) / 1e12
+                                              / PEAK_BF16_MFMA_TFLOPS, 4)},
             'max_abs_dy_vs_fp32_kernel': float((y - y32).abs().max()),
             'max_abs_dgrad_vs_fp32_kernel': float((gx - g32).abs().max()),
             'parity': 'tests/test_gpu_split.py: G1/G2 reference goldens vs fp64 within the fp32 kernel\'s error'}

@@ -195,6 +195,9 @@ int32_t siren_split_ws_floats(const siren_cfg* cfg, int64_t* count);
 int32_t siren_pack_split(const siren_cfg* cfg, const float* params, float* wsx, void* stream);
 int32_t siren_forward_grad_split(const siren_cfg* cfg, const float* wsx, const float* x, int64_t n, float* y,
                                  float* gx, void* stream);
+/* The forward-only W0 (model_out, SingleBVPNet.forward modules.py:143-160) on the same split image: the forward GEMMs
+ * only, two waves per SIMD sharing one weight ring (dense evaluation: sdf_meshing.create_mesh, summaries). */
+int32_t siren_forward_split(const siren_cfg* cfg, const float* wsx, const float* x, int64_t n, float* y, void* stream);
 
 /* Diagnostics: the W1 kernel (hidden 256, 3 hidden layers) with s_memtime stamps. stamps receives
  * 256 workgroups x 4 tiles x 4 waves x 8 events (uint64; event 0 tile start, 1..6 after GEMM 0..5, 7 tile end);

@@ -78,6 +78,7 @@ _SIGS = {
     'siren_split_ws_floats': [_CFG, ctypes.POINTER(_I64)],
     'siren_pack_split': [_CFG, _P, _P, _P],
     'siren_forward_grad_split': [_CFG, _P, _P, _I64, _P, _P, _P],
+    'siren_forward_split': [_CFG, _P, _P, _I64, _P, _P],
 }
 EXPORTED = ('siren_abi_version', 'siren_last_error') + tuple(_SIGS)
 

@@ -39,6 +39,10 @@ int64_t split_stream_words(int lh);
 void launch_pack_split(const float* p, unsigned* stream, int d, int o, int lh, float s, hipStream_t st);
 void launch_w1x(dim3 grid, hipStream_t st, const float* ws_small, const unsigned* stream, const float* x, int64_t n,
                 float* y, float* gx, int d, float w0, float w);
+// the forward-only split W0 (8 waves, 128 coordinates per workgroup tile)
+int split_fwd_tile();
+void launch_w0x(dim3 grid, hipStream_t st, const float* ws_small, const unsigned* stream, const float* x, int64_t n,
+                float* y, int d, float w0, float w);
 // tu_w4.hip: JET mode (16 coordinates per workgroup); lap (n) = sum_j Laplacian(y_j), gx (n, d) = sum_j grad y_j
 void launch_w4(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, float* y, float* gx, float* lap,
                int d, int o, int lh, float w0, float w);

@@ -332,6 +332,20 @@ int32_t siren_forward_grad_split(const siren_cfg* cfg, const float* wsx, const f
     return hip_status("siren_forward_grad_split");
 }
 
+int32_t siren_forward_split(const siren_cfg* cfg, const float* wsx, const float* x, int64_t n, float* y, void* stream) {
+    if (int rc = split_ok(cfg)) return rc;
+    if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    if (n == 0) return SIREN_OK;
+    if (wsx == nullptr || x == nullptr || y == nullptr) return fail(SIREN_EINVAL, "wsx/x/y is NULL");
+    const int64_t tile = siren::split_fwd_tile();
+    const int64_t blocks = (n + tile - 1) / tile;
+    if (blocks > 0x7fffffffll) return fail(SIREN_EINVAL, "n too large");
+    const int64_t spad = small_pad(cfg);
+    siren::launch_w0x(tile_grid(cfg, blocks, 1), (hipStream_t)stream, wsx + spad, (const unsigned*)(wsx + 2 * spad), x,
+                      n, y, cfg->d_in, cfg->omega_first, cfg->omega_hidden);
+    return hip_status("siren_forward_split");
+}
+
 // diagnostics: while set, W3 launches record s_memtime phase stamps (w3_kernel.hpp) into stamps[256][16]
 static unsigned long long* g_w3_prof = nullptr;
 int32_t siren_w3_phase_profile(uint64_t* stamps) {

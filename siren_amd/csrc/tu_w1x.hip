@@ -15,9 +15,23 @@ void launch_pack_split(const float* p, unsigned* stream, int d, int o, int lh, f
 void launch_w1x(dim3 grid, hipStream_t st, const float* ws_small, const unsigned* stream, const float* x, int64_t n,
                 float* y, float* gx, int d, float w0, float w) {
     if (d == 2)
-        hipLaunchKernelGGL((w1x_kernel<3, 2>), grid, dim3(THREADS), 0, st, ws_small, stream, x, n, y, gx, w0, w);
+        hipLaunchKernelGGL((w1x_kernel<3, 2, false>), grid, dim3(64 * x_waves<false>()), 0, st, ws_small, stream, x, n,
+                           y, gx, w0, w);
     else
-        hipLaunchKernelGGL((w1x_kernel<3, 3>), grid, dim3(THREADS), 0, st, ws_small, stream, x, n, y, gx, w0, w);
+        hipLaunchKernelGGL((w1x_kernel<3, 3, false>), grid, dim3(64 * x_waves<false>()), 0, st, ws_small, stream, x, n,
+                           y, gx, w0, w);
+}
+
+int split_fwd_tile() { return 16 * x_waves<true>(); }
+
+void launch_w0x(dim3 grid, hipStream_t st, const float* ws_small, const unsigned* stream, const float* x, int64_t n,
+                float* y, int d, float w0, float w) {
+    if (d == 2)
+        hipLaunchKernelGGL((w1x_kernel<3, 2, true>), grid, dim3(64 * x_waves<true>()), 0, st, ws_small, stream, x, n,
+                           y, (float*)nullptr, w0, w);
+    else
+        hipLaunchKernelGGL((w1x_kernel<3, 3, true>), grid, dim3(64 * x_waves<true>()), 0, st, ws_small, stream, x, n,
+                           y, (float*)nullptr, w0, w);
 }
 
 }  // namespace siren

@@ -140,14 +140,22 @@ __device__ __forceinline__ void x_read_wait01(u32x4 (&a)[3], u32x4 (&b)[3], unsi
         : "v"(vaddr));
 }
 
-// six 1 KiB global->LDS pieces of slice s for this wave (saddr form, as ring_issue4)
+// CPW 1 KiB global->LDS pieces of slice s for this wave (saddr form, as ring_issue4): 24 per slice over the waves
+// (6 each at 4 waves per workgroup, 3 at 8)
+template <int CPW>
 __device__ __forceinline__ void xring_issue(const unsigned* __restrict__ stream, float* ring, int s, int wave,
                                             unsigned lane_off) {
-    const char* src = (const char*)(stream + (int64_t)s * X_SLICE + wave * 6 * 256);
-    const unsigned dst = lds_addr(ring + (s % X_NBUF) * X_SLICE + wave * 6 * 256);
+    const char* src = (const char*)(stream + (int64_t)s * X_SLICE + wave * CPW * 256);
+    const unsigned dst = lds_addr(ring + (s % X_NBUF) * X_SLICE + wave * CPW * 256);
 #pragma unroll
-    for (int q = 0; q < 6; ++q) glds_x4(src + q * 1024, lane_off, dst + q * 1024);
+    for (int q = 0; q < CPW; ++q) glds_x4(src + q * 1024, lane_off, dst + q * 1024);
 }
+// waves per workgroup: 4 (one per SIMD) for W1; 8 (two per SIMD, sharing the ring) for the forward-only W0, whose
+// registers fit twice per SIMD without the parked cos
+template <bool FWD>
+constexpr int x_waves() { return FWD ? 8 : 4; }
+template <bool FWD, int LH>
+constexpr int x_ns() { return FWD ? LH * X_SPG : x_slices(LH); }
 
 template <int I, int N, typename F>
 __device__ __forceinline__ void xstatic_for(F&& f) {
@@ -174,7 +182,7 @@ __device__ __forceinline__ f32x4 x_pin(f32x4 v) {
 
 // Epilogue of block B producing the B operand of GEMM E (see the table at the top; the previous GEMM's output is
 // acc[(E + 1) & 1]).
-template <int E, int B, int LH, int D>
+template <int E, int B, int LH, int D, bool FWD>
 __device__ __forceinline__ void x_epilogue(XState<LH>& st, const XCtx& cx) {
     constexpr int KS = B >> 1, HALF = B & 1;
     const int nb = 16 * B + 4 * cx.g;
@@ -202,7 +210,7 @@ __device__ __forceinline__ void x_epilogue(XState<LH>& st, const XCtx& cx) {
             sn[r] = a_;
             cs[r] = c_;
         }
-        st.C[E][B] = x_to_agpr(cs);
+        if constexpr (!FWD) st.C[E][B] = x_to_agpr(cs);
         split_block<HALF>(sn, p);
     } else if constexpr (E == LH) {
         const f32x4 z = st.acc[(E + 1) & 1][B] + *(const f32x4*)(cx.sm + SM_BIAS + LH * H + nb);
@@ -228,9 +236,10 @@ __device__ __forceinline__ void x_epilogue(XState<LH>& st, const XCtx& cx) {
 // Slice (G, KS, HALF): the output blocks ob = 8 HALF .. 8 HALF + 7 of K-step KS, six MFMAs each; the mid-slice ring
 // barrier after block 3; the next block's (or the next slice's first block's) A pieces read one block ahead; then
 // the epilogue block of K-step KS + 1 (block 2 (KS + 1) + HALF) of the previous GEMM's output.
-template <int G, int KS, int HALF, int LH, int D>
+template <int G, int KS, int HALF, int LH, int D, bool FWD>
 __device__ __forceinline__ void x_slice(XState<LH>& st, const XCtx& cx) {
-    constexpr int NS = x_slices(LH);
+    constexpr int NS = x_ns<FWD, LH>();
+    constexpr int CPW = 24 / x_waves<FWD>();
     constexpr int S = G * X_SPG + 2 * KS + HALF;
     constexpr int SLOT = (S % X_NBUF) * X_SLICE * 4;
     constexpr int NSLOT = ((S + 1) % X_NBUF) * X_SLICE * 4;
@@ -244,14 +253,14 @@ __device__ __forceinline__ void x_slice(XState<LH>& st, const XCtx& cx) {
         if constexpr (obl == 4) {
             if (S + 1 < NS || cx.more) {
                 if (S + 2 < NS || cx.more)
-                    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(CPW) : "memory");
                 else
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();
                 if (S + 3 < NS || cx.more) {
                     const unsigned* sp = cx.stream;
                     asm volatile("" : "+s"(sp));
-                    xring_issue(sp, cx.ring, (S + 3) % NS, cx.wave, 16u * cx.lane);
+                    xring_issue<CPW>(sp, cx.ring, (S + 3) % NS, cx.wave, 16u * cx.lane);
                 }
             }
         }
@@ -278,39 +287,40 @@ __device__ __forceinline__ void x_slice(XState<LH>& st, const XCtx& cx) {
         }
         // the epilogue block of K-step KS + 1, placed early in the slice so its VALU spreads over the remaining
         // blocks' MFMAs (after the last block it ran as a cluster with the matrix pipe idle)
-        if constexpr (obl == X_EPI_AT && KS + 1 < X_KSTEPS) x_epilogue<G, 2 * (KS + 1) + HALF, LH, D>(st, cx);
+        if constexpr (obl == X_EPI_AT && KS + 1 < X_KSTEPS) x_epilogue<G, 2 * (KS + 1) + HALF, LH, D, FWD>(st, cx);
     });
 }
 
-template <int G, int LH, int D>
+template <int G, int LH, int D, bool FWD>
 __device__ __forceinline__ void x_gemm(XState<LH>& st, const XCtx& cx) {
 #pragma unroll
     for (int ob = 0; ob < NB; ++ob) st.acc[G & 1][ob] = f32x4{0.f, 0.f, 0.f, 0.f};
-    x_epilogue<G, 0, LH, D>(st, cx);
-    x_epilogue<G, 1, LH, D>(st, cx);
+    x_epilogue<G, 0, LH, D, FWD>(st, cx);
+    x_epilogue<G, 1, LH, D, FWD>(st, cx);
     xstatic_for<0, X_KSTEPS>([&](auto KS) {
-        x_slice<G, decltype(KS)::value, 0, LH, D>(st, cx);
-        x_slice<G, decltype(KS)::value, 1, LH, D>(st, cx);
+        x_slice<G, decltype(KS)::value, 0, LH, D, FWD>(st, cx);
+        x_slice<G, decltype(KS)::value, 1, LH, D, FWD>(st, cx);
     });
 }
 
-template <int G, int LH, int D>
+template <int G, int LH, int D, bool FWD>
 __device__ __forceinline__ void x_run(XState<LH>& st, const XCtx& cx) {
-    if constexpr (G < 2 * LH) {
-        x_gemm<G, LH, D>(st, cx);
-        x_run<G + 1, LH, D>(st, cx);
+    if constexpr (G < (FWD ? LH : 2 * LH)) {
+        x_gemm<G, LH, D, FWD>(st, cx);
+        x_run<G + 1, LH, D, FWD>(st, cx);
     }
 }
 
 // ws: the split image of siren_pack_split (small block at ws_small, bf16 stream at stream); x (n, D); y (n) / gx
 // (n, D) (y nullable). w0 / w as the fp32 kernel (phase-scaled pack).
-template <int LH, int D>
-__global__ __launch_bounds__(THREADS, 1) void w1x_kernel(const float* __restrict__ ws_small,
+template <int LH, int D, bool FWD>
+__global__ __launch_bounds__(64 * x_waves<FWD>(), 1) void w1x_kernel(const float* __restrict__ ws_small,
                                                          const unsigned* __restrict__ stream,
                                                          const float* __restrict__ x, int64_t n,
                                                          float* __restrict__ y, float* __restrict__ gx, float w0,
                                                          float w) {
-    constexpr int NS = x_slices(LH);
+    constexpr int NS = x_ns<FWD, LH>();
+    constexpr int NW = x_waves<FWD>(), NT = 64 * NW, TILEX = 16 * NW, CPW = 24 / NW;
     static_assert(NS % X_NBUF == 0, "the ring must wrap onto slot 0 at a tile boundary");
     // the small-parameter block FIRST: its epilogue reads are then one base register + immediate offsets (after the
     // 96 KiB ring they were out of ds offset range, and the compiler kept ~50 per-block addresses live and spilled them)
@@ -340,35 +350,54 @@ __global__ __launch_bounds__(THREADS, 1) void w1x_kernel(const float* __restrict
     cx.ring_vaddr2 = cx.ring_vaddr + 2 * X_SLICE * 4;
     {
         const int nf4 = (SM_BIAS + (LH + 1) * H + 3) / 4;
-        for (int e = threadIdx.x; e < nf4; e += THREADS) ((f32x4*)sm)[e] = ((const f32x4*)ws_small)[e];
+        for (int e = threadIdx.x; e < nf4; e += NT) ((f32x4*)sm)[e] = ((const f32x4*)ws_small)[e];
     }
-    const int64_t tiles = (n + TILE - 1) / TILE;
+    const int64_t tiles = (n + TILEX - 1) / TILEX;
     float xn[4];
     auto load_inputs = [&](int64_t tile) {
-        const int64_t cd = tile * TILE + cx.wave * 16 + c;
+        const int64_t cd = tile * TILEX + cx.wave * 16 + c;
         const bool ok = tile < tiles && cd < n;
 #pragma unroll
         for (int k = 0; k < 4; ++k) xn[k] = (ok && k < D) ? x[cd * D + k] : 0.f;
     };
     load_inputs(blockIdx.x);
     __syncthreads();
-    xring_issue(stream, cx.ring, 0, cx.wave, 16u * cx.lane);
-    xring_issue(stream, cx.ring, 1, cx.wave, 16u * cx.lane);
-    xring_issue(stream, cx.ring, 2, cx.wave, 16u * cx.lane);
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    xring_issue<CPW>(stream, cx.ring, 0, cx.wave, 16u * cx.lane);
+    xring_issue<CPW>(stream, cx.ring, 1, cx.wave, 16u * cx.lane);
+    xring_issue<CPW>(stream, cx.ring, 2, cx.wave, 16u * cx.lane);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * CPW) : "memory");
     __builtin_amdgcn_s_barrier();
     x_read_wait01(st.pa[0], st.pa[1], cx.ring_vaddr);
 
 #pragma unroll 1
     for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
         cx.more = tile + gridDim.x < tiles;
-        const int64_t coord = tile * TILE + cx.wave * 16 + c;
+        const int64_t coord = tile * TILEX + cx.wave * 16 + c;
         const bool valid = coord < n;
 #pragma unroll
         for (int k = 0; k < 4; ++k) st.xv[k] = xn[k];
         st.yp = 0.f;
         load_inputs(tile + gridDim.x);
-        x_run<0, LH, D>(st, cx);
+        x_run<0, LH, D, FWD>(st, cx);
+        if constexpr (FWD) {
+            // last hidden layer: a_L = sin(w z_L) and y = a_L Wout^T + bout (serial over the 16 blocks)
+            constexpr int GL = (LH - 1) & 1;
+#pragma unroll
+            for (int rb = 0; rb < NB; ++rb) {
+                const int nb = 16 * rb + 4 * cx.g;
+                const f32x4 z = st.acc[GL][rb] + *(const f32x4*)(sm + SM_BIAS + LH * H + nb);
+                const f32x4 wo = *(const f32x4*)(sm + SM_WO + nb);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float sn_, cs_;
+                    sincos_rev(z[r], sn_, cs_);
+                    st.yp += wo[r] * sn_;
+                }
+            }
+            const float yv = sum_groups(st.yp) + sm[SM_BOUT];
+            if (valid && cx.g == 0) y[coord] = yv;
+            continue;
+        }
         {
             const float yv = sum_groups(st.yp) + sm[SM_BOUT];
             if (y != nullptr && valid && cx.g == 0) y[coord] = yv;

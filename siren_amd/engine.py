@@ -182,6 +182,19 @@ class SirenEngine:
                                                      _stream(x.device)), 'siren_forward_grad_split')
         return y, gx
 
+    def forward_split(self, wsx, x, out=None):
+        """W0 (y = Phi(x)) on the split-bf16 forward kernel (siren_forward_split): dense evaluation."""
+        self._require()
+        if not self.split_supported:
+            raise _lib.SirenUnsupported('the split-bf16 kernels cover hidden 256, 3 hidden layers, in_features 2 / 3, '
+                                        'out_features 1, linear output')
+        x = self._check_x(x)
+        n = x.shape[0]
+        y = out if out is not None else torch.empty(n, 1, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_forward_split(ctypes.byref(self.cfg), _ptr(wsx), _ptr(x), n, _ptr(y),
+                                                _stream(x.device)), 'siren_forward_split')
+        return y
+
     def _fg_workspace(self, n, device):
         """siren_forward_grad's caller-owned scratch (hidden 512: the cos spill; hidden 256: none)."""
         cnt = ctypes.c_int64()

@@ -187,6 +187,10 @@ def _fused_apply(engine, jet, coords, weights_biases, precision='fp32'):
             and torch.is_grad_enabled() and x2d.requires_grad):
         y, _ = SirenJetFunction.apply(engine, x2d, flat, flat.requires_grad,
                                       precision == 'bf16x6')  # J: the node's second output
+    elif (precision == 'bf16x6' and engine.split_supported
+          and not (torch.is_grad_enabled() and (x2d.requires_grad or flat.requires_grad))):
+        # no graph is recorded (dense evaluation: create_mesh, summaries under no_grad): the split-bf16 forward
+        y = engine.forward_split(engine.pack_split(flat.detach()), x2d.detach().contiguous())
     else:
         # a graph that will want parameter gradients: the forward keeps a_l / cos for a reverse-only backward
         y = SirenFunction.apply(engine, jet, x2d, flat, torch.is_grad_enabled() and flat.requires_grad)
@@ -296,9 +300,10 @@ class SingleBVPNet(MetaModule):
     Extra keyword `jet` ('auto' | True | False): compute dPhi/dx in the forward launch (W1 kernel) so that
     diff_operators.gradient costs no second sweep; 'auto' switches it on after the first such request.
     Extra keyword `precision` ('fp32' | 'bf16x6'): 'bf16x6' evaluates that jet forward on the split-bf16 kernel
-    (fp32 operands split exactly into bf16 hi/mid/lo, fp32-level error, 1.48x the fp32 kernel at 5x256 d2/d3 o1)
-    where it covers the network; a backward through it recomputes on the fp32 kernels, so it is an evaluation mode
-    (gradient fields, summaries) -- training is faster with the default (its stored forward feeds the backward).
+    (fp32 operands split exactly into bf16 hi/mid/lo, fp32-level error, 1.6x the fp32 kernel at 5x256 d2/d3 o1)
+    where it covers the network, and a forward that records no graph (no_grad: create_mesh, summaries) on the split
+    W0 kernel (1.85x); a backward through the jet node recomputes on the fp32 kernels, so it is an evaluation mode --
+    training is faster with the default (its stored forward feeds the backward).
     """
 
     def __init__(self, out_features=1, type='sine', in_features=2, mode='mlp', hidden_features=256,

@@ -147,3 +147,60 @@ def test_module_precision_bf16x6(cuda, g1):
     assert np.max(np.abs(w_s - w_f)) <= 1e-4 * np.max(np.abs(w_f))
     with pytest.raises(ValueError):
         modules.SingleBVPNet(in_features=2, verbose=False, precision='bf16')
+
+
+@pytest.mark.parametrize('d', [2, 3])
+@pytest.mark.parametrize('n', [1, 127, 128, 129, 4097, 70000])
+def test_split_forward_ragged(cuda, n, d):
+    """The forward-only split kernel (siren_forward_split, 8 waves x 16 coordinates per tile) against the fp64
+    oracle's model_out."""
+    layers = random_layers(d, seed=3 * n + d)
+    eng = engine(d)
+    wsx = eng.pack_split(to_dev(O.flatten(layers), cuda))
+    x = np.random.default_rng(n + 11).uniform(-1, 1, (n, d)).astype(np.float32)
+    y = eng.forward_split(wsx, to_dev(x, cuda))
+    ry, _ = O.forward_grad(x, layers)
+    assert y.shape == (n, 1)
+    assert np.max(np.abs(y.cpu().numpy() - ry)) <= 1e-4
+
+
+@pytest.mark.parametrize('name', ['g1', 'g2'])
+def test_split_forward_golden_and_full_size(cuda, name, request):
+    fx = request.getfixturevalue(name)
+    g1 = request.getfixturevalue('g1')
+    flat, _ = weights_of(fx)
+    eng = engine()
+    fdev = to_dev(flat, cuda)
+    ws, wsx = eng.pack(fdev), eng.pack_split(fdev)
+    y = eng.forward_split(wsx, to_dev(g1['coords'][0], cuda)).cpu().numpy()
+    ry = fx[name.upper() + '_model_out_f64'][0]
+    ey, ey32 = np.max(np.abs(y - ry)), np.max(np.abs(eng.forward(ws, to_dev(g1['coords'][0], cuda)).cpu().numpy() - ry))
+    assert ey <= 1e-4 and ey <= 2 * ey32 + 1e-7
+    x = torch.rand(1 << 20, 2, device=cuda) * 2 - 1
+    ys, ys2, y32 = eng.forward_split(wsx, x), eng.forward_split(wsx, x), eng.forward(ws, x)
+    assert torch.equal(ys, ys2)
+    assert float((ys - y32).abs().max()) <= 1e-5
+
+
+def test_module_precision_bf16x6_no_grad_forward_and_mesh(cuda, g1):
+    """precision='bf16x6' under no_grad: model_out from the split forward kernel (vs the fp64 golden and the fp32
+    module), and sdf_meshing.create_mesh's dense evaluation through it matches the fp32 module's volume."""
+    from siren_amd import modules, sdf_meshing
+    sd = {k[2:]: np.asarray(g1[k]) for k in g1.keys() if k.startswith('w_net.')}
+    x = to_dev(g1['coords'], cuda)
+    outs = {}
+    for prec in ('fp32', 'bf16x6'):
+        m = modules.SingleBVPNet(in_features=2, verbose=False, precision=prec).to(cuda)
+        m.load_state_dict({k: torch.tensor(v) for k, v in sd.items()})
+        with torch.no_grad():
+            outs[prec] = m({'coords': x})['model_out'].cpu().numpy()[0]
+    ref = g1['G1_model_out_f64'][0]
+    assert np.max(np.abs(outs['bf16x6'] - ref)) <= 1e-4
+    assert np.max(np.abs(outs['bf16x6'] - outs['fp32'])) <= 1e-5
+    vols = {}
+    for prec in ('fp32', 'bf16x6'):
+        torch.manual_seed(0)
+        m = modules.SingleBVPNet(in_features=3, verbose=False, precision=prec).to(cuda)
+        vols[prec] = sdf_meshing.evaluate_sdf_grid(lambda p, m=m: m({'coords': p})['model_out'], 64,
+                                                    max_batch=1 << 16, device=cuda, out_device=cuda)
+    assert float((vols['fp32'] - vols['bf16x6']).abs().max()) <= 1e-5

@@ -45,6 +45,11 @@ def main():
         out[name] = {'ms': round(ms, 4), 'mcoords_s': round(a.n / ms / 1e3, 2),
                      'tflops_fp32_equiv': round(2 * F * a.n / ms / 1e9, 2),
                      'frac_fp32_peak': round(2 * F * a.n / ms / 1e9 / 157.3, 4)}
+    for name, fn in (('fwd_fp32', lambda: eng.forward(ws, x)), ('fwd_split_bf16x6', lambda: eng.forward_split(wsx, x))):
+        ms = timed(fn, a.reps)
+        out[name] = {'ms': round(ms, 4), 'mcoords_s': round(a.n / ms / 1e3, 2),
+                     'tflops_fp32_equiv': round(F * a.n / ms / 1e9, 2),
+                     'frac_fp32_peak': round(F * a.n / ms / 1e9 / 157.3, 4)}
     out['pack_split_ms'] = round(timed(lambda: eng.pack_split(flat), 10), 4)
     y, g = eng.forward_grad(ws, x)
     ys, gs = eng.forward_grad_split(wsx, x)
