@@ -36,6 +36,8 @@ PATHS = {  # name: (d, hidden, layers, o, n, work units of F)
     'hypernet': (2, 256, 3, 1, 32 * 4096, 3),
     'w1': (2, 256, 3, 1, 1 << 20, 2),
     'w1x': (2, 256, 3, 1, 1 << 20, 2),      # the split-bf16 W1 (precision mode bf16x6), same workload as w1
+    'w0': (2, 256, 3, 1, 1 << 20, 1),       # the fp32 forward-only W0 (dense evaluation)
+    'w0x': (2, 256, 3, 1, 1 << 20, 1),      # the split-bf16 forward-only W0
     'w3_wide': (3, 512, 3, 1, 1 << 18, 6),
     'video1024': (3, 1024, 3, 3, 1 << 18, 3),   # the layered path (train_video.py's width)
     'video1024_rc': (3, 1024, 3, 3, 1 << 18, 3),
@@ -78,6 +80,11 @@ def build_step(name, dev):
     if name == 'w1x':
         wsx = eng.pack_split(flat)
         return lambda: eng.forward_grad_split(wsx, x)
+    if name == 'w0':
+        return lambda: eng.forward(ws, x)
+    if name == 'w0x':
+        wsx = eng.pack_split(flat)
+        return lambda: eng.forward_split(wsx, x)
     if name == 'fwd1024':
         return lambda: eng.forward(ws, x)
     if name == 'video1024':  # the training split the module runs: stored forward, reverse-only backward
