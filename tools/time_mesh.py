@@ -1,6 +1,6 @@
 """Timing of sdf_meshing on the device: the dense decoder evaluation of create_mesh on the
 fused W0 kernel (5x256 d3 SIREN, N^3 voxels) and the device marching cubes (marching.hip) on its volume. One JSON
-line per N. usage: python tools/time_mesh.py [N ...]"""
+line per N. usage: python tools/time_mesh.py [--precision fp32|bf16x6] [N ...]"""
 import json
 import os
 import sys
@@ -11,14 +11,14 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main(Ns):
+def main(Ns, precision='fp32'):
     import __graft_entry__
     __graft_entry__.build()
     from siren_amd import sdf_meshing as M
     from siren_amd.modules import SingleBVPNet
     dev = torch.device('cuda', 0)
     torch.manual_seed(0)
-    m = SingleBVPNet(in_features=3, verbose=False).to(dev)
+    m = SingleBVPNet(in_features=3, verbose=False, precision=precision).to(dev)
     dec = lambda c: m({'coords': c})['model_out']  # noqa: E731
     dec.parameters = m.parameters
     for N in Ns:
@@ -36,11 +36,15 @@ def main(Ns):
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         mc_ms = (t2 - t1) / reps * 1e3
-        print(json.dumps({'N': N, 'voxels': N ** 3, 'eval_ms': round((t1 - t0) * 1e3, 2),
+        print(json.dumps({'N': N, 'precision': precision, 'voxels': N ** 3, 'eval_ms': round((t1 - t0) * 1e3, 2),
                           'eval_mcoords_s': round(N ** 3 / (t1 - t0) / 1e6, 1), 'mc_ms': round(mc_ms, 3),
                           'mc_gvox_s': round(N ** 3 / mc_ms / 1e6, 2), 'verts': int(v.shape[0]),
                           'faces': int(f.shape[0])}), flush=True)
 
 
 if __name__ == '__main__':
-    main([int(a) for a in sys.argv[1:]] or [256, 512])
+    args = sys.argv[1:]
+    prec = 'fp32'
+    if len(args) >= 2 and args[0] == '--precision':
+        prec, args = args[1], args[2:]
+    main([int(a) for a in args] or [256, 512], prec)
