@@ -76,11 +76,37 @@ def _host_cpu():
     return model, len(cores) or None
 
 
+def _cpu_allotment():
+    """CPUs this process may use: its affinity set, capped by the cgroup CPU quota (cpu.max) when one is set; the GPU
+    box leases a share of a large host, and nproc / os.cpu_count() show the whole machine there."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    quota = None
+    for path in ('/sys/fs/cgroup/cpu.max', '/sys/fs/cgroup/cpu/cpu.cfs_quota_us'):
+        try:
+            parts = open(path).read().split()
+        except OSError:
+            continue
+        if path.endswith('cpu.max') and parts and parts[0] != 'max':
+            quota = float(parts[0]) / float(parts[1])
+        elif path.endswith('cfs_quota_us') and parts and int(parts[0]) > 0:
+            period = float(open('/sys/fs/cgroup/cpu/cpu.cfs_period_us').read())
+            quota = float(parts[0]) / period
+        break
+    usable = affinity if quota is None else max(1, min(affinity, int(quota + 0.5)))
+    return usable, affinity, quota
+
+
 def cpu_baseline(sizes=(1 << 16, 1 << 18, 1 << 20), seconds=4.):
     """The oracle's torch restatement (reference op sequence + autograd gradient, i.e. the reference's CPU path) on
     the host cores at N = 2^16, 2^18, 2^20: at least one full pass and ~`seconds` of passes per
     size. value = the N = 2^20 rate (the headline workload's size)."""
     from oracle import siren_oracle as O
+    threads_before = torch.get_num_threads()
+    usable, affinity, quota = _cpu_allotment()
+    torch.set_num_threads(usable)  # every CPU the lease gives this process (SURVEY.md §8d: all host cores)
     torch.manual_seed(0)
     dims = [D_IN] + [H] * (LH + 1) + [D_OUT]
     params = []
@@ -103,12 +129,16 @@ def cpu_baseline(sizes=(1 << 16, 1 << 18, 1 << 20), seconds=4.):
         rates['n_2e%d' % (n.bit_length() - 1)] = round(done / el / 1e6, 4)
         total += el
     model, phys = _host_cpu()
+    used = torch.get_num_threads()
+    torch.set_num_threads(threads_before)
     return {'value': rates['n_2e%d' % (sizes[-1].bit_length() - 1)], 'unit': 'Mcoords/s',
-            'cores': torch.get_num_threads(), 'kind': 'port', 'rates_by_n': rates, 'cpu_model': model,
-            'host_physical_cores': phys,
+            'cores': used, 'kind': 'port', 'rates_by_n': rates, 'cpu_model': model,
+            'host_physical_cores': phys, 'lease_affinity_cpus': affinity,
+            'lease_cgroup_cpu_quota': quota, 'all_lease_cpus_used': used == usable,
             'sample': 'N = %s coords, >= %.0f s each (%.1f s total): 5x256 d2 o1 fwd + autograd gradient, torch CPU '
-                      'fp32 on %d threads' % ('/'.join('2^%d' % (n.bit_length() - 1) for n in sizes), seconds, total,
-                                               torch.get_num_threads())}
+                      'fp32 on %d threads = every CPU of the lease (affinity %d CPUs, cgroup quota %s)'
+                      % ('/'.join('2^%d' % (n.bit_length() - 1) for n in sizes), seconds, total, used, affinity,
+                         'none' if quota is None else '%.1f CPUs' % quota)}
 
 
 def kernel_roofline(eng, ws, x, reps=10):

@@ -17,8 +17,10 @@
  * Conventions
  *  - Every entry point returns 0 on success, otherwise a SIREN_E* code; siren_last_error() then returns a
  *    thread-local message. No C++ exception crosses this ABI.
- *  - All buffers are device pointers owned by the caller (PyTorch caching allocator). The library never
- *    allocates device memory. fp32, contiguous, row-major:
+ *  - All buffers are device pointers owned by the caller (PyTorch caching allocator). The fused kernels (hidden
+ *    256 / 512) never allocate device memory. The one exception is the layered path of other hidden widths: its
+ *    layer GEMMs go through a library-owned rocBLAS handle per device (created on first use), and rocBLAS manages
+ *    that handle's own device memory (its internal state and GEMM workspace). fp32, contiguous, row-major:
  *      x (n, d_in); y (n, d_out); gy (n, d_out); gx (n, d_in).
  *  - params is ONE flat fp32 buffer in nn.Linear / state_dict order:
  *      W_0 (H, d_in), b_0 (H), [W_l (H, H), b_l (H)] for l = 1..n_hidden, W_out (d_out, H), b_out (d_out)
@@ -38,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SIREN_ABI_VERSION 2
+#define SIREN_ABI_VERSION 3
 
 enum {
     SIREN_OK = 0,
@@ -238,7 +240,8 @@ int32_t siren_adam_step(float* params, const float* grads, float* exp_avg, float
  * in index units * spacing, faces wound so normals point towards increasing value. Two calls: siren_mc_count
  * (classification + scans; synchronises the stream to return the sizes), then siren_mc_emit into caller buffers
  * verts (n_verts, 3) fp32 and faces (n_faces, 3) int32; spacing3 is a HOST pointer to 3 floats. ws:
- * siren_mc_ws_bytes, 4-byte aligned, kept between the two calls. X * Y * Z < 2^32, X, Y <= 65535; volumes
+ * siren_mc_ws_bytes, 4-byte aligned, kept between the two calls. X * Y * Z < 2^32, X, Y <= 65535, fewer than 2^31
+ * vertices and triangles (siren_mc_count returns SIREN_EUNSUPPORTED otherwise); volumes
  * with an axis < 2 give an empty mesh. */
 int32_t siren_mc_ws_bytes(int64_t X, int64_t Y, int64_t Z, int64_t* bytes);
 int32_t siren_mc_count(const float* vol, int64_t X, int64_t Y, int64_t Z, float level, void* ws, int64_t* n_verts,
@@ -251,10 +254,28 @@ int32_t siren_mc_emit(const float* vol, int64_t X, int64_t Y, int64_t Z, float l
  * meta_modules.py:41-53) applied to coords (B, n, d_in). Element b reads params + b * param_count (state-dict
  * order, as siren_pack), ws + b * workspace_floats, x + b * n * d_in, and writes y + b * n * d_out, gx + b * n * d_in,
  * gparams + b * param_count. batch <= 65535. */
-/* siren_pack_batched fills what the batched entry points read: for a linear-output hidden-256 network only the
- * phase-scaled half of each element's workspace (run siren_pack on an element before passing its workspace to the
- * single-network second / third-order or Laplacian entry points). */
+/* siren_pack_batched fills what the first-order batched entry points read: for a linear-output hidden-256 network
+ * only the phase-scaled half of each element's workspace. siren_pack_batched_ex with full = 1 writes every element's
+ * whole image (what siren_pack writes): required by siren_second_order_batched / siren_hvp_backward_batched and by
+ * any single-network entry point handed one element's workspace; full = 0 is siren_pack_batched. */
 int32_t siren_pack_batched(const siren_cfg* cfg, const float* params, int64_t batch, float* ws, void* stream);
+int32_t siren_pack_batched_ex(const siren_cfg* cfg, const float* params, int64_t batch, float* ws, int32_t full,
+                              void* stream);
+/* Second and third order over batched weights: the backward of a hypernetwork hypo-network's gradient node
+ * (gradients_mse / divergence(gradient()) on SingleBVPNet(params=...), loss_functions.py:84-109 through
+ * meta_modules.py:81-92). Element b runs siren_second_order_ex / siren_hvp_backward on ws + b * workspace_floats
+ * (packed with full = 1), x / v / g / gx / gv + b * n * d_in, u / gy / ydot / gu + b * n * d_out,
+ * gparams + b * param_count (nullable outputs as there). tws: the *_batched_ws_floats count, reused element after
+ * element in stream order. */
+int32_t siren_second_order_batched_ws_floats(const siren_cfg* cfg, int64_t n, int64_t batch, int32_t want_theta,
+                                             int64_t* count);
+int32_t siren_second_order_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
+                                   const float* v, const float* u, const float* gy, float* tws, float* gx,
+                                   float* gparams, float* ydot, void* stream);
+int32_t siren_hvp_backward_batched_ws_floats(const siren_cfg* cfg, int64_t n, int64_t batch, int64_t* count);
+int32_t siren_hvp_backward_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
+                                   const float* v, const float* u, const float* g, float* tws, float* gx,
+                                   float* gparams, float* gv, float* gu, void* stream);
 /* W0 for every element in ONE grouped launch (grid.y = element) at hidden 256, linear output, 1..5 hidden layers;
  * other configurations run siren_forward element by element. */
 int32_t siren_forward_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,

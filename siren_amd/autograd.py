@@ -253,8 +253,9 @@ class SirenBatchedFunction(torch.autograd.Function):
     batch (siren_forward_batched); under a parameter-gradient graph the grouped stored forward (FWDS: a_l / cos kept,
     siren_forward_store_batched). Backward: gx from one grouped W1 launch; theta-gradients (what flows back into the
     hypernetwork) from the grouped reverse-only W2 (siren_backward_stored_batched), or the recompute W2
-    (siren_backward_batched) when nothing was stored. Under create_graph each element
-    becomes a SirenVJP node (W1 forward, W3 backward) and theta-gradients recompute with device torch ops."""
+    (siren_backward_batched) when nothing was stored. Under create_graph gx becomes ONE SirenBatchedVJP node (grouped W1
+    forward, per-element W3 backward on a fully packed image); theta-gradients under create_graph (meta-learning only)
+    recompute with device torch ops."""
 
     @staticmethod
     def forward(ctx, engine, x, flat, store=False):
@@ -286,12 +287,87 @@ class SirenBatchedFunction(torch.autograd.Function):
             elif need_x:
                 _, gx = engine.forward_grad_batched(ws, x, gy, want_y=False)
             return None, (gx if need_x else None), gp, None
+        # create_graph: differentiable in (x, theta, gy). The second / third-order kernels read every element's
+        # whole packed image, which the forward's first-order pack does not write (siren_pack_batched): repack full
         if need_x:
-            gx = torch.stack([SirenVJP.apply(engine, ws[b], x[b], flat[b], gy[b]) for b in range(x.shape[0])])
-        if need_p:
+            gx = SirenBatchedVJP.apply(engine, engine.pack_batched(flat, full=True), x, flat, gy)
+        if need_p:  # theta-gradients under create_graph (meta-learning; no reference caller): device torch
             gp = torch.stack([_torch_path.vjp_params(engine.cfg, x[b], flat[b], gy[b], create_graph=True)
                               for b in range(x.shape[0])])
         return None, gx, gp, None
+
+
+def _stack_or_none(parts):
+    return None if parts[0] is None else torch.stack(parts)
+
+
+class SirenBatchedVJP(torch.autograd.Function):
+    """gx (B, n, d_in) = J_b^T gy_b for batched (hypernetwork) weights as ONE graph node: forward = one grouped W1
+    launch (siren_forward_grad_batched). Its backward is the W3 sweep of every element (siren_second_order_batched:
+    H v, the theta-gradient w.r.t. the predicted weights and J v) — what gradients_mse / sdf on a hypo network need;
+    under create_graph an x-only request becomes a SirenBatchedHVP node (divergence(gradient()), laplace_mse).
+    ws must be pack_batched(full=True)."""
+
+    @staticmethod
+    def forward(ctx, engine, ws, x, flat, gy):
+        _, gx = engine.forward_grad_batched(ws, x, gy, want_y=False)
+        ctx.engine, ctx.ws = engine, ws
+        ctx.save_for_backward(x, flat, gy)
+        return gx
+
+    @staticmethod
+    def backward(ctx, ggx):
+        x, flat, gy = ctx.saved_tensors
+        eng = ctx.engine
+        # tensor inputs in order: ws (0), x (1), flat (2), gy (3)
+        need_x = ctx.needs_input_grad[2] and _will_execute(ctx, 1)
+        need_p = ctx.needs_input_grad[3] and _will_execute(ctx, 2)
+        need_gy = ctx.needs_input_grad[4] and _will_execute(ctx, 3)
+        if not (need_x or need_p or need_gy):
+            return None, None, None, None, None
+        ggx = ggx.contiguous()
+        if not eng.second_order_supported or (torch.is_grad_enabled() and (need_p or need_gy)):
+            parts = [_torch_path.vjp_vjp(eng.cfg, x[b], flat[b], gy[b], ggx[b], create_graph=torch.is_grad_enabled())
+                     for b in range(x.shape[0])]
+            return (None, None) + tuple(_stack_or_none([p[i] for p in parts]) for i in range(3))
+        if torch.is_grad_enabled():  # x only, differentiable
+            return None, None, SirenBatchedHVP.apply(eng, ctx.ws, x, flat, ggx, gy), None, None
+        res = eng.second_order_batched(ctx.ws, x, ggx, want_theta=need_p, u=gy, want_ydot=need_gy)
+        gx, gp = res[0], res[1]
+        ggy = res[2] if need_gy else None
+        return None, None, (gx if need_x else None), gp, ggy
+
+
+class SirenBatchedHVP(torch.autograd.Function):
+    """h_b = sum_j u_bj H_bj(x) v_b for batched weights as ONE graph node (the per-dimension node of divergence() on a
+    hypo network's gradient): forward = W3 per element (x part only); backward = the mixed-jet third-order adjoint
+    per element (siren_hvp_backward_batched). ws must be pack_batched(full=True)."""
+
+    @staticmethod
+    def forward(ctx, engine, ws, x, flat, v, u=None):
+        gx, _ = engine.second_order_batched(ws, x, v.contiguous(), want_theta=False, u=u)
+        ctx.engine, ctx.ws = engine, ws
+        ctx.save_for_backward(x, flat, v, u)
+        return gx
+
+    @staticmethod
+    def backward(ctx, g):
+        x, flat, v, u = ctx.saved_tensors
+        eng = ctx.engine
+        if eng.hvp_backward_supported and not torch.is_grad_enabled():
+            # tensor inputs in order: ws (0), x (1), flat (2), v (3), u (4, when given)
+            need_x = ctx.needs_input_grad[2] and _will_execute(ctx, 1)
+            need_p = ctx.needs_input_grad[3] and _will_execute(ctx, 2)
+            need_v = ctx.needs_input_grad[4] and _will_execute(ctx, 3)
+            need_u = u is not None and ctx.needs_input_grad[5] and _will_execute(ctx, 4)
+            if not (need_x or need_p or need_v or need_u):
+                return None, None, None, None, None, None
+            gx, gp, gv, gu = eng.hvp_backward_batched(ctx.ws, x, v, g.contiguous(), u, want_theta=need_p,
+                                                      want_v=need_v, want_u=need_u)
+            return None, None, (gx if need_x else None), gp, gv, gu
+        parts = [_torch_path.hvp_vjp(eng.cfg, x[b], flat[b], v[b], g[b], create_graph=torch.is_grad_enabled(),
+                                     u=None if u is None else u[b]) for b in range(x.shape[0])]
+        return (None, None) + tuple(_stack_or_none([p[i] for p in parts]) for i in range(4))
 
 
 class SirenLaplace(torch.autograd.Function):

@@ -267,17 +267,22 @@ dim3 ew_grid(int64_t work) {
     return dim3((unsigned)(b < 8192 ? (b > 0 ? b : 1) : 8192));
 }
 
-// one rocBLAS handle per device, created lazily; calls are serialised (a handle is not thread-safe)
+// one rocBLAS handle per device, created lazily; calls are serialised (a handle is not thread-safe). The handle is
+// that of the device owning the stream (not the caller's current device), and that device is current for the
+// duration of the call (restored afterwards)
 std::mutex g_blas_mu;
 rocblas_handle g_blas[64] = {};
 
 struct Blas {
     std::lock_guard<std::mutex> lock;
     rocblas_handle h = nullptr;
+    int prev = -1;
     explicit Blas(hipStream_t st) : lock(g_blas_mu) {
         int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (dev < 0 || dev >= 64) dev = 0;
+        (void)hipGetDevice(&prev);
+        if (st == nullptr || hipStreamGetDevice(st, &dev) != hipSuccess) dev = prev;
+        if (dev < 0 || dev >= 64) return;
+        if (dev != prev && hipSetDevice(dev) != hipSuccess) return;
         if (g_blas[dev] == nullptr) {
             if (rocblas_create_handle(&g_blas[dev]) != rocblas_status_success) return;
             rocblas_set_atomics_mode(g_blas[dev], rocblas_atomics_not_allowed);
@@ -285,6 +290,10 @@ struct Blas {
         }
         h = g_blas[dev];
         rocblas_set_stream(h, st);
+    }
+    ~Blas() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
     }
 };
 

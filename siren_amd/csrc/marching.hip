@@ -164,10 +164,13 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_reduce_kernel(const uint32_
     if (threadIdx.x == 0) bsum[blockIdx.x] = total;
 }
 
-// one workgroup: exclusive scan of the nb block sums in place, the grand total at bsum[nb]
+// one workgroup: exclusive scan of the nb block sums in place, the grand total at bsum[nb] — saturated to 0xffffffff
+// when it reaches 2^31 (the offsets are uint32 and the faces int32: siren_mc_count then refuses the volume instead of
+// emitting wrapped indices; one pass's total is <= 1024 x 4096 x 5 items, so the 64-bit carry is exact)
 __global__ __launch_bounds__(1024) void scan_blocks_kernel(uint32_t* __restrict__ bsum, int64_t nb) {
     __shared__ uint32_t w[16];
     uint32_t carry = 0;
+    uint64_t carry64 = 0;
     for (int64_t b0 = 0; b0 < nb; b0 += blockDim.x) {
         const int64_t e = b0 + threadIdx.x;
         const uint32_t x = e < nb ? bsum[e] : 0u;
@@ -175,8 +178,9 @@ __global__ __launch_bounds__(1024) void scan_blocks_kernel(uint32_t* __restrict_
         const uint32_t ex = block_exclusive_scan(x, w, total);
         if (e < nb) bsum[e] = carry + ex;
         carry += total;
+        carry64 += total;
     }
-    if (threadIdx.x == 0) bsum[nb] = carry;
+    if (threadIdx.x == 0) bsum[nb] = carry64 >= (1ull << 31) ? 0xffffffffu : carry;
 }
 
 // per workgroup: its items -> exclusive prefix (in place), offset by the scanned block sum

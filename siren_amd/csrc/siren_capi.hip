@@ -976,6 +976,9 @@ int32_t siren_mc_count(const float* vol, int64_t X, int64_t Y, int64_t Z, float 
         hipMemcpyAsync(&tf, siren::mc_totals(w, X, Y, Z, 1), 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
         return fail(SIREN_EHIP, "siren_mc_count: reading the totals failed");
+    if (tv >= (1u << 31) || tf >= (1u << 31))  // saturated by the scan: int32 face indices would wrap
+        return fail(SIREN_EUNSUPPORTED, "siren_mc_count: the surface has >= 2^31 vertices or triangles; mesh the "
+                                        "volume in pieces");
     *n_verts = tv;
     *n_faces = tf;
     return SIREN_OK;
@@ -1040,6 +1043,68 @@ int32_t siren_pack_batched(const siren_cfg* cfg, const float* params, int64_t ba
                        wide(cfg) ? 0 : ws_base(cfg), cfg->omega_first * kInv2Pi, cfg->omega_hidden * kInv2Pi,
                        (hipStream_t)stream, (int)batch, param_count(cfg), scaled_only ? ws_base(cfg) : 0);
     return hip_status("siren_pack_batched");
+}
+
+int32_t siren_pack_batched_ex(const siren_cfg* cfg, const float* params, int64_t batch, float* ws, int32_t full,
+                              void* stream) {
+    if (!full) return siren_pack_batched(cfg, params, batch, ws, stream);
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (batch < 0 || batch > 65535) return fail(SIREN_EINVAL, "batch must be in [0, 65535]");
+    if (batch == 0) return SIREN_OK;
+    if (params == nullptr || ws == nullptr) return fail(SIREN_EINVAL, "params/ws is NULL");
+    if (layered(cfg)) return siren_pack_batched(cfg, params, batch, ws, stream);
+    siren::launch_pack(params, ws, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden, small_pad(cfg), ws_floats(cfg),
+                       wide(cfg) ? 0 : ws_base(cfg), cfg->omega_first * kInv2Pi, cfg->omega_hidden * kInv2Pi,
+                       (hipStream_t)stream, (int)batch, param_count(cfg), 0);
+    return hip_status("siren_pack_batched_ex");
+}
+
+// second / third order over batched weights (the create_graph branch of a hypernetwork's hypo network): element b's
+// fully packed workspace (siren_pack_batched_ex full = 1) through the single-network entry points, tws reused element
+// after element (stream order)
+int32_t siren_second_order_batched_ws_floats(const siren_cfg* cfg, int64_t n, int64_t batch, int32_t want_theta,
+                                             int64_t* count) {
+    if (batch < 0) return fail(SIREN_EINVAL, "batch < 0");
+    return siren_second_order_ws_floats(cfg, n, want_theta, count);
+}
+
+int32_t siren_second_order_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
+                                   const float* v, const float* u, const float* gy, float* tws, float* gx,
+                                   float* gparams, float* ydot, void* stream) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (n < 0 || batch < 0 || batch > 65535) return fail(SIREN_EINVAL, "need n >= 0 and 0 <= batch <= 65535");
+    const int64_t W = ws_floats(cfg), P = param_count(cfg);
+    const int d = cfg->d_in, o = cfg->d_out;
+    if (batch > 0 && ws == nullptr) return fail(SIREN_EINVAL, "ws is NULL");
+    for (int64_t b = 0; b < batch; ++b)
+        if (int rc = siren_second_order_ex(cfg, ws + b * W, x ? x + b * n * d : nullptr, n, v ? v + b * n * d : nullptr,
+                                           u ? u + b * n * o : nullptr, gy ? gy + b * n * o : nullptr, tws,
+                                           gx ? gx + b * n * d : nullptr, gparams ? gparams + b * P : nullptr,
+                                           ydot ? ydot + b * n * o : nullptr, stream))
+            return rc;
+    return SIREN_OK;
+}
+
+int32_t siren_hvp_backward_batched_ws_floats(const siren_cfg* cfg, int64_t n, int64_t batch, int64_t* count) {
+    if (batch < 0) return fail(SIREN_EINVAL, "batch < 0");
+    return siren_hvp_backward_ws_floats(cfg, n, count);
+}
+
+int32_t siren_hvp_backward_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
+                                   const float* v, const float* u, const float* g, float* tws, float* gx,
+                                   float* gparams, float* gv, float* gu, void* stream) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (n < 0 || batch < 0 || batch > 65535) return fail(SIREN_EINVAL, "need n >= 0 and 0 <= batch <= 65535");
+    const int64_t W = ws_floats(cfg), P = param_count(cfg);
+    const int d = cfg->d_in, o = cfg->d_out;
+    if (batch > 0 && ws == nullptr) return fail(SIREN_EINVAL, "ws is NULL");
+    for (int64_t b = 0; b < batch; ++b)
+        if (int rc = siren_hvp_backward(cfg, ws + b * W, x ? x + b * n * d : nullptr, n, v ? v + b * n * d : nullptr,
+                                        u ? u + b * n * o : nullptr, g ? g + b * n * d : nullptr, tws,
+                                        gx ? gx + b * n * d : nullptr, gparams ? gparams + b * P : nullptr,
+                                        gv ? gv + b * n * d : nullptr, gu ? gu + b * n * o : nullptr, stream))
+            return rc;
+    return SIREN_OK;
 }
 
 int32_t siren_forward_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,

@@ -63,8 +63,11 @@ def allreduce_gradients(params, world=None, count=None):
     if not (dist.is_available() and dist.is_initialized()):
         return
     world = world or dist.get_world_size()
-    if count is not None:  # every rank sends the full bucket, an empty shard's (unset) grads as zeros
-        params = list(params)
+    if count is not None:
+        # every rank sends the full bucket of TRAINABLE parameters (so every rank must train the same set, for the
+        # buckets to line up), an empty shard's unset grads as zeros; frozen parameters keep grad None, which
+        # torch.optim skips (a zero grad would still receive weight decay / momentum)
+        params = [p for p in params if p.requires_grad]
         for p in params:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)

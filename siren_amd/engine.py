@@ -330,17 +330,76 @@ class SirenEngine:
             raise ValueError('batched coords must be (B, n, %d); got %s' % (self.cfg.d_in, tuple(x.shape)))
         return x.contiguous()
 
-    def pack_batched(self, flat):
-        """flat (B, param_count) -> packed workspaces (B, ws_floats), one grouped launch."""
+    def pack_batched(self, flat, full=False):
+        """flat (B, param_count) -> packed workspaces (B, ws_floats), one grouped launch. full=False writes what the
+        first-order batched entry points read (hidden 256: the phase-scaled half only); full=True the whole image
+        of every element, which second_order_batched / hvp_backward_batched and single-network calls need."""
         self._require()
         if flat.dim() != 2 or flat.shape[1] != self.param_count or flat.dtype != torch.float32 \
                 or flat.device.type != 'cuda':
             raise ValueError('batched params must be fp32 (B, %d) on a ROCm device' % self.param_count)
         flat = flat.contiguous()
         ws = torch.empty(flat.shape[0], self.ws_floats, dtype=torch.float32, device=flat.device)
-        _lib.check(self.lib.siren_pack_batched(ctypes.byref(self.cfg), _ptr(flat), flat.shape[0], _ptr(ws),
-                                               _stream(flat.device)), 'siren_pack_batched')
+        _lib.check(self.lib.siren_pack_batched_ex(ctypes.byref(self.cfg), _ptr(flat), flat.shape[0], _ptr(ws),
+                                                  1 if full else 0, _stream(flat.device)), 'siren_pack_batched_ex')
         return ws
+
+    def _check_batched_like(self, name, t, shape, device):
+        if t is None:
+            return None
+        if tuple(t.shape) != tuple(shape) or t.dtype != torch.float32 or t.device != device:
+            raise ValueError('%s must be fp32 %s on %s; got %s %s' % (name, tuple(shape), device, t.dtype,
+                                                                    tuple(t.shape)))
+        return t.contiguous()
+
+    def second_order_batched(self, ws, x, v, want_theta=True, gy=None, u=None, want_ydot=False):
+        """second_order for every element of batched weights (ws from pack_batched(full=True)): x, v (B, n, d_in),
+        u / gy (B, n, d_out) nullable. Returns (gx (B, n, d_in), gparams (B, P) | None[, ydot (B, n, d_out)])."""
+        self._require()
+        if not self.second_order_supported:
+            raise _lib.SirenUnsupported('siren_second_order covers d_out <= 4, linear output, hidden 256 with 1..3 '
+                                        'hidden layers or hidden 512')
+        x = self._check_xb(x)
+        B, n, d, o = x.shape[0], x.shape[1], self.cfg.d_in, self.cfg.d_out
+        v = self._check_batched_like('v', v, (B, n, d), x.device)
+        gy = self._check_batched_like('gy', gy, (B, n, o), x.device)
+        u = self._check_batched_like('u', u, (B, n, o), x.device)
+        cnt = ctypes.c_int64()
+        _lib.check(self.lib.siren_second_order_batched_ws_floats(ctypes.byref(self.cfg), n, B, 1 if want_theta else 0,
+                                                                 ctypes.byref(cnt)), 'siren_second_order_batched_ws_floats')
+        tws = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
+        gx = torch.empty(B, n, d, dtype=torch.float32, device=x.device)
+        gp = torch.empty(B, self.param_count, dtype=torch.float32, device=x.device) if want_theta else None
+        ydot = torch.empty(B, n, o, dtype=torch.float32, device=x.device) if want_ydot else None
+        _lib.check(self.lib.siren_second_order_batched(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, B, _ptr(v), _ptr(u),
+                                                       _ptr(gy), _ptr(tws), _ptr(gx), _ptr(gp), _ptr(ydot),
+                                                       _stream(x.device)), 'siren_second_order_batched')
+        return (gx, gp, ydot) if want_ydot else (gx, gp)
+
+    def hvp_backward_batched(self, ws, x, v, g, u=None, want_theta=True, want_v=False, want_u=False):
+        """hvp_backward for every element of batched weights (ws from pack_batched(full=True)). Returns
+        (gx (B, n, d_in), gparams (B, P) | None, gv | None, gu | None)."""
+        self._require()
+        if not self.hvp_backward_supported:
+            raise _lib.SirenUnsupported('siren_hvp_backward covers a linear output, hidden 256 (1..5 hidden layers) '
+                                        'or hidden 512')
+        x = self._check_xb(x)
+        B, n, d, o = x.shape[0], x.shape[1], self.cfg.d_in, self.cfg.d_out
+        v = self._check_batched_like('v', v, (B, n, d), x.device)
+        g = self._check_batched_like('g', g, (B, n, d), x.device)
+        u = self._check_batched_like('u', u, (B, n, o), x.device)
+        cnt = ctypes.c_int64()
+        _lib.check(self.lib.siren_hvp_backward_batched_ws_floats(ctypes.byref(self.cfg), n, B, ctypes.byref(cnt)),
+                   'siren_hvp_backward_batched_ws_floats')
+        tws = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
+        gx = torch.empty(B, n, d, dtype=torch.float32, device=x.device)
+        gp = torch.empty(B, self.param_count, dtype=torch.float32, device=x.device) if want_theta else None
+        gv = torch.empty(B, n, d, dtype=torch.float32, device=x.device) if want_v else None
+        gu = torch.empty(B, n, o, dtype=torch.float32, device=x.device) if want_u else None
+        _lib.check(self.lib.siren_hvp_backward_batched(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, B, _ptr(v), _ptr(u),
+                                                       _ptr(g), _ptr(tws), _ptr(gx), _ptr(gp), _ptr(gv), _ptr(gu),
+                                                       _stream(x.device)), 'siren_hvp_backward_batched')
+        return gx, gp, gv, gu
 
     def forward_batched(self, ws, x):
         """W0 over (B, n, d_in) with per-element weights -> (B, n, d_out)."""

@@ -168,13 +168,15 @@ def convert_sdf_samples_to_ply(pytorch_3d_sdf_tensor, voxel_grid_origin, voxel_s
     return mesh_points, faces
 
 
-def create_mesh(decoder, filename, N=256, max_batch=1 << 22, offset=None, scale=None, log=print):
-    """sdf_meshing.py:13-71 on the device: dense decoder evaluation + level-0 surface -> filename + '.ply'."""
+def create_mesh(decoder, filename, N=256, max_batch=64 ** 3, offset=None, scale=None):
+    """sdf_meshing.py:13-71 on the device: decoder.eval(), dense decoder evaluation in max_batch chunks (the reference's
+    defaults; a larger max_batch means fewer, larger W0 launches) + level-0 surface -> filename + '.ply'."""
     start = time.time()
+    if hasattr(decoder, 'eval'):
+        decoder.eval()
     voxel_origin = [-1, -1, -1]
     voxel_size = 2.0 / (N - 1)
     dev = next(iter(decoder.parameters())).device if hasattr(decoder, 'parameters') else torch.device('cuda')
     sdf = evaluate_sdf_grid(decoder, N, max_batch, device=dev, out_device=dev)
-    if log:
-        log('sampling takes: %f' % (time.time() - start))
+    print('sampling takes: %f' % (time.time() - start))
     return convert_sdf_samples_to_ply(sdf, voxel_origin, voxel_size, os.fspath(filename) + '.ply', offset, scale)

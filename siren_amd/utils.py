@@ -58,26 +58,26 @@ def sdf_slices(model, resolution=512):
 
 
 def make_contour_plot(array_2d, mode='log'):
-    """utils.py:225-246 (matplotlib, 'agg')."""
+    """Filled-contour figure of a 2-D SDF slice for write_sdf_summary (the reference's helper, utils.py:225-246, drawn
+    with the same figure): symmetric levels — 'log': +-10^-2 .. 10^0 in six magnitudes per sign, 13 palette entries;
+    otherwise ten linear levels on [-0.5, 0.5] — from the 'Spectral' map, thin black isolines plus a heavier zero
+    level set, rows flipped so that the slice's first row is drawn at the bottom."""
     import matplotlib
     matplotlib.use('agg')
     import matplotlib.pyplot as plt
-    fig, ax = plt.subplots(figsize=(2.75, 2.75), dpi=300)
+    field = np.asarray(array_2d)[::-1]
     if mode == 'log':
-        num_levels = 6
-        levels_pos = np.logspace(-2, 0, num=num_levels)
-        levels = np.concatenate((-1. * levels_pos[::-1], np.zeros((0)), levels_pos), axis=0)
-        colors = plt.get_cmap('Spectral')(np.linspace(0., 1., num=num_levels * 2 + 1))
+        mags = np.logspace(-2, 0, 6)
+        levels, n_colors = np.concatenate([-mags[::-1], mags]), 13
     else:
-        num_levels = 10
-        levels = np.linspace(-.5, .5, num=num_levels)
-        colors = plt.get_cmap('Spectral')(np.linspace(0., 1., num=num_levels))
-    sample = np.flipud(array_2d)
-    cs = ax.contourf(sample, levels=levels, colors=colors)
-    fig.colorbar(cs)
-    ax.contour(sample, levels=levels, colors='k', linewidths=0.1)
-    ax.contour(sample, levels=[0], colors='k', linewidths=0.3)
-    ax.axis('off')
+        levels, n_colors = np.linspace(-.5, .5, 10), 10
+    palette = plt.get_cmap('Spectral')(np.linspace(0., 1., n_colors))
+    fig = plt.figure(figsize=(2.75, 2.75), dpi=300)
+    ax = fig.add_subplot()
+    fig.colorbar(ax.contourf(field, levels=levels, colors=palette))
+    for lv, lw in ((levels, 0.1), ([0.], 0.3)):
+        ax.contour(field, levels=lv, colors='k', linewidths=lw)
+    ax.set_axis_off()
     return fig
 
 

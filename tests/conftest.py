@@ -105,3 +105,8 @@ def g9():
 @pytest.fixture(scope='session')
 def g10():
     return load_golden('g10')
+
+
+@pytest.fixture(scope='session')
+def g11():
+    return load_golden('g11')

@@ -28,6 +28,8 @@ Fixtures:
   G10 hidden 1024 (the reference's train_video.py width): SingleBVPNet(in 3, out 3, hidden 1024) seed 0, 512 coords:
       parameter checksums (fp64 sums + first rows: the init pin without 12 MB of weights), model_out / gradient (fp32
       and fp64) and a slice of the fp64 image_mse theta-grads (first / output layers whole, 4 rows of every hidden W).
+  G11 second / third order through G7's batched weights: gradients_mse and laplace_mse (divergence(gradient()))
+      on SingleBVPNet(params=hypernetwork output), fp64 gradients w.r.t. the predicted weights and model_in.
   G6  vector outputs / PML losses: 5x256 d2 o2 (helmholtz_pml, loss_functions.py:139-211)
       and 5x256 d3 o1 (wave_pml, loss_functions.py:112-136), 1024 coords each: jacobian / hessian
       (diff_operators.py:5-24, 46-59), the loss terms and their fp64 theta-grads.
@@ -216,6 +218,54 @@ def make_g7(modules, D, L, meta):
     np.savez_compressed(os.path.join(OUT, 'golden_g7.npz'), **store)
 
 
+def make_g11(modules, D, L, meta):
+    """G11: second and third order through batched (hypernetwork) weights: G7's HyperNetwork weights (same seed,
+    checked equal to golden_g7's), the reference's gradients_mse (loss_functions.py:84-89) and laplace_mse (:104-109,
+    laplace = divergence(gradient()), diff_operators.py:27-36) on SingleBVPNet(params=...) in fp64: loss values, the
+    gradients w.r.t. every predicted weight tensor and w.r.t. model_in."""
+    import meta_modules
+    torch.manual_seed(8)
+    hypo = modules.SingleBVPNet(type='sine', in_features=2, out_features=1)
+    hyper = meta_modules.HyperNetwork(hyper_in_features=8, hyper_hidden_layers=1, hyper_hidden_features=32,
+                                      hypo_module=hypo)
+    z = torch.randn(3, 8)
+    gen = torch.Generator().manual_seed(7)
+    coords = torch.rand(3, 512, 2, generator=gen) * 2 - 1
+    with torch.no_grad():
+        params = hyper(z)
+    g7 = np.load(os.path.join(OUT, 'golden_g7.npz'))
+    for k, v in params.items():
+        assert np.array_equal(v.numpy().astype(np.float32), g7['p_' + k]), k
+    assert np.array_equal(coords.numpy(), g7['coords'])
+    gen = torch.Generator().manual_seed(11)
+    gt = {'gradients': torch.randn(3, 512, 2, generator=gen) * 10., 'laplace': torch.randn(3, 512, 1, generator=gen) * 100.}
+    store = {'gt_gradients': gt['gradients'].numpy(), 'gt_laplace': gt['laplace'].numpy()}
+    def run(lname, dtype):
+        hp = hypo.to(dtype)
+        pd = OrderedDict((k, v.to(dtype).requires_grad_(True)) for k, v in params.items())
+        out = hp({'coords': coords.to(dtype)}, params=pd)
+        ld = getattr(L, lname)(out, {k: v.to(dtype) for k, v in gt.items()})
+        total = sum(v.mean() for v in ld.values())
+        wrt = [out['model_in']] + list(pd.values())
+        grads = [torch.zeros_like(t) if g is None else g
+                 for t, g in zip(wrt, torch.autograd.grad(total, wrt, allow_unused=True))]  # bout: unused
+        return float(total.detach()), [g.detach().double().numpy() for g in grads]
+
+    for lname in ('gradients_mse', 'laplace_mse'):
+        total, grads = run(lname, torch.float64)
+        meta['G11_%s_f64' % lname] = total
+        store['G11_%s_xgrad' % lname] = grads[0]
+        for k, g in zip(params.keys(), grads[1:]):
+            store['G11_%s_grad_%s' % (lname, k)] = g.astype(np.float32)
+        # the reference's own fp32 error (SURVEY.md §8c: the floor a kernel's error is judged against), relative to
+        # the fp64 max, for model_in and every weight tensor
+        _, g32 = run(lname, torch.float32)
+        store['G11_%s_xgrad_f32_relerr' % lname] = np.array(np.max(np.abs(g32[0] - grads[0])) / np.max(np.abs(grads[0])))
+        for k, a, b in zip(params.keys(), g32[1:], grads[1:]):
+            store['G11_%s_grad_%s_f32_relerr' % (lname, k)] = np.array(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+    np.savez_compressed(os.path.join(OUT, 'golden_g11.npz'), **store)
+
+
 def import_reference_dataio():
     """dataio.py with the image / video packages it imports at module level stubbed (only get_mgrid is used)."""
     for name in ('skimage', 'skimage.filters', 'skvideo', 'skvideo.io', 'torchvision', 'torchvision.transforms',
@@ -359,7 +409,7 @@ def main():
         with open(os.path.join(OUT, 'manifest.json')) as f:
             meta = json.load(f)
         for name in args.only.split(','):
-            {'g6': make_g6, 'g7': make_g7, 'g8': make_g8, 'g9': make_g9, 'g10': make_g10}[name](modules, D, L, meta)
+            {'g6': make_g6, 'g7': make_g7, 'g8': make_g8, 'g9': make_g9, 'g10': make_g10, 'g11': make_g11}[name](modules, D, L, meta)
         with open(os.path.join(OUT, 'manifest.json'), 'w') as f:
             json.dump(meta, f, indent=1, sort_keys=True)
         return

@@ -124,3 +124,91 @@ def test_stored_batched_split_matches_recompute(cuda, B, n, d, L, o, H):
     gxr, gpr = eng.backward_params_batched(wsb, x, gy)
     assert float((gxs - gxr).abs().max()) <= 1e-5 * float(gxr.abs().max())
     assert float((gps - gpr).abs().max()) <= 1e-5 * float(gpr.abs().max())
+
+
+def _poison_pack(monkeypatch):
+    """pack_batched into a NaN-filled buffer: any read of a part the pack does not write poisons the result."""
+    import ctypes
+    from siren_amd import _lib, engine as E
+
+    def pack_batched(self, flat, full=False):
+        flat = flat.contiguous()
+        ws = torch.full((flat.shape[0], self.ws_floats), float('nan'), dtype=torch.float32, device=flat.device)
+        _lib.check(self.lib.siren_pack_batched_ex(ctypes.byref(self.cfg), E._ptr(flat), flat.shape[0], E._ptr(ws),
+                                                  1 if full else 0, E._stream(flat.device)), 'siren_pack_batched_ex')
+        return ws
+    monkeypatch.setattr(E.SirenEngine, 'pack_batched', pack_batched)
+
+
+def _forbid_torch_path(monkeypatch):
+    from siren_amd import _torch_path
+
+    def boom(*a, **k):
+        raise AssertionError('device-torch recompute used on a kernel-covered path')
+    for name in ('vjp_params', 'jacobian_vjp', 'vjp_vjp', 'hvp_vjp', 'laplace_vjp', 'forward', 'laplacian'):
+        monkeypatch.setattr(_torch_path, name, boom)
+
+
+@pytest.mark.parametrize('lname', ['gradients_mse', 'laplace_mse'])
+def test_hypo_second_and_third_order_vs_reference(cuda, g7, g11, monkeypatch, lname):
+    """gradients_mse (second order) and laplace_mse through the reference's divergence(gradient()) (third order) on a
+    hypernetwork-parameterised SingleBVPNet match the reference's G11 fp64 gradients w.r.t. every predicted weight
+    tensor and w.r.t. model_in — with the packed workspaces NaN-poisoned before packing (an unwritten read fails
+    loudly) and every device-torch recompute forbidden (W1 grouped forward, W3 / mixed-jet backward per element)."""
+    from siren_amd.modules import SingleBVPNet
+    from siren_amd import loss_functions as LF
+    _poison_pack(monkeypatch)
+    _forbid_torch_path(monkeypatch)
+    m = SingleBVPNet(in_features=2, out_features=1, verbose=False).to(cuda)
+    params = OrderedDict((k[2:], torch.tensor(v, device=cuda, requires_grad=True))
+                         for k, v in g7.items() if k.startswith('p_'))
+    out = m({'coords': torch.tensor(g7['coords'], device=cuda)}, params=params)
+    gt = {'gradients': torch.tensor(g11['gt_gradients'], device=cuda),
+          'laplace': torch.tensor(g11['gt_laplace'], device=cuda)}
+    ld = getattr(LF, lname)(out, gt)
+    total = sum(v.mean() for v in ld.values())
+    wrt = [out['model_in']] + list(params.values())
+    grads = torch.autograd.grad(total, wrt, allow_unused=True)
+    # the hypernetwork's third element has derivatives up to 1.5e5, where the reference's OWN fp32 run is already
+    # 5e-5 .. 8e-5 (relative to max) from its fp64 result (G11 *_f32_relerr): the bar is 1e-4 of max, or twice the
+    # reference's fp32 error where that is the larger (SURVEY.md §8c: the fp32 golden's error is the floor)
+    def bar(key):
+        return max(1e-4, 2. * float(g11[key + '_f32_relerr']))
+    gxr = g11['G11_%s_xgrad' % lname]
+    gx = grads[0].detach().cpu().numpy()
+    assert np.isfinite(gx).all()
+    rel = np.max(np.abs(gx - gxr)) / np.max(np.abs(gxr))
+    print('%s model_in grad: rel %.2e (reference fp32: %.2e)' % (lname, rel, float(g11['G11_%s_xgrad_f32_relerr' % lname])))
+    assert rel <= bar('G11_%s_xgrad' % lname), rel
+    for k, gr in zip(params.keys(), grads[1:]):
+        key = 'G11_%s_grad_%s' % (lname, k)
+        ref = g11[key]
+        got = np.zeros_like(ref) if gr is None else gr.cpu().numpy()
+        assert np.isfinite(got).all(), k
+        scale = max(float(np.max(np.abs(ref))), 1e-30)
+        assert np.max(np.abs(got - ref)) <= bar(key) * scale + 1e-12, (k, np.max(np.abs(got - ref)) / scale)
+
+
+@pytest.mark.parametrize('B,n,d,L,o,H', [(3, 1000, 2, 3, 1, 256), (2, 333, 3, 2, 3, 256), (2, 300, 3, 3, 2, 512)])
+def test_batched_second_third_order_equal_per_element(cuda, B, n, d, L, o, H):
+    """siren_second_order_batched / siren_hvp_backward_batched equal the single-network entry points element by
+    element (bitwise) on a full batched pack, which equals siren_pack per element."""
+    from siren_amd.engine import SirenEngine
+    eng = SirenEngine(d, H, L, o)
+    flat = torch.tensor(random_flat(B, d, L, o, H, seed=7 * n + B), device=cuda)
+    x = torch.rand(B, n, d, device=cuda) * 2 - 1
+    v = torch.randn(B, n, d, device=cuda)
+    g = torch.randn(B, n, d, device=cuda)
+    u = torch.randn(B, n, o, device=cuda)
+    gy = torch.randn(B, n, o, device=cuda)
+    wsb = eng.pack_batched(flat, full=True)
+    gxb, gpb, ydb = eng.second_order_batched(wsb, x, v, want_theta=True, gy=gy, u=u, want_ydot=True)
+    hx, hp, hv, hu = eng.hvp_backward_batched(wsb, x, v, g, u, want_theta=True, want_v=True, want_u=True)
+    for b in range(B):
+        ws = eng.pack(flat[b])
+        assert torch.equal(ws, wsb[b])
+        gx1, gp1, yd1 = eng.second_order(ws, x[b], v[b], want_theta=True, gy=gy[b], u=u[b], want_ydot=True)
+        assert torch.equal(gx1, gxb[b]) and torch.equal(gp1, gpb[b]) and torch.equal(yd1, ydb[b])
+        r = eng.hvp_backward(ws, x[b], v[b], g[b], u[b], want_theta=True, want_v=True, want_u=True)
+        for a1, ab in zip(r, (hx, hp, hv, hu)):
+            assert torch.equal(a1, ab[b])

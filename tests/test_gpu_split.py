@@ -204,3 +204,34 @@ def test_module_precision_bf16x6_no_grad_forward_and_mesh(cuda, g1):
         vols[prec] = sdf_meshing.evaluate_sdf_grid(lambda p, m=m: m({'coords': p})['model_out'], 64,
                                                     max_batch=1 << 16, device=cuda, out_device=cuda)
     assert float((vols['fp32'] - vols['bf16x6']).abs().max()) <= 1e-5
+
+
+@pytest.mark.parametrize('w0,w', [(30., 10.), (3000., 30.), (10., 30.)])
+@pytest.mark.parametrize('d', [2, 3])
+@pytest.mark.parametrize('n', [63, 1000, 4097])
+def test_split_distinct_omegas(cuda, w0, w, d, n):
+    """omega_first != omega_hidden on the split kernels (separate pack-scale corrections for the first layer and the
+    hidden layers): forward_grad_split and forward_split vs the fp64 oracle; the init divides by omega as the notebook
+    Siren does (ipynb:71-108), so the pre-activations keep the reference's scale."""
+    from siren_amd.engine import SirenEngine
+    rng = np.random.default_rng(n + d + int(w0))
+    dims = [d] + [256] * 4 + [1]
+    layers = []
+    for i, (fi, fo) in enumerate(zip(dims[:-1], dims[1:])):
+        bound = 1. / fi if i == 0 else np.sqrt(6. / fi) / w
+        layers.append((rng.uniform(-bound, bound, (fo, fi)).astype(np.float32),
+                       (rng.uniform(-1, 1, fo) / np.sqrt(fi)).astype(np.float32)))
+    eng = SirenEngine(d, 256, 3, 1, w0, w, True)
+    flat = to_dev(O.flatten(layers), cuda)
+    wsx = eng.pack_split(flat)
+    x = np.random.default_rng(n).uniform(-1, 1, (n, d)).astype(np.float32)
+    xd = to_dev(x, cuda)
+    y, gx = eng.forward_grad_split(wsx, xd)
+    yf = eng.forward_split(wsx, xd)
+    y32, gx32 = eng.forward_grad(eng.pack(flat), xd)
+    ry, rg = O.forward_grad(x, layers, omega_first=w0, omega_hidden=w)
+    # the fp32 kernel's own error bounds the split's (fp32-equivalent precision mode), as at omega 30 / 30
+    ey, eg = np.max(np.abs(y.cpu().numpy() - ry)), np.max(np.abs(gx.cpu().numpy() - rg))
+    ey32, eg32 = np.max(np.abs(y32.cpu().numpy() - ry)), np.max(np.abs(gx32.cpu().numpy() - rg))
+    assert ey <= max(1e-4, 2 * ey32) and eg <= max(tol_rel(rg), 2 * eg32 + 1e-6), (ey, eg, ey32, eg32)
+    assert np.max(np.abs(yf.cpu().numpy() - ry)) <= max(1e-4, 2 * ey32)

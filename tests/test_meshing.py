@@ -155,7 +155,7 @@ def test_create_mesh_on_fused_kernel(cuda, tmp_path):
     level = float(sdf.median())
     dec2 = lambda c: dec(c) - level  # noqa: E731
     dec2.parameters = m.parameters
-    pts_out, faces = M.create_mesh(dec2, os.path.join(tmp_path, 'mesh'), N=N, max_batch=1 << 16, log=None)
+    pts_out, faces = M.create_mesh(dec2, os.path.join(tmp_path, 'mesh'), N=N, max_batch=1 << 16)
     v, f = M.read_ply(os.path.join(tmp_path, 'mesh.ply'))
     assert f.shape[0] > 0 and v.shape[0] > 0 and f.max() < v.shape[0]
 
