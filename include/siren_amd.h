@@ -186,6 +186,21 @@ int32_t siren_hvp_backward(const siren_cfg* cfg, const float* ws, const float* x
                            const float* u, const float* g, float* tws, float* gx, float* gparams, float* gv,
                            float* gu, void* stream);
 
+/* The backward of a Hessian node Hm (n, d_in, d_in) = sum_j u_j H_j(x) (u (n, d_out), NULL = ones): the node that
+ * every divergence() / hessian() column of one gradient node reads (diff_operators.py:5-36), so autograd sums the
+ * cotangents of all those columns into ONE G (n, d_in, d_in) and the whole third-order backward of laplace_mse through
+ * the reference's divergence(gradient()) (loss_functions.py:104-109) is one call. With S = sum_c <G_c, Hm_c>
+ * = sum_c sum_j u_cj D2 Phi_j(x_c)[Q_c], Q = sym(G):
+ *   gx (n, d_in)          = dS/dx
+ *   gparams (param_count) = dS/dtheta                      (skipped when NULL)
+ *   gu (n, d_out)         = dS/du_j = D2 Phi_j[Q]          (skipped when NULL)
+ * One forward-mode jet (value, d/dx_1, d/dx_2, the second-order stream along Q) + its reverse (4 coordinates x 4
+ * streams per MFMA tile), the split-K MFMA weight gradient over 4n columns and a deterministic slab reduction. Hidden
+ * 256, linear output, 1..5 hidden layers, d_in <= 2. tws: siren_hessian_backward_ws_floats(cfg, n) floats. */
+int32_t siren_hessian_backward_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count);
+int32_t siren_hessian_backward(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* G,
+                               const float* u, float* tws, float* gx, float* gparams, float* gu, void* stream);
+
 /* Split-bf16 W1 (precision mode "bf16x6"): siren_forward_grad with gy = ones for the headline network (hidden 256,
  * 3 hidden layers, d_in 2 / 3, d_out 1, linear output) with the layer GEMMs on the bf16 matrix pipe. Every fp32
  * weight and activation is split exactly into three bf16 pieces (hi + mid + lo) and each K-step sums the six products

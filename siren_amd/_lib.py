@@ -79,6 +79,8 @@ _SIGS = {
     'siren_pack_split': [_CFG, _P, _P, _P],
     'siren_forward_grad_split': [_CFG, _P, _P, _I64, _P, _P, _P],
     'siren_forward_split': [_CFG, _P, _P, _I64, _P, _P],
+    'siren_hessian_backward_ws_floats': [_CFG, _I64, ctypes.POINTER(_I64)],
+    'siren_hessian_backward': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P],
     'siren_pack_batched_ex': [_CFG, _P, _I64, _P, ctypes.c_int32, _P],
     'siren_second_order_batched_ws_floats': [_CFG, _I64, _I64, ctypes.c_int32, ctypes.POINTER(_I64)],
     'siren_second_order_batched': [_CFG, _P, _P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P],

@@ -29,6 +29,12 @@
 // reverse gives every cotangent of the node at once:
 //   gx = W0^T zb_0,value   gv = W0^T zb_0,v   gu_j = D2 y_j[v, g] (the forward's last jet)   dtheta as for W4s
 // with the first layer's tangents W0 v / W0 g (per coordinate) and the output seed sum_j u_j Wout_j.
+//
+// QG = true (with MIX): the backward of a Hessian node Hm = sum_j u_j H_j(x) (n, d, d), d <= 2 — the node that every
+// divergence() / hessian() column of one gradient node shares, so autograd sums all their cotangents into ONE
+// cotangent G (n, d, d) and calls ONE backward. S = sum_c <G_c, Hm_c> = sum_c sum_j u_j D2 y_j(x_c)[Q_c] with
+// Q = sym(G): the tangents are the coordinate axes (as the W4 jet) and the second-order stream follows the
+// per-coordinate quadratic form Q (jet_sin_q / jet_sin_adjoint_q); tq (n, d, d) = G; gu_j = D2 y_j[Q].
 #include "lds_ops.h"
 #include "ring.hpp"
 #include "siren_common.h"
@@ -67,14 +73,15 @@ enum { JET_BOTH = 0, JET_FWD = 1, JET_REV = 2 };
 // JET_FWD: glap is unused and the outputs go to y (n, o) / gx (n, d) / lap (n) (each nullable)
 // MIX: tv / tg (n, d) the tangents v / g, tu (n, o) the output weighting (NULL = ones); gv (n, d) and gu (n, o)
 // nullable outputs; glap unused (JET_BOTH only)
-template <int PHASE, bool MIX = false>
+template <int PHASE, bool MIX = false, bool QG = false>
 __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
     const float* __restrict__ ws, const float* __restrict__ x, int64_t n, const float* __restrict__ glap,
     float* __restrict__ gx, int d, int o, int lh, float w0, float w, float* __restrict__ spill,
     float* __restrict__ abuf, float* __restrict__ dbuf, int64_t n_pad, float* __restrict__ y,
     float* __restrict__ lap, const float* __restrict__ tv, const float* __restrict__ tg,
-    const float* __restrict__ tu, float* __restrict__ gv, float* __restrict__ gu) {
+    const float* __restrict__ tu, float* __restrict__ gv, float* __restrict__ gu, const float* __restrict__ tq = nullptr) {
     static_assert(!MIX || PHASE == JET_BOTH, "the mixed jet runs as one launch");
+    static_assert(!QG || MIX, "the quadratic-form jet is the mixed jet's variant");
     __shared__ __attribute__((aligned(16))) float lds[NBUF * SLICE + SMALL_MAX];
     float* ring = lds;
     float* sm = lds + NBUF * SLICE;
@@ -99,7 +106,9 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
     float jcf[MAXD];  // first-layer coefficients of W0[:, k] per stream
 #pragma unroll
     for (int k = 0; k < MAXD; ++k) {
-        if constexpr (MIX) {
+        if constexpr (QG) {  // tangents along the coordinate axes (d <= 2)
+            jcf[k] = val * xv[k] + (js == k + 1 ? 1.f : 0.f);
+        } else if constexpr (MIX) {
             const float* tp = js == 1 ? tv : tg;
             jcf[k] = (valid && k < d && (js == 1 || js == 2)) ? tp[coord * d + k] : val * xv[k];
         } else {
@@ -111,6 +120,19 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
     const float m12 = (js == 1 || js == 2) ? 1.f : 0.f;
     const float gl = (PHASE != JET_FWD && valid && js == 3) ? (MIX ? 1.f : glap[coord]) : 0.f;
     const bool s1 = js == 1;
+    // QG: this coordinate's quadratic form Q = sym(G) (G (n, d, d), d <= 2; rows / columns beyond d are zero)
+    float q11 = 0.f, q12x2 = 0.f, q22 = 0.f;
+    if constexpr (QG) {
+        if (valid) {
+            const float* gq = tq + coord * d * d;
+            q11 = gq[0];
+            if (d > 1) {
+                q12x2 = gq[1] + gq[2];
+                q22 = gq[3];
+            }
+        }
+    }
+    const float qa = s1 ? 2.f * q11 : q12x2, qb = s1 ? q12x2 : 2.f * q22;  // this lane's row of 2 Q (streams 1, 2)
     __syncthreads();
     const int p0 = PHASE == JET_REV ? lh : 0, p1 = PHASE == JET_FWD ? lh : 2 * lh;
     int s = p0 * NB;
@@ -138,7 +160,7 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
             for (int k = 0; k < MAXD; ++k)
                 if (k < d) z += jcf[k] * *(const f32x4*)(sm + SM_W0 + k * H + nb);
             zs.next_store(z);
-            act[rb] = jet_sin<MIX>(z, w0, val, kb0, kg0);
+            act[rb] = QG ? jet_sin_q(z, w0, val, kb0, kg0, q11, q12x2, q22) : jet_sin<MIX>(z, w0, val, kb0, kg0);
         }
         jstore_tile(abuf + toff, act);
     }
@@ -164,7 +186,7 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
             for (int rb = 0; rb < NB; ++rb) {
                 const f32x4 z = acc[rb] + val * *(const f32x4*)(bl + 16 * rb);
                 zs.next_store(z);
-                act[rb] = jet_sin<MIX>(z, w, val, kb, kg);
+                act[rb] = QG ? jet_sin_q(z, w, val, kb, kg, q11, q12x2, q22) : jet_sin<MIX>(z, w, val, kb, kg);
             }
             jstore_tile(abuf + (int64_t)l * lstride + toff, act);
             if (PHASE == JET_FWD && l == lh) {
@@ -226,7 +248,8 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
                     } else {
                         sd = *(const f32x4*)(sm + SM_SEED + 16 * rb + 4 * g);
                     }
-                    act[rb] = jet_sin_adjoint<MIX>(gl * sd, zl.next_load(), w, val, m12, s1);
+                    act[rb] = QG ? jet_sin_adjoint_q(gl * sd, zl.next_load(), w, val, m12, q11, q12x2, q22, qa, qb)
+                                 : jet_sin_adjoint<MIX>(gl * sd, zl.next_load(), w, val, m12, s1);
                 }
                 jstore_tile(dbuf + (int64_t)lh * lstride + toff, act);
             }
@@ -237,7 +260,8 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
             const float wl = lm == 0 ? w0 : w;
 #pragma unroll
             for (int rb = 0; rb < NB; ++rb) {
-                act[rb] = jet_sin_adjoint<MIX>(acc[rb], zl.next_load(), wl, val, m12, s1);
+                act[rb] = QG ? jet_sin_adjoint_q(acc[rb], zl.next_load(), wl, val, m12, q11, q12x2, q22, qa, qb)
+                             : jet_sin_adjoint<MIX>(acc[rb], zl.next_load(), wl, val, m12, s1);
             }
             jstore_tile(dbuf + (int64_t)lm * lstride + toff, act);
         }

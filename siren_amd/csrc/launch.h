@@ -60,6 +60,9 @@ void launch_small_jet(dim3 grid, hipStream_t st, const float* abuf, const float*
 void launch_jet_mix(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* v,
                     const float* g, const float* u, float* gx, float* gv, float* gu, int d, int o, int lh, float w0,
                     float w, float* spill, float* abuf, float* dbuf, int64_t n_pad);
+void launch_jet_quad(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* G,
+                     const float* u, float* gx, float* gu, int d, int o, int lh, float w0, float w, float* spill,
+                     float* abuf, float* dbuf, int64_t n_pad);
 void launch_small_mix(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* v,
                       const float* g, const float* u, int64_t n, int64_t n_pad, int64_t tps, float* eslab, int64_t E,
                       int d, int o, int lh, int h);

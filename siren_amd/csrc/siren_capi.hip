@@ -770,6 +770,56 @@ int32_t siren_hvp_backward(const siren_cfg* cfg, const float* ws, const float* x
                         "siren_hvp_backward (reduce)");
 }
 
+// ---- the backward of a Hessian node Hm = sum_j u_j H_j (n, d, d): the quadratic-form jet (jet_kernel.hpp QG) ------
+namespace {
+int check_quad(const siren_cfg* cfg) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (wide(cfg) || layered(cfg) || !cfg->outermost_linear || cfg->n_hidden > 5 || cfg->d_in > 2)
+        return fail(SIREN_EUNSUPPORTED, "siren_hessian_backward covers hidden 256, 1..5 hidden layers, in_features "
+                                        "<= 2, linear output");
+    return SIREN_OK;
+}
+}  // namespace
+
+int32_t siren_hessian_backward_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count) {
+    if (int rc = check_quad(cfg)) return rc;
+    if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
+    *count = JetPlan(cfg, n).total;
+    return SIREN_OK;
+}
+
+int32_t siren_hessian_backward(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* G,
+                               const float* u, float* tws, float* gx, float* gparams, float* gu, void* stream) {
+    if (int rc = check_quad(cfg)) return rc;
+    if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    const JetPlan plan(cfg, n);
+    const hipStream_t st = (hipStream_t)stream;
+    const int64_t P = param_count(cfg);
+    if (n == 0) {
+        if (gparams != nullptr) (void)hipMemsetAsync(gparams, 0, P * sizeof(float), st);
+        return hip_status("siren_hessian_backward");
+    }
+    if (ws == nullptr || tws == nullptr || gx == nullptr || x == nullptr || G == nullptr)
+        return fail(SIREN_EINVAL, "ws/x/G/tws/gx is NULL");
+    float* abuf = tws;
+    float* dbuf = abuf + plan.buf_floats;
+    float* spill = dbuf + plan.buf_floats;
+    float* partial = spill + plan.buf_floats;
+    siren::launch_jet_quad(dim3((unsigned)(plan.n_pad / 16)), st, ws, x, n, G, u, gx, gu, cfg->d_in, cfg->d_out,
+                           cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, spill, abuf, dbuf, plan.n_pad);
+    if (int rc = hip_status("siren_hessian_backward (quadratic-form jet)")) return rc;
+    if (gparams == nullptr) return SIREN_OK;
+    siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden), st, abuf, dbuf, plan.cols, plan.tps,
+                        partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1, siren::H, 1);
+    if (int rc = hip_status("siren_hessian_backward (wgrad)")) return rc;
+    // EDGE_MIX with v = e_1, g = e_2 (NULL tangents): dW0[:, k] = sum zb_0,value x_k + zb_0,tangent k
+    siren::launch_small_mix(plan.es.grid(cfg), st, abuf, dbuf, x, nullptr, nullptr, u, n, plan.n_pad, plan.es.tps,
+                            partial + plan.eslab_off, plan.es.E, cfg->d_in, cfg->d_out, cfg->n_hidden, siren::H);
+    if (int rc = hip_status("siren_hessian_backward (small)")) return rc;
+    return finish_grads(cfg, st, partial, plan.splits, 0, partial + plan.eslab_off, plan.es, gparams,
+                        "siren_hessian_backward (reduce)");
+}
+
 // ---- W3: second-order adjoint (Hessian-vector product + mixed theta gradient), d_out == 1 ---------------
 namespace {
 struct W3Plan {

@@ -214,6 +214,44 @@ __device__ __forceinline__ f32x4 jet_sin_adjoint(const f32x4& u, const f32x4& z,
     return out;
 }
 
+// QUAD (the backward of a Hessian node, Hm = sum_j u_j H_j (n, d, d), d <= 2): streams (value, d/dx_1, d/dx_2, second)
+// with the second-order stream along the per-coordinate symmetric quadratic form Q = sym(cotangent of Hm):
+//   a_3 = w c z_3 - w^2 s (q11 z_1^2 + 2 q12 z_1 z_2 + q22 z_2^2)          (q12x2 = 2 q12)
+__device__ __forceinline__ f32x4 jet_sin_q(const f32x4& z, float w, float ka, float kb, float kg, float q11,
+                                           float q12x2, float q22) {
+    f32x4 out;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float z0 = quad_bcast<0>(z[r]), t1 = quad_bcast<1>(z[r]), t2 = quad_bcast<2>(z[r]);
+        float sn, cs;
+        sincos_fast(w * z0, sn, cs);
+        const float q2 = __builtin_fmaf(t1, __builtin_fmaf(q11, t1, q12x2 * t2), (q22 * t2) * t2);
+        out[r] = __builtin_fmaf(ka, sn, __builtin_fmaf(kb * cs, z[r], -(kg * sn) * q2));
+    }
+    return out;
+}
+// its adjoint: zb_3 = w c u_3, zb_i = w c u_i - w^2 s (2 Q z)_i u_3 (qa, qb = this lane's row of 2 Q: stream 1 ->
+// (2 q11, 2 q12), stream 2 -> (2 q12, 2 q22)), zb_0 = w c u_0 - w^2 s (u_1 z_1 + u_2 z_2) - u_3 (w^2 s z_3 + w^3 c z^T Q z)
+__device__ __forceinline__ f32x4 jet_sin_adjoint_q(const f32x4& u, const f32x4& z, float w, float m0, float m12,
+                                                   float q11, float q12x2, float q22, float qa, float qb) {
+    f32x4 out;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float z0 = quad_bcast<0>(z[r]), z1 = quad_bcast<1>(z[r]), z2 = quad_bcast<2>(z[r]);
+        const float z3 = quad_bcast<3>(z[r]);
+        const float u1 = quad_bcast<1>(u[r]), u2 = quad_bcast<2>(u[r]), u3 = quad_bcast<3>(u[r]);
+        float sn, cs;
+        sincos_fast(w * z0, sn, cs);
+        const float wc = w * cs, w2s = w * w * sn;
+        const float t12 = w2s * (__builtin_fmaf(qa, z1, qb * z2) * u3);
+        const float q2 = __builtin_fmaf(z1, __builtin_fmaf(q11, z1, q12x2 * z2), (q22 * z2) * z2);
+        const float t0 = __builtin_fmaf(w2s, __builtin_fmaf(u1, z1, u2 * z2),
+                                        u3 * __builtin_fmaf(w2s, z3, (w * w * wc) * q2));
+        out[r] = __builtin_fmaf(wc, u[r], -__builtin_fmaf(m12, t12, m0 * t0));
+    }
+    return out;
+}
+
 __device__ __forceinline__ float sin_phase(float t) {
     float s, c;
     sincos_phase(t, s, c);

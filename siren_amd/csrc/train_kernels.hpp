@@ -209,7 +209,8 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
 //             dW0[:, k] = sum zb_0,value x_k + zb_0,tangent k, db0 = sum zb_0,value, dWout = sum glap a_L,second
 //   EDGE_MIX: the mixed jet (third-order adjoint, jet_kernel.hpp MIX): rows as EDGE_JET, scalars x, v (sc), g (sgy)
 //             (n, d) and u (su, (n, o), NULL = ones): dW0[:, k] = sum zb_0,value x_k + zb_0,v v_k + zb_0,g g_k,
-//             db0 = sum zb_0,value, dWout_j = sum u_j a_L,second, dbout = 0
+//             db0 = sum zb_0,value, dWout_j = sum u_j a_L,second, dbout = 0; sc / sgy == NULL: v = e_1 / g = e_2 (the
+//             QUAD jet of a Hessian node: tangents along the coordinate axes)
 //   EDGE_J2 : two-stream jet tiles (wide_jet_kernel.hpp: 16 columns = 8 coordinates x (value, tangent along v)),
 //             rows zb_0 jet, a_L jet; scalars x, v (sc), gy (sgy, nullable), u (su, NULL = ones):
 //             dW0[:, k] = sum zb_0,val x_k + zb_0,tan v_k, db0 = sum zb_0,val, dWout_j = sum gy_j a_L,val + u_j a_L,tan,
@@ -287,7 +288,12 @@ __global__ __launch_bounds__(edge_threads(KIND)) void edge_kernel(const float* _
 #pragma unroll
                 for (int k = 0; k < MAXD; ++k) scal[e][k] = (ok && k < d) ? x[cd * d + k] : 0.f;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) scal[e][4 + j] = (ok && j < ns) ? sc[cd * ns + j] : 0.f;
+                for (int j = 0; j < 4; ++j) {
+                    if (KIND == EDGE_MIX && sc == nullptr)  // QUAD (Hessian node): v = e_1 for every coordinate
+                        scal[e][4 + j] = (ok && j == 0) ? 1.f : 0.f;
+                    else
+                        scal[e][4 + j] = (ok && j < ns) ? sc[cd * ns + j] : 0.f;
+                }
                 if constexpr (KIND == EDGE_W3) {
 #pragma unroll
                     for (int j = 0; j < MAXO; ++j) {
@@ -302,7 +308,8 @@ __global__ __launch_bounds__(edge_threads(KIND)) void edge_kernel(const float* _
                     }
                 } else if constexpr (KIND == EDGE_MIX) {
 #pragma unroll
-                    for (int k = 0; k < MAXD; ++k) scal[e][8 + k] = (ok && k < d) ? sgy[cd * d + k] : 0.f;
+                    for (int k = 0; k < MAXD; ++k)  // QUAD: g = e_2 (d = 2) when sgy == nullptr
+                        scal[e][8 + k] = (ok && k < d) ? (sgy != nullptr ? sgy[cd * d + k] : (k == 1 ? 1.f : 0.f)) : 0.f;
 #pragma unroll
                     for (int j = 0; j < MAXO; ++j)
                         scal[e][12 + j] = (ok && j < o) ? (su != nullptr ? su[cd * o + j] : 1.f) : 0.f;

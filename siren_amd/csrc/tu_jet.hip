@@ -34,4 +34,12 @@ void launch_jet_mix(dim3 grid, hipStream_t st, const float* ws, const float* x, 
                        w, spill, abuf, dbuf, n_pad, NUL, NUL, v, g, u, gv, gu);
 }
 
+// backward of a Hessian node (QG: quadratic form G (n, d, d) per coordinate, tangents the coordinate axes, d <= 2)
+void launch_jet_quad(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* G,
+                     const float* u, float* gx, float* gu, int d, int o, int lh, float w0, float w, float* spill,
+                     float* abuf, float* dbuf, int64_t n_pad) {
+    hipLaunchKernelGGL((jet_store_kernel<JET_BOTH, true, true>), grid, dim3(THREADS), 0, st, ws, x, n, NOF, gx, d, o,
+                       lh, w0, w, spill, abuf, dbuf, n_pad, NUL, NUL, NOF, NOF, u, NUL, gu, G);
+}
+
 }  // namespace siren

@@ -230,6 +230,51 @@ class SirenEngine:
                    'siren_hvp_backward')
         return gx, gp, gv, gu
 
+    @property
+    def hessian_backward_supported(self):
+        """siren_hessian_backward covers this network: hidden 256, 1..5 hidden layers, d_in <= 2, linear output."""
+        c = self.cfg
+        return (self.supported and c.hidden == 256 and 1 <= c.n_hidden <= 5 and c.d_in <= 2
+                and bool(c.outermost_linear))
+
+    def hessian(self, ws, x, u=None):
+        """Hm (n, d_in, d_in) = sum_j u_j H_j(x) (u (n, d_out), None = ones): column i = the x-part of the W3 sweep
+        along e_i (second_order with want_theta=False), one launch per input dimension."""
+        n, d = x.shape[0], self.cfg.d_in
+        hm = torch.empty(n, d, d, dtype=torch.float32, device=x.device)
+        for i in range(d):
+            v = torch.zeros(n, d, dtype=torch.float32, device=x.device)
+            v[:, i] = 1.
+            hm[:, :, i] = self.second_order(ws, x, v, want_theta=False, u=u)[0]
+        return hm
+
+    def hessian_backward(self, ws, x, G, u=None, want_theta=True, want_u=False):
+        """The backward of the Hessian node: d/d(x, theta, u) of sum_c <G_c, Hm_c> (siren_hessian_backward).
+        Returns (gx, gparams | None, gu | None)."""
+        self._require()
+        if not self.hessian_backward_supported:
+            raise _lib.SirenUnsupported('siren_hessian_backward covers hidden 256, 1..5 hidden layers, in_features '
+                                        '<= 2, linear output')
+        x = self._check_x(x)
+        n, d, o = x.shape[0], self.cfg.d_in, self.cfg.d_out
+        if G.numel() != n * d * d or G.dtype != torch.float32 or G.device != x.device:
+            raise ValueError('G must be fp32 (%d, %d, %d) on %s' % (n, d, d, x.device))
+        if u is not None and (u.numel() != n * o or u.dtype != torch.float32 or u.device != x.device):
+            raise ValueError('u must be fp32 (%d, %d) on %s' % (n, o, x.device))
+        G = G.contiguous()
+        u = u.contiguous() if u is not None else None
+        cnt = ctypes.c_int64()
+        _lib.check(self.lib.siren_hessian_backward_ws_floats(ctypes.byref(self.cfg), n, ctypes.byref(cnt)),
+                   'siren_hessian_backward_ws_floats')
+        tws = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
+        gx = torch.empty(n, d, dtype=torch.float32, device=x.device)
+        gp = torch.empty(self.param_count, dtype=torch.float32, device=x.device) if want_theta else None
+        gu = torch.empty(n, o, dtype=torch.float32, device=x.device) if want_u else None
+        _lib.check(self.lib.siren_hessian_backward(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(G), _ptr(u),
+                                                   _ptr(tws), _ptr(gx), _ptr(gp), _ptr(gu), _stream(x.device)),
+                   'siren_hessian_backward')
+        return gx, gp, gu
+
     def forward_laplace(self, ws, x, want_y=False, want_gx=False):
         """W4 in one launch: (y | None, sum_j grad y_j | None, sum_j Laplacian y_j (n, 1)) — what
         diff_operators.gradient / laplace return (diff_operators.py:27-43)."""
