@@ -92,6 +92,25 @@ def hvp_vjp(cfg, x, flat, v, g, create_graph, u=None):
     return rx, rp, rv, ru
 
 
+def hessian_vjp(cfg, x, flat, G, create_graph, u=None):
+    """d/d(x, theta, u) of <G, Hm>, Hm[c, :, i] = sum_j u_j H_j(x_c) e_i (u (n, d_out), None = ones)."""
+    with torch.enable_grad():
+        ur = None
+        if u is not None:
+            ur = u if u.requires_grad else u.detach().requires_grad_(True)
+        y = forward(cfg, x, flat)
+        J = torch.autograd.grad(y, x, torch.ones_like(y) if ur is None else ur, create_graph=True)[0]
+        S = 0.
+        for i in range(x.shape[-1]):
+            e = torch.zeros_like(J)
+            e[:, i] = 1.
+            S = S + (torch.autograd.grad(J, x, e, create_graph=True)[0] * G[:, :, i]).sum()
+        rx, rp, ru = _grads(S, [x, flat, ur], None, create_graph)
+    if u is None or not u.requires_grad:
+        ru = None
+    return rx, rp, ru
+
+
 def laplacian(cfg, x, flat):
     """sum_j sum_i d2 Phi_j / dx_i2 as a differentiable graph (diff_operators.laplace's op sequence)."""
     y = forward(cfg, x, flat)

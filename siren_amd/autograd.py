@@ -164,7 +164,10 @@ class SirenJetFunction(torch.autograd.Function):
         if need_x:
             gx = gy * J if gy is not None else None
             if gJ is not None:
-                if engine.second_order_supported:
+                h = _hessian_product(ctx, engine, ws, x, flat, gJ)
+                if h is not None:
+                    pass
+                elif engine.second_order_supported:
                     h = SirenHVP.apply(engine, ws, x, flat, gJ)
                 else:
                     h, _ = _torch_path.jacobian_vjp(engine.cfg, x, flat, gJ, create_graph=True)
@@ -212,6 +215,51 @@ class SirenHVP(torch.autograd.Function):
         return None, None, rx, rp, rv, ru
 
 
+class SirenHessian(torch.autograd.Function):
+    """Hm (n, d, d), Hm[c, :, i] = sum_j u_j H_j(x_c) e_i (u (n, d_out), None = ones) as ONE graph node per gradient
+    node. Every create_graph x-derivative of that gradient node — each divergence() term of the reference's
+    laplace = divergence(gradient()) (diff_operators.py:27-36), each hessian() column (:5-24) — is the cheap torch
+    product Hm v, so autograd SUMS all their cotangents into one G (n, d, d) and calls this backward ONCE: one
+    quadratic-form jet sweep + one MFMA wgrad (siren_hessian_backward) for the whole third-order term, where one
+    SirenHVP node per dimension cost d mixed-jet sweeps and d wgrads. Forward: the W3 x-part along each axis."""
+
+    @staticmethod
+    def forward(ctx, engine, ws, x, flat, u=None):
+        hm = engine.hessian(ws, x, u)
+        ctx.engine, ctx.ws = engine, ws
+        ctx.save_for_backward(x, flat, u)
+        return hm
+
+    @staticmethod
+    def backward(ctx, G):
+        x, flat, u = ctx.saved_tensors
+        eng = ctx.engine
+        # tensor inputs in order: ws (0), x (1), flat (2), u (3, when given)
+        need_x = ctx.needs_input_grad[2] and _will_execute(ctx, 1)
+        need_p = ctx.needs_input_grad[3] and _will_execute(ctx, 2)
+        need_u = u is not None and ctx.needs_input_grad[4] and _will_execute(ctx, 3)
+        if not (need_x or need_p or need_u):
+            return None, None, None, None, None
+        if not torch.is_grad_enabled():
+            gx, gp, gu = eng.hessian_backward(ctx.ws, x, G.contiguous(), u, want_theta=need_p, want_u=need_u)
+            return None, None, (gx if need_x else None), gp, gu
+        rx, rp, ru = _torch_path.hessian_vjp(eng.cfg, x, flat, G, create_graph=True, u=u)
+        return None, None, rx, rp, ru
+
+
+def _hessian_product(ctx, engine, ws, x, flat, v, u=None):
+    """sum_j u_j H_j v through the gradient node's shared SirenHessian node (built on the first request, kept on the
+    gradient node's ctx: later requests of the same node reuse it), or None when the kernels do not cover it."""
+    if not (engine.hessian_backward_supported and engine.second_order_supported):
+        return None
+    hm = getattr(ctx, 'hessian_node', None)
+    if hm is None:
+        hm = SirenHessian.apply(engine, ws, x, flat, u)
+        ctx.hessian_node = hm
+    # elementwise (n, d, d) products: a batched GEMM of n 2x2 matrices runs ~100x slower on the BLAS path
+    return (hm * v.unsqueeze(-2)).sum(-1)
+
+
 class SirenVJP(torch.autograd.Function):
     """gx = J^T gy = sum_j gy_j dPhi_j/dx as a graph node; forward is the fused W1 kernel. Its backward is the W3
     kernel with output weighting u = gy and v = ggx (siren_second_order_ex), which also returns ggy = J ggx in the
@@ -240,7 +288,10 @@ class SirenVJP(torch.autograd.Function):
             gx, gp, ggy = _torch_path.vjp_vjp(eng.cfg, x, flat, gy, ggx, create_graph=torch.is_grad_enabled())
             return None, None, gx, gp, ggy
         if torch.is_grad_enabled():  # x only, differentiable
-            return None, None, SirenHVP.apply(eng, ctx.ws, x, flat, ggx, gy), None, None
+            h = _hessian_product(ctx, eng, ctx.ws, x, flat, ggx, gy)
+            if h is None:
+                h = SirenHVP.apply(eng, ctx.ws, x, flat, ggx, gy)
+            return None, None, h, None, None
         res = eng.second_order(ctx.ws, x, ggx, want_theta=need_p, u=gy, want_ydot=need_gy)
         gx, gp = res[0], res[1]
         ggy = res[2] if need_gy else None

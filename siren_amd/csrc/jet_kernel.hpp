@@ -120,19 +120,17 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
     const float m12 = (js == 1 || js == 2) ? 1.f : 0.f;
     const float gl = (PHASE != JET_FWD && valid && js == 3) ? (MIX ? 1.f : glap[coord]) : 0.f;
     const bool s1 = js == 1;
-    // QG: this coordinate's quadratic form Q = sym(G) (G (n, d, d), d <= 2; rows / columns beyond d are zero)
-    float q11 = 0.f, q12x2 = 0.f, q22 = 0.f;
+    // QG: this lane's row of 2 Q (streams 1, 2; Q = sym(G), G (n, d, d), d <= 2) for jet_sin_q / jet_sin_adjoint_q
+    f32x2 qreg = {0.f, 0.f};
     if constexpr (QG) {
-        if (valid) {
+        if (valid && (js == 1 || js == 2)) {
             const float* gq = tq + coord * d * d;
-            q11 = gq[0];
-            if (d > 1) {
-                q12x2 = gq[1] + gq[2];
-                q22 = gq[3];
-            }
+            const float q12x2 = d > 1 ? gq[1] + gq[2] : 0.f;
+            qreg[0] = js == 1 ? 2.f * gq[0] : q12x2;
+            qreg[1] = js == 1 ? q12x2 : (d > 1 ? 2.f * gq[3] : 0.f);
         }
     }
-    const float qa = s1 ? 2.f * q11 : q12x2, qb = s1 ? q12x2 : 2.f * q22;  // this lane's row of 2 Q (streams 1, 2)
+    auto qload = [&]() -> f32x2 { return qreg; };
     __syncthreads();
     const int p0 = PHASE == JET_REV ? lh : 0, p1 = PHASE == JET_FWD ? lh : 2 * lh;
     int s = p0 * NB;
@@ -152,6 +150,7 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
         jstore_tile(dbuf + (int64_t)lh * lstride + toff, act);
     } else {
         LaneBlocks zs{sp};
+        const f32x2 qc = qload();
 #pragma unroll
         for (int rb = 0; rb < NB; ++rb) {
             const int nb = 16 * rb + 4 * g;
@@ -159,8 +158,14 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
 #pragma unroll
             for (int k = 0; k < MAXD; ++k)
                 if (k < d) z += jcf[k] * *(const f32x4*)(sm + SM_W0 + k * H + nb);
-            zs.next_store(z);
-            act[rb] = QG ? jet_sin_q(z, w0, val, kb0, kg0, q11, q12x2, q22) : jet_sin<MIX>(z, w0, val, kb0, kg0);
+            if constexpr (QG) {
+                f32x4 kz;
+                act[rb] = jet_sin_q(z, w0, val, kb0, kg0, qc[0], qc[1], js == 3, kz);
+                zs.next_store(kz);
+            } else {
+                zs.next_store(z);
+                act[rb] = jet_sin<MIX>(z, w0, val, kb0, kg0);
+            }
         }
         jstore_tile(abuf + toff, act);
     }
@@ -182,11 +187,18 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
             const float* bl = sm + SM_BIAS + l * H + 4 * g;
             float* zp = sp + (int64_t)l * lstride;
             LaneBlocks zs{zp};
+            const f32x2 qc = qload();
 #pragma unroll
             for (int rb = 0; rb < NB; ++rb) {
                 const f32x4 z = acc[rb] + val * *(const f32x4*)(bl + 16 * rb);
-                zs.next_store(z);
-                act[rb] = QG ? jet_sin_q(z, w, val, kb, kg, q11, q12x2, q22) : jet_sin<MIX>(z, w, val, kb, kg);
+                if constexpr (QG) {
+                    f32x4 kz;
+                    act[rb] = jet_sin_q(z, w, val, kb, kg, qc[0], qc[1], js == 3, kz);
+                    zs.next_store(kz);
+                } else {
+                    zs.next_store(z);
+                    act[rb] = jet_sin<MIX>(z, w, val, kb, kg);
+                }
             }
             jstore_tile(abuf + (int64_t)l * lstride + toff, act);
             if (PHASE == JET_FWD && l == lh) {
@@ -234,6 +246,7 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
                 // seed: u_L (cotangent of the a_L jet) = (sum_j Wout_j) glap on the second-order stream only
                 // (MIX: sum_j u_j Wout_j), then zb_L = adjoint of the last sine layer
                 LaneBlocks zl{zp};
+                const f32x2 qc = qload();
                 float uw[MAXO];  // MIX: this coordinate's output weighting (the seed is sum_j u_j Wout_j)
 #pragma unroll
                 for (int j = 0; j < MAXO; ++j)
@@ -248,7 +261,7 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
                     } else {
                         sd = *(const f32x4*)(sm + SM_SEED + 16 * rb + 4 * g);
                     }
-                    act[rb] = QG ? jet_sin_adjoint_q(gl * sd, zl.next_load(), w, val, m12, q11, q12x2, q22, qa, qb)
+                    act[rb] = QG ? jet_sin_adjoint_q(gl * sd, zl.next_load(), w, val, m12, qc[0], qc[1])
                                  : jet_sin_adjoint<MIX>(gl * sd, zl.next_load(), w, val, m12, s1);
                 }
                 jstore_tile(dbuf + (int64_t)lh * lstride + toff, act);
@@ -258,9 +271,10 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
             const int lm = 2 * lh - p - 1;
             LaneBlocks zl{sp + (int64_t)lm * lstride};
             const float wl = lm == 0 ? w0 : w;
+            const f32x2 qc = qload();
 #pragma unroll
             for (int rb = 0; rb < NB; ++rb) {
-                act[rb] = QG ? jet_sin_adjoint_q(acc[rb], zl.next_load(), wl, val, m12, q11, q12x2, q22, qa, qb)
+                act[rb] = QG ? jet_sin_adjoint_q(acc[rb], zl.next_load(), wl, val, m12, qc[0], qc[1])
                              : jet_sin_adjoint<MIX>(acc[rb], zl.next_load(), wl, val, m12, s1);
             }
             jstore_tile(dbuf + (int64_t)lm * lstride + toff, act);

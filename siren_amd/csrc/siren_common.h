@@ -6,6 +6,7 @@
 namespace siren {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // ---------------------------------------------------------------------------------------------------------
 // Geometry of the fused H=256 kernels.
@@ -215,38 +216,42 @@ __device__ __forceinline__ f32x4 jet_sin_adjoint(const f32x4& u, const f32x4& z,
 }
 
 // QUAD (the backward of a Hessian node, Hm = sum_j u_j H_j (n, d, d), d <= 2): streams (value, d/dx_1, d/dx_2, second)
-// with the second-order stream along the per-coordinate symmetric quadratic form Q = sym(cotangent of Hm):
-//   a_3 = w c z_3 - w^2 s (q11 z_1^2 + 2 q12 z_1 z_2 + q22 z_2^2)          (q12x2 = 2 q12)
-__device__ __forceinline__ f32x4 jet_sin_q(const f32x4& z, float w, float ka, float kb, float kg, float q11,
-                                           float q12x2, float q22) {
+// with the second-order stream along the per-coordinate symmetric quadratic form Q = sym(cotangent of Hm). Lanes of
+// streams 1 and 2 hold their row of 2 Q as (c1, c2): lin = c1 z1 + c2 z2 = (2 Q z)_i there, and the form comes from
+// those two lanes, z^T Q z = (z1 lin_1 + z2 lin_2) / 2.
+// forward (stream 3): a_3 = w c z_3 - w^2 s z^T Q z. The reverse needs z_3 and z^T Q z only in the combination
+// K = w^2 s z_3 + w^3 c z^T Q z (zb_0's last term), so the stream-3 lane stores K in the z-jet scratch instead of z_3
+// (kz): the reverse epilogue then computes no quadratic form (it sits at the 2-waves-per-SIMD register budget).
+__device__ __forceinline__ f32x4 jet_sin_q(const f32x4& z, float w, float ka, float kb, float kg, float c1, float c2,
+                                           bool s3, f32x4& kz) {
     f32x4 out;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const float z0 = quad_bcast<0>(z[r]), t1 = quad_bcast<1>(z[r]), t2 = quad_bcast<2>(z[r]);
+        const float lin = __builtin_fmaf(c1, t1, c2 * t2);
+        const float q2 = 0.5f * __builtin_fmaf(t1, quad_bcast<1>(lin), t2 * quad_bcast<2>(lin));
         float sn, cs;
         sincos_fast(w * z0, sn, cs);
-        const float q2 = __builtin_fmaf(t1, __builtin_fmaf(q11, t1, q12x2 * t2), (q22 * t2) * t2);
         out[r] = __builtin_fmaf(ka, sn, __builtin_fmaf(kb * cs, z[r], -(kg * sn) * q2));
+        kz[r] = s3 ? __builtin_fmaf(kg * sn, z[r], (kg * w * cs) * q2) : z[r];
     }
     return out;
 }
-// its adjoint: zb_3 = w c u_3, zb_i = w c u_i - w^2 s (2 Q z)_i u_3 (qa, qb = this lane's row of 2 Q: stream 1 ->
-// (2 q11, 2 q12), stream 2 -> (2 q12, 2 q22)), zb_0 = w c u_0 - w^2 s (u_1 z_1 + u_2 z_2) - u_3 (w^2 s z_3 + w^3 c z^T Q z)
+// its adjoint (z = the stored jet, stream 3 holding K): zb_3 = w c u_3, zb_i = w c u_i - w^2 s (2 Q z)_i u_3,
+// zb_0 = w c u_0 - w^2 s (u_1 z_1 + u_2 z_2) - u_3 K
 __device__ __forceinline__ f32x4 jet_sin_adjoint_q(const f32x4& u, const f32x4& z, float w, float m0, float m12,
-                                                   float q11, float q12x2, float q22, float qa, float qb) {
+                                                   float c1, float c2) {
     f32x4 out;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const float z0 = quad_bcast<0>(z[r]), z1 = quad_bcast<1>(z[r]), z2 = quad_bcast<2>(z[r]);
-        const float z3 = quad_bcast<3>(z[r]);
+        const float K = quad_bcast<3>(z[r]);
         const float u1 = quad_bcast<1>(u[r]), u2 = quad_bcast<2>(u[r]), u3 = quad_bcast<3>(u[r]);
         float sn, cs;
         sincos_fast(w * z0, sn, cs);
         const float wc = w * cs, w2s = w * w * sn;
-        const float t12 = w2s * (__builtin_fmaf(qa, z1, qb * z2) * u3);
-        const float q2 = __builtin_fmaf(z1, __builtin_fmaf(q11, z1, q12x2 * z2), (q22 * z2) * z2);
-        const float t0 = __builtin_fmaf(w2s, __builtin_fmaf(u1, z1, u2 * z2),
-                                        u3 * __builtin_fmaf(w2s, z3, (w * w * wc) * q2));
+        const float t12 = w2s * (__builtin_fmaf(c1, z1, c2 * z2) * u3);
+        const float t0 = __builtin_fmaf(w2s, __builtin_fmaf(u1, z1, u2 * z2), u3 * K);
         out[r] = __builtin_fmaf(wc, u[r], -__builtin_fmaf(m12, t12, m0 * t0));
     }
     return out;

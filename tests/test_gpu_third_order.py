@@ -227,3 +227,87 @@ def test_reference_recipe_laplace_mse_hidden512_on_kernels(cuda, monkeypatch):
         for (k, p), r in zip(m.named_parameters(), ref):
             r = r.numpy()
             assert np.max(np.abs(p.grad.cpu().numpy() - r)) <= 1e-4 * np.max(np.abs(r)) + 1e-12, k
+
+
+def hessian_vjp_ref(x, layers, G, u):
+    """fp64 autograd of S = sum_c <G_c, Hm_c>, Hm[c, :, i] = sum_j u_j H_j(x_c) e_i: dS/dx, dS/dtheta, dS/du."""
+    xt = torch.tensor(x, dtype=torch.float64, requires_grad=True)
+    params = [torch.tensor(t, dtype=torch.float64, requires_grad=True) for W, b in layers for t in (W, b)]
+    y = O.torch_forward(xt, params)
+    ut = (torch.ones_like(y) if u is None else torch.tensor(u, dtype=torch.float64)).requires_grad_(True)
+    Ju = torch.autograd.grad(y, xt, ut, create_graph=True)[0]
+    Gt = torch.tensor(G, dtype=torch.float64)
+    S = 0.
+    for i in range(x.shape[1]):
+        e = torch.zeros_like(Ju)
+        e[:, i] = 1.
+        S = S + (torch.autograd.grad(Ju, xt, e, create_graph=True)[0] * Gt[:, :, i]).sum()
+    grads = torch.autograd.grad(S, [xt, ut] + params, allow_unused=True)
+    gp = torch.cat([(torch.zeros_like(p) if gg is None else gg).reshape(-1) for gg, p in zip(grads[2:], params)])
+    return grads[0].numpy(), gp.numpy(), grads[1].numpy()
+
+
+@pytest.mark.parametrize('n,d,L,o,weighted', [(1, 2, 3, 1, False), (15, 2, 3, 1, False), (4097, 2, 3, 1, False),
+                                               (333, 1, 2, 3, True), (700, 2, 1, 2, True), (2048, 2, 3, 2, True),
+                                               (300, 1, 5, 1, False), (65, 2, 4, 4, True), (1000, 2, 5, 1, True)])
+def test_hessian_backward_vs_fp64(cuda, n, d, L, o, weighted):
+    """siren_hessian_backward (the quadratic-form jet: one sweep for the whole Hessian node's cotangent G, any
+    non-symmetric G, optional output weighting u) against fp64 autograd; and the node's forward (the Hessian)."""
+    from siren_amd.engine import SirenEngine
+    layers = random_layers(d, L, o, seed=5 * n + L + o)
+    eng = SirenEngine(d, 256, L, o)
+    assert eng.hessian_backward_supported
+    ws = eng.pack(to_dev(O.flatten(layers), cuda))
+    rng = np.random.default_rng(n + 3 * d)
+    x = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    G = (rng.normal(size=(n, d, d)) / n).astype(np.float32)
+    u = rng.normal(size=(n, o)).astype(np.float32) if weighted else None
+    ud = to_dev(u, cuda) if weighted else None
+    gx, gp, gu = eng.hessian_backward(ws, to_dev(x, cuda), to_dev(G, cuda), ud, want_theta=True, want_u=True)
+    rgx, rgp, rgu = hessian_vjp_ref(x, layers, G, u)
+    assert np.max(np.abs(gp.cpu().numpy() - rgp)) <= 1e-4 * np.max(np.abs(rgp))
+    assert np.max(np.abs(gx.cpu().numpy() - rgx)) <= 1e-4 * max(1e-6, np.max(np.abs(rgx)))
+    assert np.max(np.abs(gu.cpu().numpy() - rgu)) <= 1e-4 * max(1e-6, np.max(np.abs(rgu)))
+    gx2, none_p, none_u = eng.hessian_backward(ws, to_dev(x, cuda), to_dev(G, cuda), ud, want_theta=False)
+    assert none_p is None and none_u is None and torch.equal(gx, gx2)
+    if not eng.second_order_supported:  # the node's forward runs on the W3 kernel (1..3 hidden layers)
+        return
+    # the node's forward: Hm[:, :, i] = sum_j u_j H_j e_i
+    hm = eng.hessian(ws, to_dev(x, cuda), ud).cpu().numpy()
+    xt = torch.tensor(x, dtype=torch.float64, requires_grad=True)
+    params = [torch.tensor(t, dtype=torch.float64) for W, b in layers for t in (W, b)]
+    y = O.torch_forward(xt, params)
+    Ju = torch.autograd.grad(y, xt, torch.ones_like(y) if u is None else torch.tensor(u, dtype=torch.float64),
+                             create_graph=True)[0]
+    for i in range(d):
+        e = torch.zeros_like(Ju)
+        e[:, i] = 1.
+        ref = torch.autograd.grad(Ju, xt, e, retain_graph=True)[0].numpy()
+        assert np.max(np.abs(hm[:, :, i] - ref)) <= 1e-4 * max(1., np.max(np.abs(ref)))
+
+
+def test_reference_recipe_runs_one_hessian_backward(cuda, monkeypatch):
+    """The reference's divergence(gradient()) records d Hessian products of ONE shared SirenHessian node, so the
+    backward runs siren_hessian_backward once per step (not d mixed-jet sweeps)."""
+    from siren_amd.engine import SirenEngine
+    from siren_amd.modules import SingleBVPNet
+    calls = {'hess': 0, 'hvp': 0}
+    orig_h, orig_v = SirenEngine.hessian_backward, SirenEngine.hvp_backward
+
+    def hess(self, *a, **k):
+        calls['hess'] += 1
+        return orig_h(self, *a, **k)
+
+    def hvp(self, *a, **k):
+        calls['hvp'] += 1
+        return orig_v(self, *a, **k)
+    monkeypatch.setattr(SirenEngine, 'hessian_backward', hess)
+    monkeypatch.setattr(SirenEngine, 'hvp_backward', hvp)
+    torch.manual_seed(0)
+    m = SingleBVPNet(verbose=False).to(cuda)
+    coords = (torch.rand(1, 1000, 2) * 2 - 1).to(cuda)
+    for step in range(2):  # SirenVJP nodes, then jet mode (SirenJetFunction)
+        out = m({'coords': coords})
+        loss = torch.mean(reference_laplace(out['model_out'], out['model_in']) ** 2)
+        loss.backward()
+        assert calls == {'hess': step + 1, 'hvp': 0}

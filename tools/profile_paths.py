@@ -8,8 +8,8 @@ Paths (BASELINE.json configs; F = 2 sum fan_in fan_out FLOP per coordinate, SURV
   sdf          5x256 d3 o1, 2^19 coords: forward_grad_store + seeded W3 from the kept forward (sdf kernels, 8F)
   video        5x512 d3 o3, 2^20 coords: forward_store + backward_stored (hidden 512 W2 = 3F)
   poisson      5x256 d2 o1, 512^2 grid: forward_laplace_store + laplace_backward_stored (W4s = 3 (1 + 2d) F = 15F)
-  poisson_ref  5x256 d2 o1, 512^2 grid: the reference recipe's kernels: W1 (J), d x W3 (H e_i), d x mixed jet
-               (third-order adjoint); the same loss gradient as poisson (15F counted)
+  poisson_ref  5x256 d2 o1, 512^2 grid: the reference recipe's kernels: W1 (J), d x W3 (the shared Hessian node's
+               columns H e_i), ONE quadratic-form jet (its backward); the same loss gradient as poisson (15F counted)
   w3_theta     5x256 d2 o1, 2^19 coords: W3 H v + theta-grads without a kept forward (6F)
   hypernet     32 x 4096 coords, 5x256 d2 o1 per-element weights: grouped stored forward + grouped reverse-only W2
                (the hypernetwork training kernels, W2 = 3F)
@@ -125,15 +125,12 @@ def build_step(name, dev):
             e[:, i] = 1.
             es.append(e)
 
+        G = torch.diag_embed(gl.expand(n, d))  # the summed cotangent of the shared Hessian node: glap * I
+
         def step():
             eng.forward_grad(ws, x)
-            gx = 0.
-            for i in range(d):
-                eng.second_order(ws, x, es[i], want_theta=False)  # the divergence's H e_i nodes (forward)
-            for i in range(d):
-                r = eng.hvp_backward(ws, x, es[i], gl * es[i])      # their backward (third order)
-                gx = gx + r[1]
-            return gx
+            eng.hessian(ws, x)                      # the shared Hessian node (forward): H e_i per dimension
+            return eng.hessian_backward(ws, x, G)   # its ONE backward (third order): the quadratic-form jet
         return step
     raise ValueError(name)
 
