@@ -1296,6 +1296,8 @@ int32_t siren_forward_store_batched(const siren_cfg* cfg, const float* ws, const
         float* cbuf = tws + 2 * batch * plan.act_floats + batch * plan.partial_floats;
         siren::FusedArgs fa{w1_ws(cfg, ws), x, n, nullptr, y, nullptr, d, o, cfg->n_hidden, cfg->omega_first,
                             cfg->omega_hidden, 0, abuf, cbuf, plan.n_pad, W};
+        // one workgroup per tile (a persistent grid of ~2 workgroups per CU measured 1 % slower at 32 x 4096,
+        // tools/profile_paths.py hypernet vs hypernet_np)
         siren::launch_w0s(dim3((unsigned)(plan.n_pad / siren::TILE), (unsigned)batch), (hipStream_t)stream, fa);
         return hip_status("siren_forward_store_batched (grouped)");
     }

@@ -263,6 +263,24 @@ __device__ __forceinline__ float sin_phase(float t) {
     return s;
 }
 
+// Grouped launches over batched weights (grid.y = element): the hardware deals blocks round-robin over the 8 XCDs
+// (blocks b and b + 8 share one; MI355X_MICROARCH.md, workgroup dispatch — observed placement, used for speed only),
+// so the linear block id is renumbered XCD-major: the blocks of one XCD take consecutive (element, x) slots, an XCD
+// works through its elements one or two at a time, and its 4 MiB L2 holds those elements' weight streams instead of
+// a slice of every element's. Identity when the grid is not a multiple of 8 blocks.
+__device__ __forceinline__ void xcd_remap(unsigned& bx, unsigned& by) {
+    const unsigned gx = gridDim.x, total = gridDim.x * gridDim.y;
+    if (total % 8u != 0u) {
+        bx = blockIdx.x;
+        by = blockIdx.y;
+        return;
+    }
+    const unsigned L = blockIdx.x + blockIdx.y * gx;
+    const unsigned q = (L % 8u) * (total / 8u) + L / 8u;
+    by = q / gx;
+    bx = q % gx;
+}
+
 // Sum over the 4 lane groups g (lanes c, c+16, c+32, c+48 hold partial sums of one coordinate).
 __device__ __forceinline__ float sum_groups(float v) {
     v += __shfl_xor(v, 16);

@@ -57,9 +57,28 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
                                                           int64_t bstride_part = 0) {
     __shared__ __attribute__((aligned(16))) float ring[WG_NBUF * WG_SLOT];
     const ParamOffsets off(d, o, lh, h);
-    const int s = blockIdx.x, l = blockIdx.y + 1;
-    // grid.z = batch element x (h/256)^2 quadrants (grouped W2 over batched weights: per-element tiles / slabs)
-    const int qn = h / 256, qz = blockIdx.z % (qn * qn), bz = blockIdx.z / (qn * qn);
+    // grid (S, LH, batch x (h/256)^2 quadrants; grouped W2 over batched weights: per-element tiles / slabs)
+    const int qn = h / 256, nq = qn * qn;
+    int s = blockIdx.x, ly = blockIdx.y, zz = blockIdx.z;
+    if (nq > 1) {
+        // the quadrants (qr, qc) of one (split, layer) read the same delta half qr / activation half qc: the blocks are
+        // renumbered so that those nq blocks are consecutive slots of ONE XCD (blocks are dealt round-robin over the 8
+        // XCDs; MI355X_MICROARCH.md) and run together, so each half comes from HBM once and is re-read from that
+        // XCD's L2 (the quadrant-major grid re-read every half from HBM: traffic 2x the tiles)
+        const unsigned total = gridDim.x * gridDim.y * gridDim.z;
+        if (total % 8u == 0u) {
+            const unsigned L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+            unsigned q = (L % 8u) * (total / 8u) + L / 8u;
+            const unsigned quad = q % (unsigned)nq;
+            q /= (unsigned)nq;
+            s = (int)(q % gridDim.x);
+            q /= gridDim.x;
+            ly = (int)(q % gridDim.y);
+            zz = (int)((q / gridDim.y) * nq + quad);
+        }
+    }
+    const int l = ly + 1;
+    const int qz = zz % nq, bz = zz / nq;
     const int qr = qz / qn, qc = qz % qn;
     abuf += bz * bstride_act;
     dbuf += bz * bstride_act;

@@ -421,8 +421,14 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
     }
     cx.d = d;
     cx.o = o;
-    if (ws_bstride != 0) {  // grouped launch over batched (hypernetwork) weights: blockIdx.y = batch element
-        const int64_t b = blockIdx.y;
+    // grouped launch over batched (hypernetwork) weights: block (x, element), renumbered XCD-major (xcd_remap) so each
+    // XCD's 4 MiB L2 streams one or two elements' weights at a time instead of a slice of every element's
+    int64_t bx = blockIdx.x;
+    if (ws_bstride != 0) {
+        unsigned rx, ry;
+        xcd_remap(rx, ry);
+        bx = rx;
+        const int64_t b = ry;
         ws += b * ws_bstride;
         x += b * n * d;
         if (y != nullptr) y += b * n * o;
@@ -471,7 +477,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
 #pragma unroll
         for (int j = 0; j < MAXO; ++j) gn[j] = (gy != nullptr && ok && j < o) ? gy[cd * o + j] : 0.f;
     };
-    load_inputs(blockIdx.x);
+    load_inputs(bx);
     if constexpr (JET) {
         // jet coefficients on phase-scaled jets: w / s = 2 pi for every layer (jet_sin_rev)
         const float val = js == 0 ? 1.f : 0.f;
@@ -494,7 +500,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
     // ---- coordinate tiles: a persistent grid walks tile = blockIdx.x, + gridDim.x, ... (a one-tile-per-
     // workgroup grid runs the loop once); the weight ring streams on across tile boundaries ----------------------
 #pragma unroll 1
-    for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    for (int64_t tile = bx; tile < tiles; tile += gridDim.x) {
         cx.more = tile + gridDim.x < tiles;
         const int64_t coord = coord_of(tile);
         const bool valid = coord < n;
@@ -525,7 +531,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
         }
 
         if constexpr ((MODE & MODE_PROF) != 0) {
-            const int64_t it = (tile - blockIdx.x) / gridDim.x;
+            const int64_t it = (tile - bx) / gridDim.x;
             cx.prof = (blockIdx.x < PROF_BLOCKS && it < PROF_TILES)
                           ? (unsigned long long*)abuf + ((blockIdx.x * PROF_TILES + it) * WAVES + cx.wave) * PROF_EVENTS
                           : nullptr;

@@ -72,10 +72,12 @@ def io_bytes(path, k):
         return {'lay_first_kernel': 2 * tile + C * d * 4, 'lay_sine_kernel': 3 * tile,
                 'lay_last_kernel': 3 * tile + C * o * 4, 'lay_rev_kernel<0>': 3 * tile,
                 'lay_rev_kernel<1>': 3 * tile + C * o * 4, 'lay_rev_kernel<2>': 3 * tile + C * d * 4}.get(k)
+    # (hypernet: n_pad is one element's, n the whole batch; every element's weight stream is read once)
+    stream = B * (2 * L * H * H * 4) if path == 'hypernet' else 0
     if re.match(r'w1_kernel<\d+,4>', k) or (k.startswith('wide_kernel<4') and path == 'video'):
-        return 2 * (L + 1) * n_pad * T + n * (d + o) * 4   # FWDS: a tiles + cos of L + 1 layers
+        return B * 2 * (L + 1) * n_pad * T + n * (d + o) * 4 + stream // 2   # FWDS: a tiles + cos of L + 1 layers
     if re.match(r'w1_kernel<\d+,5>', k) or k.startswith('wide_kernel<5'):
-        return (L + 1) * n_pad * T + L * n_pad * T + n * (d + o) * 4  # REV: cos read, delta tiles written
+        return B * ((L + 1) * n_pad * T + L * n_pad * T) + n * (d + o) * 4 + stream // 2  # REV: cos read, deltas
     return None
 
 

@@ -34,6 +34,7 @@ PATHS = {  # name: (d, hidden, layers, o, n, work units of F)
     'poisson_ref': (2, 256, 3, 1, 512 * 512, 15),
     'w3_theta': (2, 256, 3, 1, 1 << 19, 6),
     'hypernet': (2, 256, 3, 1, 32 * 4096, 3),
+    'hypernet_np': (2, 256, 3, 1, 32 * 4096, 3),   # the same with SIREN_FLAG_NO_PERSIST (one workgroup per tile)
     'w1': (2, 256, 3, 1, 1 << 20, 2),
     'w1x': (2, 256, 3, 1, 1 << 20, 2),      # the split-bf16 W1 (precision mode bf16x6), same workload as w1
     'w0': (2, 256, 3, 1, 1 << 20, 1),       # the fp32 forward-only W0 (dense evaluation)
@@ -56,9 +57,9 @@ def build_step(name, dev):
     torch.manual_seed(0)
     net = FCBlock(d, o, L, H, outermost_linear=True, nonlinearity='sine')
     flat = torch.cat([p.detach().reshape(-1) for p in net.parameters()]).to(dev)
-    eng = SirenEngine(d, H, L, o)
+    eng = SirenEngine(d, H, L, o, flags=2 if name == 'hypernet_np' else 0)
     g = torch.Generator(device=dev).manual_seed(1)
-    if name == 'hypernet':
+    if name.startswith('hypernet'):
         B = 32
         fb = flat[None].repeat(B, 1) + 1e-3 * torch.randn(B, flat.numel(), device=dev, generator=g)
         wsb = eng.pack_batched(fb)
