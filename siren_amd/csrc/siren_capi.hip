@@ -121,10 +121,13 @@ int64_t param_count(const siren_cfg* cfg) {
 }
 
 // Split-K factor of the weight-gradient kernel: its grid is (S, L, (H/256)^2) workgroups at one per CU, so S is
-// chosen to fill two whole rounds of the 256 CUs (a grid of 513 would run a third round for one workgroup).
-int64_t wgrad_splits(const siren_cfg* cfg) {
+// chosen to fill whole rounds of the 256 CUs (a grid of 257 would run a second round for one workgroup).
+// Round 3 A/B (profiles/r03g_wgrad_rounds.log): one round of ~256 workgroups beats two rounds of ~512 by 2 % on the
+// image-fit step and 0.5 % on the Poisson / video steps (half the per-workgroup prologue / slab epilogue and slabs to
+// reduce); grouped launches over batched weights keep two rounds (their per-element splits are few already).
+int64_t wgrad_splits(const siren_cfg* cfg, int64_t target = 256) {
     const int64_t per_split = (int64_t)cfg->n_hidden * (cfg->hidden / 256) * (cfg->hidden / 256);
-    const int64_t s = 512 / per_split;
+    const int64_t s = target / per_split;
     return s > 0 ? s : 1;
 }
 
@@ -162,7 +165,7 @@ struct TrainPlan {
         : es(cfg, (n + siren::TILE - 1) / siren::TILE * siren::TILE / 16, batch) {
         n_pad = (n + siren::TILE - 1) / siren::TILE * siren::TILE;
         tiles = n_pad / 16;
-        const int64_t want = std::max<int64_t>(1, wgrad_splits(cfg) / std::max<int64_t>(1, batch));
+        const int64_t want = batch > 1 ? std::max<int64_t>(1, wgrad_splits(cfg, 512) / batch) : wgrad_splits(cfg);
         splits = tiles < want ? tiles : want;
         if (splits < 1) splits = 1;
         tps = std::max<int64_t>(1, (tiles + splits - 1) / splits);  // n == 0: no tiles, one empty split

@@ -38,9 +38,9 @@ def plan(path):
     n_pad = (n + (15 if jet else 63)) // (16 if jet else 64) * (16 if jet else 64)
     cols = 4 * n_pad if jet else n_pad
     tiles = cols // 16
-    want = max(1, 512 // (L * (H // 256) ** 2))
+    want = max(1, 256 // (L * (H // 256) ** 2))
     if path == 'hypernet':
-        want = max(1, want // 32)
+        want = max(1, 512 // (L * (H // 256) ** 2) // 32)
     S = max(1, min(tiles, want))
     tps = max(1, -(-tiles // S))
     S = max(1, -(-tiles // tps))
