@@ -40,6 +40,11 @@
 #include "siren_common.h"
 #include "siren_params.h"
 
+#ifndef SIREN_PROBE
+#define SIREN_PROBE 0
+#endif
+
+
 namespace siren {
 
 // Tile / scratch accessors that step their pointer through an opaque register: the compiler would otherwise
@@ -136,6 +141,9 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
     int s = p0 * NB;
     ring_issue(stream, ring, s, nslices, wave, lane);
     ring_issue(stream, ring, s + 1, nslices, wave, lane);
+    // slice s0 published before the first pass (its successors are published by the mid-slice barriers)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
 
     // ---- first layer: z_0 jet (VALU, K = d_in) ---------------------------------------------------------------
     f32x4 act[NB], acc[NB];
@@ -174,12 +182,21 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
     for (int p = p0; p < p1; ++p) {
 #pragma unroll
         for (int ob = 0; ob < NB; ++ob) acc[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
+        {
+            // mid-slice ring protocol (ring_mid / slice_mma_mid): the operand reads run on across the slice seams
+            const unsigned rbase = lds_addr(ring) + 16u * lane;
+            f32x4 a0 = lds_read4<0>(rbase + (s % NBUF) * SLICE * 4);
+            f32x4 a1 = lds_read4<1024>(rbase + (s % NBUF) * SLICE * 4);
 #pragma unroll
-        for (int kb2 = 0; kb2 < NB; ++kb2) {
-            ring_wait(s, nslices);
-            ring_issue(stream, ring, s + 2, nslices, wave, lane);
-            slice_mma<NB>(lds_addr(ring + (s % NBUF) * SLICE) + 16u * lane, act[kb2], acc);  // lds_ops.h
-            ++s;
+            for (int kb2 = 0; kb2 < NB; ++kb2) {
+                const unsigned va = rbase + (s % NBUF) * SLICE * 4, vn = rbase + ((s + 1) % NBUF) * SLICE * 4;
+                auto mid = [&]() { ring_mid(stream, ring, s, nslices, wave, lane); };
+                if (kb2 + 1 < NB)
+                    slice_mma_mid<NB, 4, true>(va, vn, act[kb2], acc, a0, a1, a0, a1, mid);
+                else
+                    slice_mma_mid<NB, 4, false>(va, vn, act[kb2], acc, a0, a1, a0, a1, mid);
+                ++s;
+            }
         }
         if (p < lh) {
             // forward layer l = p + 1: z_l jet -> scratch, a_l jet -> abuf
@@ -191,6 +208,12 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
 #pragma unroll
             for (int rb = 0; rb < NB; ++rb) {
                 const f32x4 z = acc[rb] + val * *(const f32x4*)(bl + 16 * rb);
+#if SIREN_PROBE >= 1
+                if (true) {
+                    zs.next_store(z);
+                    act[rb] = z;
+                } else
+#endif
                 if constexpr (QG) {
                     f32x4 kz;
                     act[rb] = jet_sin_q(z, w, val, kb, kg, qc[0], qc[1], js == 3, kz);
@@ -200,7 +223,9 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
                     act[rb] = jet_sin<MIX>(z, w, val, kb, kg);
                 }
             }
+#if SIREN_PROBE < 2
             jstore_tile(abuf + (int64_t)l * lstride + toff, act);
+#endif
             if (PHASE == JET_FWD && l == lh) {
                 // outputs per stream (the W4 forward's): y_j (value), sum_j dy_j/dx_k (tangent k), sum_j Lap y_j
                 float tot = 0.f;
@@ -274,10 +299,16 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
             const f32x2 qc = qload();
 #pragma unroll
             for (int rb = 0; rb < NB; ++rb) {
+#if SIREN_PROBE >= 1  // timing probe (tools/probe_build.sh): no epilogue arithmetic
+                act[rb] = acc[rb] + zl.next_load();
+#else
                 act[rb] = QG ? jet_sin_adjoint_q(acc[rb], zl.next_load(), wl, val, m12, qc[0], qc[1])
                              : jet_sin_adjoint<MIX>(acc[rb], zl.next_load(), wl, val, m12, s1);
+#endif
             }
+#if SIREN_PROBE < 2
             jstore_tile(dbuf + (int64_t)lm * lstride + toff, act);
+#endif
         }
     }
 

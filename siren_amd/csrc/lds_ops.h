@@ -61,6 +61,49 @@ __device__ __forceinline__ void slice_pairs(unsigned vaddr, const f32x4& bop, f3
     if constexpr (P + 1 < NBLK / 2) slice_pairs<P + 1, NBLK>(vaddr, bop, acc, n0, n1);
 }
 
+// Mid-slice ring protocol (the W1 kernel's; here for the runtime-loop kernels): the barrier sits
+// after output-block pair MID of slice s instead of at the slice start. It publishes slice s+1 (its loads were
+// issued one slice earlier) and frees the slot of slice s-1 for slice s+2, so the pair-ahead operand reads run on
+// across the slice seam (the last pair of a slice reads the next slice's first pair) and no wave waits for the
+// barrier with an empty MFMA queue. mid() = the wait + barrier + issue; NEXT = read the next slice's first pair.
+template <int P, int NBLK, int MID, bool NEXT, class Mid>
+__device__ __forceinline__ void slice_pairs_mid(unsigned vaddr, unsigned vnext, const f32x4& bop, f32x4 (&acc)[NBLK],
+                                                f32x4 a0, f32x4 a1, f32x4& o0, f32x4& o1, Mid& mid) {
+    constexpr int ob = 2 * P;
+    constexpr bool last = P + 1 == NBLK / 2;
+    if constexpr (P == MID) mid();
+    f32x4 n0, n1;
+    if constexpr (!last) {
+        n0 = lds_read4<(ob + 2) * 1024>(vaddr);
+        n1 = lds_read4<(ob + 3) * 1024>(vaddr);
+        lgkm_wait<2>(a0, a1);
+    } else if constexpr (NEXT) {
+        n0 = lds_read4<0>(vnext);
+        n1 = lds_read4<1024>(vnext);
+        lgkm_wait<2>(a0, a1);
+    } else {
+        lgkm_wait<0>(a0, a1);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        acc[ob] = mfma4(a0[r], bop[r], acc[ob]);
+        acc[ob + 1] = mfma4(a1[r], bop[r], acc[ob + 1]);
+    }
+    if constexpr (!last) {
+        slice_pairs_mid<P + 1, NBLK, MID, NEXT>(vaddr, vnext, bop, acc, n0, n1, o0, o1, mid);
+    } else if constexpr (NEXT) {
+        o0 = n0;
+        o1 = n1;
+    }
+}
+// one slice with the mid-slice barrier: a0 / a1 = its first pair (in flight); with NEXT, o0 / o1 receive the next
+// slice's first pair (in flight)
+template <int NBLK, int MID, bool NEXT, class Mid>
+__device__ __forceinline__ void slice_mma_mid(unsigned vaddr, unsigned vnext, const f32x4& bop, f32x4 (&acc)[NBLK],
+                                              f32x4 a0, f32x4 a1, f32x4& o0, f32x4& o1, Mid&& mid) {
+    slice_pairs_mid<0, NBLK, MID, NEXT>(vaddr, vnext, bop, acc, a0, a1, o0, o1, mid);
+}
+
 // one slice; vaddr = LDS byte address of the ring slot + 16 * lane
 template <int NBLK>
 __device__ __forceinline__ void slice_mma(unsigned vaddr, const f32x4& bop, f32x4 (&acc)[NBLK]) {
@@ -93,6 +136,41 @@ template <int NBLK>
 __device__ __forceinline__ void slice_mma2(unsigned vaddr, const f32x4& bp, const f32x4& bt, f32x4 (&accp)[NBLK],
                                            f32x4 (&acct)[NBLK]) {
     slice_singles2<0, NBLK>(vaddr, bp, bt, accp, acct, lds_read4<0>(vaddr));
+}
+
+// slice_singles2 with the mid-slice barrier (slice_pairs_mid): mid() before block MID, the last block reads the next
+// slice's first block (NEXT) into o
+template <int OB, int NBLK, int MID, bool NEXT, class Mid>
+__device__ __forceinline__ void slice_singles2_mid(unsigned vaddr, unsigned vnext, const f32x4& bp, const f32x4& bt,
+                                                   f32x4 (&accp)[NBLK], f32x4 (&acct)[NBLK], f32x4 a, f32x4& o,
+                                                   Mid& mid) {
+    constexpr bool last = OB + 1 == NBLK;
+    if constexpr (OB == MID) mid();
+    f32x4 nx;
+    if constexpr (!last) {
+        nx = lds_read4<(OB + 1) * 1024>(vaddr);
+        lgkm_wait1<1>(a);
+    } else if constexpr (NEXT) {
+        nx = lds_read4<0>(vnext);
+        lgkm_wait1<1>(a);
+    } else {
+        lgkm_wait1<0>(a);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        accp[OB] = mfma4(a[r], bp[r], accp[OB]);
+        acct[OB] = mfma4(a[r], bt[r], acct[OB]);
+    }
+    if constexpr (!last) {
+        slice_singles2_mid<OB + 1, NBLK, MID, NEXT>(vaddr, vnext, bp, bt, accp, acct, nx, o, mid);
+    } else if constexpr (NEXT) {
+        o = nx;
+    }
+}
+template <int NBLK, int MID, bool NEXT, class Mid>
+__device__ __forceinline__ void slice_mma2_mid(unsigned vaddr, unsigned vnext, const f32x4& bp, const f32x4& bt,
+                                               f32x4 (&accp)[NBLK], f32x4 (&acct)[NBLK], f32x4 a, f32x4& o, Mid&& mid) {
+    slice_singles2_mid<0, NBLK, MID, NEXT>(vaddr, vnext, bp, bt, accp, acct, a, o, mid);
 }
 
 }  // namespace siren

@@ -28,4 +28,13 @@ __device__ __forceinline__ void ring_wait(int s, int nslices) {
     __builtin_amdgcn_s_barrier();
 }
 
+// Mid-slice form (slice_mma_mid): in slice s, wait until slice s+1 has landed (it is the newest load in flight; a
+// pass's epilogue stores are waited for too), barrier, then refill the slot of slice s-1 with slice s+2.
+__device__ __forceinline__ void ring_mid(const float* __restrict__ stream, float* ring, int s, int nslices, int wave,
+                                         int lane) {
+    if (s + 1 < nslices) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    ring_issue(stream, ring, s + 2, nslices, wave, lane);
+}
+
 }  // namespace siren

@@ -35,6 +35,9 @@
 
 namespace siren {
 
+// The layer GEMMs with the mid-slice ring protocol (ring_mid, lds_ops.h slice_*_mid): slice s is published on entry
+// (by the previous GEMM's last mid-slice barrier or the kernel's ring prologue); the operand reads run on across the
+// slice seams inside the GEMM.
 __device__ __forceinline__ void layer_mma2(const float* __restrict__ stream, float* ring, int& s, int nslices,
                                            int wave, int lane, const f32x4 (&bp)[NB], const f32x4 (&bt)[NB],
                                            f32x4 (&accp)[NB], f32x4 (&acct)[NB]) {
@@ -43,11 +46,16 @@ __device__ __forceinline__ void layer_mma2(const float* __restrict__ stream, flo
         accp[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
         acct[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    const unsigned rbase = lds_addr(ring) + 16u * lane;
+    f32x4 a = lds_read4<0>(rbase + (s % NBUF) * SLICE * 4);
 #pragma unroll
     for (int kb = 0; kb < NB; ++kb) {
-        ring_wait(s, nslices);
-        ring_issue(stream, ring, s + 2, nslices, wave, lane);
-        slice_mma2<NB>(lds_addr(ring + (s % NBUF) * SLICE) + 16u * lane, bp[kb], bt[kb], accp, acct);  // lds_ops.h
+        const unsigned va = rbase + (s % NBUF) * SLICE * 4, vn = rbase + ((s + 1) % NBUF) * SLICE * 4;
+        auto mid = [&]() { ring_mid(stream, ring, s, nslices, wave, lane); };
+        if (kb + 1 < NB)
+            slice_mma2_mid<NB, NB / 2, true>(va, vn, bp[kb], bt[kb], accp, acct, a, a, mid);
+        else
+            slice_mma2_mid<NB, NB / 2, false>(va, vn, bp[kb], bt[kb], accp, acct, a, a, mid);
         ++s;
     }
 }
@@ -57,11 +65,17 @@ __device__ __forceinline__ void layer_mma1(const float* __restrict__ stream, flo
                                            int wave, int lane, const f32x4 (&bt)[NB], f32x4 (&acct)[NB]) {
 #pragma unroll
     for (int ob = 0; ob < NB; ++ob) acct[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const unsigned rbase = lds_addr(ring) + 16u * lane;
+    f32x4 a0 = lds_read4<0>(rbase + (s % NBUF) * SLICE * 4);
+    f32x4 a1 = lds_read4<1024>(rbase + (s % NBUF) * SLICE * 4);
 #pragma unroll
     for (int kb = 0; kb < NB; ++kb) {
-        ring_wait(s, nslices);
-        ring_issue(stream, ring, s + 2, nslices, wave, lane);
-        slice_mma<NB>(lds_addr(ring + (s % NBUF) * SLICE) + 16u * lane, bt[kb], acct);  // lds_ops.h
+        const unsigned va = rbase + (s % NBUF) * SLICE * 4, vn = rbase + ((s + 1) % NBUF) * SLICE * 4;
+        auto mid = [&]() { ring_mid(stream, ring, s, nslices, wave, lane); };
+        if (kb + 1 < NB)
+            slice_mma_mid<NB, NB / 4, true>(va, vn, bt[kb], acct, a0, a1, a0, a1, mid);
+        else
+            slice_mma_mid<NB, NB / 4, false>(va, vn, bt[kb], acct, a0, a1, a0, a1, mid);
         ++s;
     }
 }
@@ -131,6 +145,8 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
     __syncthreads();
     ring_issue(stream, ring, 0, nslices, wave, lane);
     ring_issue(stream, ring, 1, nslices, wave, lane);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // slice 0 (and every earlier load) landed: publish it
+    __builtin_amdgcn_s_barrier();
 
     f32x4 actp[NB], actt[NB], accp[NB], acct[NB];
     // ---- layer 0 (VALU): z0 = W0 x + b0, zd0 = W0 v ----------------------------------------------------
