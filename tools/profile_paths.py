@@ -57,7 +57,8 @@ def build_step(name, dev):
     torch.manual_seed(0)
     net = FCBlock(d, o, L, H, outermost_linear=True, nonlinearity='sine')
     flat = torch.cat([p.detach().reshape(-1) for p in net.parameters()]).to(dev)
-    eng = SirenEngine(d, H, L, o, flags=2 if name == 'hypernet_np' else 0)
+    # SIREN_FLAGS (env): cfg.reserved flags for A/B runs (2 = SIREN_FLAG_NO_PERSIST)
+    eng = SirenEngine(d, H, L, o, flags=2 if name == 'hypernet_np' else int(os.environ.get('SIREN_FLAGS', '0')))
     g = torch.Generator(device=dev).manual_seed(1)
     if name.startswith('hypernet'):
         B = 32
