@@ -80,13 +80,15 @@ void launch_small_j2(dim3 grid, hipStream_t st, const float* abuf, const float* 
                      const float* gy, const float* u, int64_t n, int64_t n_pad, int64_t tps, float* eslab, int64_t E,
                      int d, int o, int lh);
 // tu_w3.hip (launch_small_w3 lives in tu_train.hip with the other edge-layer reductions)
+// ws_bs != 0: grouped over batched weights (grid.y = element; per-element strides of ws, the spill and A / At / D / Dt)
 void launch_w3(bool theta, dim3 grid, hipStream_t st, const float* ws, const float* x, const float* v, const float* gy,
                const float* u, float* ydot, int o, int64_t n, float* gx, float* spill, float* A, float* At, float* D,
                float* Dt, int64_t n_pad, int d, int lh, float w0, float w, const float* kA = nullptr,
-               const float* kC = nullptr, unsigned long long* prof = nullptr);
+               const float* kC = nullptr, unsigned long long* prof = nullptr, int64_t ws_bs = 0, int64_t spill_bs = 0,
+               int64_t buf_bs = 0);
 void launch_small_w3(dim3 grid, hipStream_t st, const float* At, const float* D, const float* Dt, const float* AL,
                      const float* x, const float* v, const float* gy, const float* u, int64_t n, int64_t n_pad, int64_t tps,
-                     float* eslab, int64_t E, int d, int o, int lh);
+                     float* eslab, int64_t E, int d, int o, int lh, int64_t bstride_act = 0, int64_t bstride_e = 0);
 // tu_train.hip
 // bstride_act / bstride_part: grouped W2 over batched weights (grid.z of wgrad, grid.y of small / reduce = element)
 void launch_wgrad(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, int64_t n_pad, int64_t tps,

@@ -828,8 +828,11 @@ namespace {
 struct W3Plan {
     int64_t n_pad, tiles, splits, tps, spill_floats, buf_floats, partial_floats, total, eslab_off;
     EdgeSplit es;
-    W3Plan(const siren_cfg* cfg, int64_t n, bool theta) : es(cfg, (n + siren::TILE - 1) / siren::TILE * siren::TILE / 16) {
-        const TrainPlan tp(cfg, n);
+    // batch > 1: a grouped launch over batched weights (per-element layout strides: spill_floats, buf_floats,
+    // partial_floats; fewer splits per element, as TrainPlan)
+    W3Plan(const siren_cfg* cfg, int64_t n, bool theta, int64_t batch = 1)
+        : es(cfg, (n + siren::TILE - 1) / siren::TILE * siren::TILE / 16, batch) {
+        const TrainPlan tp(cfg, n, batch);
         n_pad = tp.n_pad;
         tiles = tp.tiles;
         splits = tp.splits;
@@ -1115,9 +1118,23 @@ int32_t siren_pack_batched_ex(const siren_cfg* cfg, const float* params, int64_t
 // second / third order over batched weights (the create_graph branch of a hypernetwork's hypo network): element b's
 // fully packed workspace (siren_pack_batched_ex full = 1) through the single-network entry points, tws reused element
 // after element (stream order)
+// grouped W3 (hidden 256, 1..3 hidden layers, elements below ~2 CU rounds of tiles): ONE W3 launch (grid.y = element),
+// two grouped wgrad launches, one edge and one reduction launch over all elements; workspace per element = the W3Plan
+// of the grouped split ([spill][A][At][D][Dt][partial slabs], each block holding every element's part)
+bool grouped_w3(const siren_cfg* cfg, int64_t n) {
+    return !wide(cfg) && !layered(cfg) && cfg->outermost_linear && cfg->n_hidden <= siren::MAX_LH_GRAD &&
+           (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0 && (n + siren::TILE - 1) / siren::TILE < 2 * cu_count();
+}
+
 int32_t siren_second_order_batched_ws_floats(const siren_cfg* cfg, int64_t n, int64_t batch, int32_t want_theta,
                                              int64_t* count) {
     if (batch < 0) return fail(SIREN_EINVAL, "batch < 0");
+    if (batch > 1 && n > 0 && grouped_w3(cfg, n)) {
+        if (int rc = check_cfg(cfg, true)) return rc;
+        if (count == nullptr) return fail(SIREN_EINVAL, "count is NULL");
+        *count = batch * W3Plan(cfg, n, want_theta != 0, batch).total;
+        return SIREN_OK;
+    }
     return siren_second_order_ws_floats(cfg, n, want_theta, count);
 }
 
@@ -1129,6 +1146,37 @@ int32_t siren_second_order_batched(const siren_cfg* cfg, const float* ws, const 
     const int64_t W = ws_floats(cfg), P = param_count(cfg);
     const int d = cfg->d_in, o = cfg->d_out;
     if (batch > 0 && ws == nullptr) return fail(SIREN_EINVAL, "ws is NULL");
+    if (batch > 1 && n > 0 && grouped_w3(cfg, n)) {
+        if (x == nullptr || v == nullptr || tws == nullptr || gx == nullptr)
+            return fail(SIREN_EINVAL, "x/v/tws/gx is NULL");
+        const bool theta = gparams != nullptr;
+        const W3Plan plan(cfg, n, theta, batch);
+        const hipStream_t st = (hipStream_t)stream;
+        float* spill = tws;
+        float* A = spill + batch * plan.spill_floats;
+        float* At = A + batch * plan.buf_floats;
+        float* D = At + batch * plan.buf_floats;
+        float* Dt = D + batch * plan.buf_floats;
+        float* partial = Dt + batch * plan.buf_floats;
+        siren::launch_w3(theta, dim3((unsigned)(plan.n_pad / siren::TILE), (unsigned)batch), st, ws, x, v, gy, u, ydot,
+                         o, n, gx, spill, A, At, D, Dt, plan.n_pad, d, cfg->n_hidden, cfg->omega_first,
+                         cfg->omega_hidden, nullptr, nullptr, nullptr, W, plan.spill_floats, plan.buf_floats);
+        if (int rc = hip_status("siren_second_order_batched (grouped w3)")) return rc;
+        if (!theta) return SIREN_OK;
+        const dim3 wgrid((unsigned)plan.splits, (unsigned)cfg->n_hidden, (unsigned)batch);
+        siren::launch_wgrad(wgrid, st, A, D, plan.n_pad, plan.tps, partial, P, d, o, cfg->n_hidden, 1, siren::H, 0,
+                            plan.buf_floats, plan.partial_floats);
+        siren::launch_wgrad(wgrid, st, At, Dt, plan.n_pad, plan.tps, partial + plan.splits * P, P, d, o,
+                            cfg->n_hidden, 0, siren::H, 0, plan.buf_floats, plan.partial_floats);
+        if (int rc = hip_status("siren_second_order_batched (grouped wgrad)")) return rc;
+        const float* a_last = A + (int64_t)cfg->n_hidden * plan.n_pad * siren::H;
+        siren::launch_small_w3(plan.es.grid(cfg, batch), st, At, D, Dt, a_last, x, v, gy, u, n, plan.n_pad,
+                               plan.es.tps, partial + plan.eslab_off, plan.es.E, d, o, cfg->n_hidden, plan.buf_floats,
+                               plan.partial_floats);
+        if (int rc = hip_status("siren_second_order_batched (grouped small)")) return rc;
+        return finish_grads(cfg, st, partial, plan.splits, plan.splits, partial + plan.eslab_off, plan.es, gparams,
+                            "siren_second_order_batched (grouped reduce)", batch, plan.partial_floats);
+    }
     for (int64_t b = 0; b < batch; ++b)
         if (int rc = siren_second_order_ex(cfg, ws + b * W, x ? x + b * n * d : nullptr, n, v ? v + b * n * d : nullptr,
                                            u ? u + b * n * o : nullptr, gy ? gy + b * n * o : nullptr, tws,

@@ -278,12 +278,20 @@ __global__ __launch_bounds__(edge_threads(KIND)) void edge_kernel(const float* _
     const int64_t q = (t1 - t0 + EDGE_GROUPS - 1) / EDGE_GROUPS;
     const int64_t g0 = t0 + grp * q < t1 ? t0 + grp * q : t1, g1 = g0 + q < t1 ? g0 + q : t1;
     const int64_t trips = (q + EDGE_CHUNK - 1) / EDGE_CHUNK;
-    if (gridDim.z > 1) {  // grouped W2 (EDGE_W2 over batched weights): grid.z = batch element
+    if (gridDim.z > 1) {  // grouped over batched weights (EDGE_W2: W2, EDGE_W3: second order): grid.z = element
         const int64_t b = blockIdx.z;
         r0 += b * bstride_act;
         r1 += b * bstride_act;
         x += b * n * d;
-        sc += b * n * o;
+        if constexpr (KIND == EDGE_W3) {
+            r2 += b * bstride_act;
+            if (r3 != nullptr) r3 += b * bstride_act;
+            sc += b * n * d;  // v
+            if (sgy != nullptr) sgy += b * n * o;
+            if (su != nullptr) su += b * n * o;
+        } else {
+            sc += b * n * o;  // gy
+        }
         eslab += b * bstride_e;
     }
     const int64_t tstride = (int64_t)h * 16;

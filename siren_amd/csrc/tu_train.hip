@@ -23,9 +23,10 @@ void launch_small(dim3 grid, hipStream_t st, const float* abuf, const float* dbu
 
 void launch_small_w3(dim3 grid, hipStream_t st, const float* At, const float* D, const float* Dt, const float* AL,
                      const float* x, const float* v, const float* gy, const float* u, int64_t n, int64_t n_pad,
-                     int64_t tps, float* eslab, int64_t E, int d, int o, int lh) {
+                     int64_t tps, float* eslab, int64_t E, int d, int o, int lh, int64_t bstride_act,
+                     int64_t bstride_e) {
     hipLaunchKernelGGL(edge_kernel<EDGE_W3>, grid, dim3(edge_threads(EDGE_W3)), 0, st, D, At + (int64_t)lh * n_pad * H,
-                       Dt, AL, x, v, gy, u, n, n_pad / 16, tps, eslab, E, d, o, lh, H, (int64_t)0, (int64_t)0);
+                       Dt, AL, x, v, gy, u, n, n_pad / 16, tps, eslab, E, d, o, lh, H, bstride_act, bstride_e);
 }
 
 void launch_small_jet(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x,

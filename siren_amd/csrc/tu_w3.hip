@@ -9,10 +9,10 @@ namespace siren {
 void launch_w3(bool theta, dim3 grid, hipStream_t st, const float* ws, const float* x, const float* v, const float* gy,
                const float* u, float* ydot, int o, int64_t n, float* gx, float* spill, float* A, float* At, float* D,
                float* Dt, int64_t n_pad, int d, int lh, float w0, float w, const float* kA, const float* kC,
-               unsigned long long* prof) {
+               unsigned long long* prof, int64_t ws_bs, int64_t spill_bs, int64_t buf_bs) {
 #define SIREN_L(LHV, TH, KP)                                                                                    \
     hipLaunchKernelGGL((w3_kernel<LHV, TH, KP>), grid, dim3(THREADS), 0, st, ws, x, v, gy, u, ydot, o, n, gx, spill, A, \
-                       At, D, Dt, n_pad, d, w0, w, kA, kC, prof)
+                       At, D, Dt, n_pad, d, w0, w, kA, kC, prof, ws_bs, spill_bs, buf_bs)
 #define SIREN_LH(TH, KP)                   \
     switch (lh) {                          \
         case 1: SIREN_L(1, TH, KP); break; \

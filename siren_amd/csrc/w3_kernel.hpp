@@ -101,17 +101,40 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
                                                         float* __restrict__ Dt, int64_t n_pad, int d, float w0,
                                                         float w, const float* __restrict__ kA,
                                                         const float* __restrict__ kC,
-                                                        unsigned long long* __restrict__ prof = nullptr) {
+                                                        unsigned long long* __restrict__ prof = nullptr,
+                                                        int64_t ws_bs = 0, int64_t spill_bs = 0, int64_t buf_bs = 0) {
     __shared__ __attribute__((aligned(16))) float lds[NBUF * SLICE + SMALL_MAX + WAVES * STB_SCRATCH];
     float* ring = lds;
     float* sm = lds + NBUF * SLICE;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane >> 4, c = lane & 15;
     const int nslices = 2 * LH * NB;
+    // grouped launch over batched weights (siren_second_order_batched): block (x, element), renumbered XCD-major
+    int64_t bx = blockIdx.x;
+    if (ws_bs != 0) {
+        unsigned rx, ry;
+        xcd_remap(rx, ry);
+        bx = rx;
+        const int64_t b = ry;
+        ws += b * ws_bs;
+        x += b * n * d;
+        v += b * n * d;
+        gx += b * n * d;
+        if (gy != nullptr) gy += b * n * o;
+        if (u != nullptr) u += b * n * o;
+        if (ydot != nullptr) ydot += b * n * o;
+        spill += b * spill_bs;
+        if (THETA) {
+            A += b * buf_bs;
+            At += b * buf_bs;
+            D += b * buf_bs;
+            Dt += b * buf_bs;
+        }
+    }
     const float* stream = ws + small_pad(LH);
-    const int64_t tile = (int64_t)blockIdx.x * WAVES + wave;
+    const int64_t tile = bx * WAVES + wave;
     // diagnostics (siren_w3_phase_profile): s_memtime after each phase, workgroups < 256, wave 0
-    const bool rec = prof != nullptr && blockIdx.x < 256 && wave == 0;
+    const bool rec = prof != nullptr && blockIdx.x < 256 && blockIdx.y == 0 && wave == 0;
     int ev = 0;
     auto mark = [&]() {
         if (rec) {
@@ -127,14 +150,14 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
     const int64_t tbase = tile * (H * 16);  // the wave's tile (store_block4)
     float* stb = lds + NBUF * SLICE + SMALL_MAX + wave * STB_SCRATCH;
     auto kept_c = [&](int l, int rb) -> f32x4 {
-        return *(const f32x4*)(kC + cos_off(blockIdx.x, wave, LH, l, rb, lane));
+        return *(const f32x4*)(kC + cos_off(bx, wave, LH, l, rb, lane));
     };
 
     {
         const int nf4 = (small_floats(LH) + 3) / 4;
         for (int e = threadIdx.x; e < nf4; e += THREADS) ((f32x4*)sm)[e] = ((const f32x4*)ws)[e];
     }
-    const int64_t coord = (int64_t)blockIdx.x * TILE + wave * 16 + c;
+    const int64_t coord = bx * TILE + wave * 16 + c;
     const bool valid = coord < n;
     float xv[MAXD], vv[MAXD];
 #pragma unroll

@@ -192,7 +192,9 @@ def test_hypo_second_and_third_order_vs_reference(cuda, g7, g11, monkeypatch, ln
 @pytest.mark.parametrize('B,n,d,L,o,H', [(3, 1000, 2, 3, 1, 256), (2, 333, 3, 2, 3, 256), (2, 300, 3, 3, 2, 512)])
 def test_batched_second_third_order_equal_per_element(cuda, B, n, d, L, o, H):
     """siren_second_order_batched / siren_hvp_backward_batched equal the single-network entry points element by
-    element (bitwise) on a full batched pack, which equals siren_pack per element."""
+    element on a full batched pack, which equals siren_pack per element: bitwise for everything but the hidden-256
+    second-order theta gradient, whose grouped W3 path (one launch per stage over all elements) splits the
+    coordinate sum into fewer slabs than the single-network call (summation order only: 1e-5 of the largest)."""
     from siren_amd.engine import SirenEngine
     eng = SirenEngine(d, H, L, o)
     flat = torch.tensor(random_flat(B, d, L, o, H, seed=7 * n + B), device=cuda)
@@ -208,7 +210,14 @@ def test_batched_second_third_order_equal_per_element(cuda, B, n, d, L, o, H):
         ws = eng.pack(flat[b])
         assert torch.equal(ws, wsb[b])
         gx1, gp1, yd1 = eng.second_order(ws, x[b], v[b], want_theta=True, gy=gy[b], u=u[b], want_ydot=True)
-        assert torch.equal(gx1, gxb[b]) and torch.equal(gp1, gpb[b]) and torch.equal(yd1, ydb[b])
+        assert torch.equal(gx1, gxb[b]) and torch.equal(yd1, ydb[b])
+        if H == 256:
+            assert torch.isfinite(gpb[b]).all()
+            assert (gp1 - gpb[b]).abs().max() <= 1e-5 * gp1.abs().max(), (gp1 - gpb[b]).abs().max()
+        else:
+            assert torch.equal(gp1, gpb[b])
         r = eng.hvp_backward(ws, x[b], v[b], g[b], u[b], want_theta=True, want_v=True, want_u=True)
         for a1, ab in zip(r, (hx, hp, hv, hu)):
             assert torch.equal(a1, ab[b])
+    gx0, gp0 = eng.second_order_batched(wsb, x, v, want_theta=False, gy=gy, u=u)
+    assert gp0 is None and torch.equal(gx0, gxb)

@@ -13,6 +13,7 @@ Paths (BASELINE.json configs; F = 2 sum fan_in fan_out FLOP per coordinate, SURV
   w3_theta     5x256 d2 o1, 2^19 coords: W3 H v + theta-grads without a kept forward (6F)
   hypernet     32 x 4096 coords, 5x256 d2 o1 per-element weights: grouped stored forward + grouped reverse-only W2
                (the hypernetwork training kernels, W2 = 3F)
+  hypernet_w3  the same batch: grouped W3 H v + theta-grads (second_order_batched, 6F); _loop = 32 single calls
   w1           5x256 d2 o1, 2^20 coords: the headline W1 launch (2F)
   w1x          the same on the split-bf16 kernel (w1x_kernel.hpp, precision mode bf16x6)
   w3_wide      5x512 d3 o1, 2^18 coords: W3 H v + theta-grads at hidden 512 (two-stream jet + wgrad, 6F)
@@ -35,6 +36,8 @@ PATHS = {  # name: (d, hidden, layers, o, n, work units of F)
     'w3_theta': (2, 256, 3, 1, 1 << 19, 6),
     'hypernet': (2, 256, 3, 1, 32 * 4096, 3),
     'hypernet_np': (2, 256, 3, 1, 32 * 4096, 3),   # the same with SIREN_FLAG_NO_PERSIST (one workgroup per tile)
+    'hypernet_w3': (2, 256, 3, 1, 32 * 4096, 6),   # grouped W3 H v + theta-grads over 32 per-element networks
+    'hypernet_w3_loop': (2, 256, 3, 1, 32 * 4096, 6),  # the same as 32 single-network second_order calls
     'w1': (2, 256, 3, 1, 1 << 20, 2),
     'w1x': (2, 256, 3, 1, 1 << 20, 2),      # the split-bf16 W1 (precision mode bf16x6), same workload as w1
     'w0': (2, 256, 3, 1, 1 << 20, 1),       # the fp32 forward-only W0 (dense evaluation)
@@ -60,6 +63,15 @@ def build_step(name, dev):
     # SIREN_FLAGS (env): cfg.reserved flags for A/B runs (2 = SIREN_FLAG_NO_PERSIST)
     eng = SirenEngine(d, H, L, o, flags=2 if name == 'hypernet_np' else int(os.environ.get('SIREN_FLAGS', '0')))
     g = torch.Generator(device=dev).manual_seed(1)
+    if name.startswith('hypernet_w3'):
+        B = 32
+        fb = flat[None].repeat(B, 1) + 1e-3 * torch.randn(B, flat.numel(), device=dev, generator=g)
+        wsb = eng.pack_batched(fb, full=True)
+        xb = torch.rand(B, n // B, d, device=dev, generator=g) * 2 - 1
+        vb = torch.randn(B, n // B, d, device=dev, generator=g)
+        if name == 'hypernet_w3':
+            return lambda: eng.second_order_batched(wsb, xb, vb, want_theta=True)
+        return lambda: [eng.second_order(wsb[b], xb[b], vb[b], want_theta=True) for b in range(B)]
     if name.startswith('hypernet'):
         B = 32
         fb = flat[None].repeat(B, 1) + 1e-3 * torch.randn(B, flat.numel(), device=dev, generator=g)
