@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SIREN_ABI_VERSION 3
+#define SIREN_ABI_VERSION 4
 
 enum {
     SIREN_OK = 0,
@@ -200,6 +200,22 @@ int32_t siren_hvp_backward(const siren_cfg* cfg, const float* ws, const float* x
 int32_t siren_hessian_backward_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count);
 int32_t siren_hessian_backward(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* G,
                                const float* u, float* tws, float* gx, float* gparams, float* gu, void* stream);
+
+/* The Hessian node's forward, Hm (n, d_in, d_in) = sum_j u_j H_j(x) (u (n, d_out), NULL = ones) — what each
+ * divergence() / hessian() column of the reference reads (diff_operators.py:5-36: autograd.grad of one gradient
+ * column per input dimension) — in ONE forward-mode second-order jet sweep over the coordinate axes (value, 2
+ * tangents, 3 second-order streams; 8 coordinates x 6 streams in three MFMA tiles, no reverse sweep). kept (nullable,
+ * siren_hessian_ws_floats(cfg, n, 1, &count) floats; caller-owned, 0 floats with keep = 0) receives the per-layer
+ * jets: siren_hessian_backward_kept with the same kept then skips the forward GEMMs of its quadratic-form jet. Same
+ * coverage as siren_hessian_backward. */
+int32_t siren_hessian_ws_floats(const siren_cfg* cfg, int64_t n, int32_t keep, int64_t* count);
+int32_t siren_hessian(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* u, float* kept,
+                      float* hm, void* stream);
+/* siren_hessian_backward reading its forward jets from a siren_hessian kept buffer of the same (ws, x, n) (kept
+ * NULL: recompute, = siren_hessian_backward). */
+int32_t siren_hessian_backward_kept(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* G,
+                                    const float* u, const float* kept, float* tws, float* gx, float* gparams,
+                                    float* gu, void* stream);
 
 /* Split-bf16 W1 (precision mode "bf16x6"): siren_forward_grad with gy = ones for the headline network (hidden 256,
  * 3 hidden layers, d_in 2 / 3, d_out 1, linear output) with the layer GEMMs on the bf16 matrix pipe. Every fp32

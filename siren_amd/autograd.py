@@ -221,11 +221,17 @@ class SirenHessian(torch.autograd.Function):
     laplace = divergence(gradient()) (diff_operators.py:27-36), each hessian() column (:5-24) — is the cheap torch
     product Hm v, so autograd SUMS all their cotangents into one G (n, d, d) and calls this backward ONCE: one
     quadratic-form jet sweep + one MFMA wgrad (siren_hessian_backward) for the whole third-order term, where one
-    SirenHVP node per dimension cost d mixed-jet sweeps and d wgrads. Forward: the W3 x-part along each axis."""
+    SirenHVP node per dimension cost d mixed-jet sweeps and d wgrads. Forward: one forward-mode second-order jet
+    (siren_hessian) that keeps its per-layer jets (KEEP_MAX_BYTES) for the backward, which then runs the reverse
+    GEMMs only."""
+
+    KEEP_MAX_BYTES = 16 << 30  # kept jets: 4 (n_hidden + 1) 6 256 bytes per point (6 KiB / layer)
 
     @staticmethod
     def forward(ctx, engine, ws, x, flat, u=None):
-        hm = engine.hessian(ws, x, u)
+        per_point = 4 * (engine.cfg.n_hidden + 1) * 6 * 256
+        keep = x.shape[0] * per_point <= SirenHessian.KEEP_MAX_BYTES
+        hm, ctx.kept = engine.hessian(ws, x, u, keep=True) if keep else (engine.hessian(ws, x, u), None)
         ctx.engine, ctx.ws = engine, ws
         ctx.save_for_backward(x, flat, u)
         return hm
@@ -241,7 +247,9 @@ class SirenHessian(torch.autograd.Function):
         if not (need_x or need_p or need_u):
             return None, None, None, None, None
         if not torch.is_grad_enabled():
-            gx, gp, gu = eng.hessian_backward(ctx.ws, x, G.contiguous(), u, want_theta=need_p, want_u=need_u)
+            gx, gp, gu = eng.hessian_backward(ctx.ws, x, G.contiguous(), u, want_theta=need_p, want_u=need_u,
+                                              kept=ctx.kept)
+            ctx.kept = None
             return None, None, (gx if need_x else None), gp, gu
         rx, rp, ru = _torch_path.hessian_vjp(eng.cfg, x, flat, G, create_graph=True, u=u)
         return None, None, rx, rp, ru
@@ -250,7 +258,7 @@ class SirenHessian(torch.autograd.Function):
 def _hessian_product(ctx, engine, ws, x, flat, v, u=None):
     """sum_j u_j H_j v through the gradient node's shared SirenHessian node (built on the first request, kept on the
     gradient node's ctx: later requests of the same node reuse it), or None when the kernels do not cover it."""
-    if not (engine.hessian_backward_supported and engine.second_order_supported):
+    if not engine.hessian_backward_supported:
         return None
     hm = getattr(ctx, 'hessian_node', None)
     if hm is None:

@@ -62,7 +62,11 @@ void launch_jet_mix(dim3 grid, hipStream_t st, const float* ws, const float* x, 
                     float w, float* spill, float* abuf, float* dbuf, int64_t n_pad);
 void launch_jet_quad(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* G,
                      const float* u, float* gx, float* gu, int d, int o, int lh, float w0, float w, float* spill,
-                     float* abuf, float* dbuf, int64_t n_pad);
+                     float* abuf, float* dbuf, int64_t n_pad, const float* kept = nullptr);
+// tu_hess.hip: the Hessian node's forward, Hm (n, d, d) = sum_j u_j H_j (d <= 2) in one 6-stream forward jet sweep
+// (grid = hess_groups(n) / 4 workgroups); kept (nullable) receives the per-layer jets for launch_jet_quad
+void launch_hess(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* u, int d, int o,
+                 int lh, float w0, float w, float* hm, float* kept);
 void launch_small_mix(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* v,
                       const float* g, const float* u, int64_t n, int64_t n_pad, int64_t tps, float* eslab, int64_t E,
                       int d, int o, int lh, int h);

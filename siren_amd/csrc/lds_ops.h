@@ -173,4 +173,40 @@ __device__ __forceinline__ void slice_mma2_mid(unsigned vaddr, unsigned vnext, c
     slice_singles2_mid<0, NBLK, MID, NEXT>(vaddr, vnext, bp, bt, accp, acct, a, o, mid);
 }
 
+// three column tiles sharing every A operand (hess_kernel.hpp: 8 coordinates x 6 Hessian-jet streams): 12 MFMAs per
+// block read, K-step-major so a dependent MFMA is two MFMAs (64 cycles) behind; otherwise slice_singles2_mid
+template <int OB, int NBLK, int MID, bool NEXT, class Mid>
+__device__ __forceinline__ void slice_singles3_mid(unsigned vaddr, unsigned vnext, const f32x4& b0, const f32x4& b1,
+                                                   const f32x4& b2, f32x4 (&acc)[3][NBLK], f32x4 a, f32x4& o,
+                                                   Mid& mid) {
+    constexpr bool last = OB + 1 == NBLK;
+    if constexpr (OB == MID) mid();
+    f32x4 nx;
+    if constexpr (!last) {
+        nx = lds_read4<(OB + 1) * 1024>(vaddr);
+        lgkm_wait1<1>(a);
+    } else if constexpr (NEXT) {
+        nx = lds_read4<0>(vnext);
+        lgkm_wait1<1>(a);
+    } else {
+        lgkm_wait1<0>(a);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        acc[0][OB] = mfma4(a[r], b0[r], acc[0][OB]);
+        acc[1][OB] = mfma4(a[r], b1[r], acc[1][OB]);
+        acc[2][OB] = mfma4(a[r], b2[r], acc[2][OB]);
+    }
+    if constexpr (!last) {
+        slice_singles3_mid<OB + 1, NBLK, MID, NEXT>(vaddr, vnext, b0, b1, b2, acc, nx, o, mid);
+    } else if constexpr (NEXT) {
+        o = nx;
+    }
+}
+template <int NBLK, int MID, bool NEXT, class Mid>
+__device__ __forceinline__ void slice_mma3_mid(unsigned vaddr, unsigned vnext, const f32x4& b0, const f32x4& b1,
+                                               const f32x4& b2, f32x4 (&acc)[3][NBLK], f32x4 a, f32x4& o, Mid&& mid) {
+    slice_singles3_mid<0, NBLK, MID, NEXT>(vaddr, vnext, b0, b1, b2, acc, a, o, mid);
+}
+
 }  // namespace siren

@@ -1,5 +1,6 @@
 // siren_capi.hip — the C ABI of libsiren_amd.so (include/siren_amd.h): validation, workspace sizing and
 // dispatch to the kernel launchers (launch.h; one translation unit per kernel family).
+#include "hess_kernel.hpp"
 #include "launch.h"
 #include "siren_common.h"
 #include "siren_params.h"
@@ -791,8 +792,34 @@ int32_t siren_hessian_backward_ws_floats(const siren_cfg* cfg, int64_t n, int64_
     return SIREN_OK;
 }
 
+// ---- the Hessian node's forward: Hm (n, d, d) = sum_j u_j H_j in one 6-stream forward jet (hess_kernel.hpp) -----
+int32_t siren_hessian_ws_floats(const siren_cfg* cfg, int64_t n, int32_t keep, int64_t* count) {
+    if (int rc = check_quad(cfg)) return rc;
+    if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
+    *count = keep ? siren::hess_groups(n) * 8 * (int64_t)(cfg->n_hidden + 1) * 6 * siren::H : 0;
+    return SIREN_OK;
+}
+
+int32_t siren_hessian(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* u, float* kept,
+                      float* hm, void* stream) {
+    if (int rc = check_quad(cfg)) return rc;
+    if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    if (n == 0) return SIREN_OK;
+    if (ws == nullptr || x == nullptr || hm == nullptr) return fail(SIREN_EINVAL, "ws/x/hm is NULL");
+    if (n > (int64_t)0x7fffffff * 8) return fail(SIREN_EINVAL, "n exceeds the grid");
+    siren::launch_hess(dim3((unsigned)(siren::hess_groups(n) / siren::WAVES)), (hipStream_t)stream, ws, x, n, u,
+                       cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, hm, kept);
+    return hip_status("siren_hessian");
+}
+
 int32_t siren_hessian_backward(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* G,
                                const float* u, float* tws, float* gx, float* gparams, float* gu, void* stream) {
+    return siren_hessian_backward_kept(cfg, ws, x, n, G, u, nullptr, tws, gx, gparams, gu, stream);
+}
+
+int32_t siren_hessian_backward_kept(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* G,
+                                    const float* u, const float* kept, float* tws, float* gx, float* gparams,
+                                    float* gu, void* stream) {
     if (int rc = check_quad(cfg)) return rc;
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
     const JetPlan plan(cfg, n);
@@ -809,7 +836,7 @@ int32_t siren_hessian_backward(const siren_cfg* cfg, const float* ws, const floa
     float* spill = dbuf + plan.buf_floats;
     float* partial = spill + plan.buf_floats;
     siren::launch_jet_quad(dim3((unsigned)(plan.n_pad / 16)), st, ws, x, n, G, u, gx, gu, cfg->d_in, cfg->d_out,
-                           cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, spill, abuf, dbuf, plan.n_pad);
+                           cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, spill, abuf, dbuf, plan.n_pad, kept);
     if (int rc = hip_status("siren_hessian_backward (quadratic-form jet)")) return rc;
     if (gparams == nullptr) return SIREN_OK;
     siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden), st, abuf, dbuf, plan.cols, plan.tps,

@@ -1,0 +1,15 @@
+// tu_hess.hip — the Hessian node's forward (hess_kernel.hpp).
+#include "hess_kernel.hpp"
+#include "launch.h"
+
+namespace siren {
+
+void launch_hess(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* u, int d, int o,
+                 int lh, float w0, float w, float* hm, float* kept) {
+    if (kept != nullptr)
+        hipLaunchKernelGGL(hess_kernel<true>, grid, dim3(THREADS), 0, st, ws, x, n, u, d, o, lh, w0, w, hm, kept);
+    else
+        hipLaunchKernelGGL(hess_kernel<false>, grid, dim3(THREADS), 0, st, ws, x, n, u, d, o, lh, w0, w, hm, kept);
+}
+
+}  // namespace siren

@@ -237,20 +237,34 @@ class SirenEngine:
         return (self.supported and c.hidden == 256 and 1 <= c.n_hidden <= 5 and c.d_in <= 2
                 and bool(c.outermost_linear))
 
-    def hessian(self, ws, x, u=None):
-        """Hm (n, d_in, d_in) = sum_j u_j H_j(x) (u (n, d_out), None = ones): column i = the x-part of the W3 sweep
-        along e_i (second_order with want_theta=False), one launch per input dimension."""
-        n, d = x.shape[0], self.cfg.d_in
+    def hessian(self, ws, x, u=None, keep=False):
+        """Hm (n, d_in, d_in) = sum_j u_j H_j(x) (u (n, d_out), None = ones) in one forward-mode second-order jet
+        sweep (siren_hessian). keep=True also returns the per-layer jets (n-proportional fp32 buffer) that
+        hessian_backward(..., kept=) reads instead of recomputing its forward: (hm, kept)."""
+        self._require()
+        if not self.hessian_backward_supported:
+            raise _lib.SirenUnsupported('siren_hessian covers hidden 256, 1..5 hidden layers, in_features <= 2, '
+                                        'linear output')
+        x = self._check_x(x)
+        n, d, o = x.shape[0], self.cfg.d_in, self.cfg.d_out
+        if u is not None and (u.numel() != n * o or u.dtype != torch.float32 or u.device != x.device):
+            raise ValueError('u must be fp32 (%d, %d) on %s' % (n, o, x.device))
+        u = u.contiguous() if u is not None else None
         hm = torch.empty(n, d, d, dtype=torch.float32, device=x.device)
-        for i in range(d):
-            v = torch.zeros(n, d, dtype=torch.float32, device=x.device)
-            v[:, i] = 1.
-            hm[:, :, i] = self.second_order(ws, x, v, want_theta=False, u=u)[0]
-        return hm
+        kept = None
+        if keep:
+            cnt = ctypes.c_int64()
+            _lib.check(self.lib.siren_hessian_ws_floats(ctypes.byref(self.cfg), n, 1, ctypes.byref(cnt)),
+                       'siren_hessian_ws_floats')
+            kept = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_hessian(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(u), _ptr(kept), _ptr(hm),
+                                          _stream(x.device)), 'siren_hessian')
+        return (hm, kept) if keep else hm
 
-    def hessian_backward(self, ws, x, G, u=None, want_theta=True, want_u=False):
-        """The backward of the Hessian node: d/d(x, theta, u) of sum_c <G_c, Hm_c> (siren_hessian_backward).
-        Returns (gx, gparams | None, gu | None)."""
+    def hessian_backward(self, ws, x, G, u=None, want_theta=True, want_u=False, kept=None):
+        """The backward of the Hessian node: d/d(x, theta, u) of sum_c <G_c, Hm_c> (siren_hessian_backward; with
+        kept = hessian(ws, x, u, keep=True)[1] of the same inputs, siren_hessian_backward_kept skips the forward
+        GEMMs). Returns (gx, gparams | None, gu | None)."""
         self._require()
         if not self.hessian_backward_supported:
             raise _lib.SirenUnsupported('siren_hessian_backward covers hidden 256, 1..5 hidden layers, in_features '
@@ -270,9 +284,15 @@ class SirenEngine:
         gx = torch.empty(n, d, dtype=torch.float32, device=x.device)
         gp = torch.empty(self.param_count, dtype=torch.float32, device=x.device) if want_theta else None
         gu = torch.empty(n, o, dtype=torch.float32, device=x.device) if want_u else None
-        _lib.check(self.lib.siren_hessian_backward(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(G), _ptr(u),
-                                                   _ptr(tws), _ptr(gx), _ptr(gp), _ptr(gu), _stream(x.device)),
-                   'siren_hessian_backward')
+        if kept is not None:
+            cnt = ctypes.c_int64()
+            _lib.check(self.lib.siren_hessian_ws_floats(ctypes.byref(self.cfg), n, 1, ctypes.byref(cnt)),
+                       'siren_hessian_ws_floats')
+            if kept.numel() != cnt.value or kept.dtype != torch.float32 or kept.device != x.device:
+                raise ValueError('kept must be the fp32 buffer of hessian(..., keep=True) for these %d points' % n)
+        _lib.check(self.lib.siren_hessian_backward_kept(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(G), _ptr(u),
+                                                        _ptr(kept), _ptr(tws), _ptr(gx), _ptr(gp), _ptr(gu),
+                                                        _stream(x.device)), 'siren_hessian_backward_kept')
         return gx, gp, gu
 
     def forward_laplace(self, ws, x, want_y=False, want_gx=False):

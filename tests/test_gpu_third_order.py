@@ -270,10 +270,18 @@ def test_hessian_backward_vs_fp64(cuda, n, d, L, o, weighted):
     assert np.max(np.abs(gu.cpu().numpy() - rgu)) <= 1e-4 * max(1e-6, np.max(np.abs(rgu)))
     gx2, none_p, none_u = eng.hessian_backward(ws, to_dev(x, cuda), to_dev(G, cuda), ud, want_theta=False)
     assert none_p is None and none_u is None and torch.equal(gx, gx2)
-    if not eng.second_order_supported:  # the node's forward runs on the W3 kernel (1..3 hidden layers)
-        return
-    # the node's forward: Hm[:, :, i] = sum_j u_j H_j e_i
-    hm = eng.hessian(ws, to_dev(x, cuda), ud).cpu().numpy()
+    # the node's forward (siren_hessian, one 6-stream jet sweep): Hm[:, :, i] = sum_j u_j H_j e_i; with its kept
+    # jets the backward skips its forward GEMMs (siren_hessian_backward_kept) — same bar against fp64
+    hm0 = eng.hessian(ws, to_dev(x, cuda), ud)
+    hmk, kept = eng.hessian(ws, to_dev(x, cuda), ud, keep=True)
+    assert torch.equal(hm0, hmk) and torch.isfinite(kept).all()
+    kx, kp, ku = eng.hessian_backward(ws, to_dev(x, cuda), to_dev(G, cuda), ud, want_theta=True, want_u=True,
+                                      kept=kept)
+    assert np.max(np.abs(kp.cpu().numpy() - rgp)) <= 1e-4 * np.max(np.abs(rgp))
+    assert np.max(np.abs(kx.cpu().numpy() - rgx)) <= 1e-4 * max(1e-6, np.max(np.abs(rgx)))
+    assert np.max(np.abs(ku.cpu().numpy() - rgu)) <= 1e-4 * max(1e-6, np.max(np.abs(rgu)))
+    hm = hm0.cpu().numpy()
+    assert np.array_equal(hm, np.swapaxes(hm, 1, 2))  # symmetric by construction (H_12 written twice)
     xt = torch.tensor(x, dtype=torch.float64, requires_grad=True)
     params = [torch.tensor(t, dtype=torch.float64) for W, b in layers for t in (W, b)]
     y = O.torch_forward(xt, params)
@@ -284,6 +292,24 @@ def test_hessian_backward_vs_fp64(cuda, n, d, L, o, weighted):
         e[:, i] = 1.
         ref = torch.autograd.grad(Ju, xt, e, retain_graph=True)[0].numpy()
         assert np.max(np.abs(hm[:, :, i] - ref)) <= 1e-4 * max(1., np.max(np.abs(ref)))
+
+
+def test_hessian_node_forward_matches_w3_axes(cuda):
+    """siren_hessian (forward-mode 6-stream jet) against the W3 reverse-over-forward sweep along each axis (the
+    node's previous forward): two independent second-order methods agree to fp32 rounding."""
+    from siren_amd.engine import SirenEngine
+    for n, d, L, o, weighted in [(5000, 2, 3, 1, False), (77, 1, 2, 2, True), (1031, 2, 1, 3, True)]:
+        layers = random_layers(d, L, o, seed=n)
+        eng = SirenEngine(d, 256, L, o)
+        ws = eng.pack(to_dev(O.flatten(layers), cuda))
+        x = (torch.rand(n, d, device=cuda) * 2 - 1)
+        u = torch.randn(n, o, device=cuda) if weighted else None
+        hm = eng.hessian(ws, x, u)
+        for i in range(d):
+            v = torch.zeros(n, d, device=cuda)
+            v[:, i] = 1.
+            col = eng.second_order(ws, x, v, want_theta=False, u=u)[0]
+            assert (hm[:, :, i] - col).abs().max() <= 2e-5 * max(1., float(col.abs().max())), (n, d, i)
 
 
 def test_reference_recipe_runs_one_hessian_backward(cuda, monkeypatch):
