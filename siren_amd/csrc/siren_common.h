@@ -292,16 +292,17 @@ __device__ __forceinline__ float sin_phase(float t) {
 // (blocks b and b + 8 share one; MI355X_MICROARCH.md, workgroup dispatch — observed placement, used for speed only),
 // so the linear block id is renumbered XCD-major: the blocks of one XCD take consecutive (element, x) slots, an XCD
 // works through its elements one or two at a time, and its 4 MiB L2 holds those elements' weight streams instead of
-// a slice of every element's. Identity when the grid is not a multiple of 8 blocks.
+// a slice of every element's.
+// XCD-major slot of linear block L in a grid of `total` blocks: XCD x holds blocks x, x + 8, ... (k + 1 of them for
+// x < r, k otherwise, total = 8 k + r), and they take the consecutive slots prefix(x) + L / 8 — a bijection for any
+// total (a group of consecutive slots straddles two XCDs only at the 8 XCD boundaries).
+__device__ __forceinline__ unsigned xcd_slot(unsigned L, unsigned total) {
+    const unsigned x = L % 8u, k = total / 8u, r = total % 8u;
+    return x * k + (x < r ? x : r) + L / 8u;
+}
 __device__ __forceinline__ void xcd_remap(unsigned& bx, unsigned& by) {
     const unsigned gx = gridDim.x, total = gridDim.x * gridDim.y;
-    if (total % 8u != 0u) {
-        bx = blockIdx.x;
-        by = blockIdx.y;
-        return;
-    }
-    const unsigned L = blockIdx.x + blockIdx.y * gx;
-    const unsigned q = (L % 8u) * (total / 8u) + L / 8u;
+    const unsigned q = xcd_slot(blockIdx.x + blockIdx.y * gx, total);
     by = q / gx;
     bx = q % gx;
 }

@@ -66,16 +66,13 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
         // XCDs; MI355X_MICROARCH.md) and run together, so each half comes from HBM once and is re-read from that
         // XCD's L2 (the quadrant-major grid re-read every half from HBM: traffic 2x the tiles)
         const unsigned total = gridDim.x * gridDim.y * gridDim.z;
-        if (total % 8u == 0u) {
-            const unsigned L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-            unsigned q = (L % 8u) * (total / 8u) + L / 8u;
-            const unsigned quad = q % (unsigned)nq;
-            q /= (unsigned)nq;
-            s = (int)(q % gridDim.x);
-            q /= gridDim.x;
-            ly = (int)(q % gridDim.y);
-            zz = (int)((q / gridDim.y) * nq + quad);
-        }
+        unsigned q = xcd_slot(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), total);
+        const unsigned quad = q % (unsigned)nq;
+        q /= (unsigned)nq;
+        s = (int)(q % gridDim.x);
+        q /= gridDim.x;
+        ly = (int)(q % gridDim.y);
+        zz = (int)((q / gridDim.y) * nq + quad);
     }
     const int l = ly + 1;
     const int qz = zz % nq, bz = zz / nq;

@@ -36,7 +36,8 @@ def plan(path):
     if path == 'hypernet':
         n = 4096
     n_pad = (n + (15 if jet else 63)) // (16 if jet else 64) * (16 if jet else 64)
-    cols = 4 * n_pad if jet else n_pad
+    # jet paths: 4 streams per coordinate; w3_wide: the two-stream (value, tangent) tiles of the hidden-512 W3
+    cols = 4 * n_pad if jet else (2 * n_pad if path == 'w3_wide' else n_pad)
     tiles = cols // 16
     want = max(1, 256 // (L * (H // 256) ** 2))
     if path == 'hypernet':
@@ -55,8 +56,8 @@ def io_bytes(path, k):
     T = H * 4  # one layer's tile bytes per column
     hid = L * (H * H + H)
     if k.startswith('wgrad_kernel'):   # a_{l-1} and delta_l tiles of the hidden layers, S hidden-layer slabs
-        per = 2 * L * cols * T + S * hid * 4
-        return B * per if path != 'w3_theta' and path != 'sdf' else None
+        per = 2 * L * cols * T + S * hid * 4   # (w3_theta / sdf: one of the two launches, (A, D) or (At, Dt))
+        return B * per
     if k.startswith('edge_kernel'):    # delta_0 / a_L rows + the coordinate scalars, S edge slabs
         return B * (2 * cols * T + S * (P - hid) * 4) if path not in ('w3_theta', 'sdf') else None
     if k.startswith('reduce_kernel'):  # the slabs once, the gradient once
@@ -65,6 +66,12 @@ def io_bytes(path, k):
         return 2 * (L + 1) * cols * T + n * (d + 1) * 4
     if k.startswith('jet_store_kernel<2'):   # JET_REV: z-jets read, zb-jets written
         return 2 * (L + 1) * cols * T
+    if k.startswith('hess_kernel<true'):  # the Hessian node's forward: x read, the kept 6-stream jets and Hm written
+        return 6 * (L + 1) * n_pad * T + n * (d + d * d) * 4
+    if k.startswith('hess_kernel'):
+        return n * (d + d * d) * 4
+    if k.startswith('jet_store_kernel<0,true,true,true'):  # reverse-only QG jet: kept jets read, a- and zb-jets written
+        return 6 * (L + 1) * n_pad * T + 2 * (L + 1) * cols * T + n * (d + d * d) * 4
     if k.startswith('jet_store_kernel<0,true'):  # mixed jet (both phases): a-, z-, zb-jets
         return 3 * (L + 1) * cols * T + n * 3 * d * 4
     if k.startswith('lay_'):  # layered path epilogues, per 16384-coordinate chunk (layered.hip)
