@@ -54,6 +54,9 @@ enum {
 #define SIREN_FLAG_LEGACY_KERNEL 1
 /* cfg.reserved flag (benchmarking only): one workgroup per coordinate tile instead of the persistent grid. */
 #define SIREN_FLAG_NO_PERSIST 2
+/* cfg.reserved flag (benchmarking only): the round-2 second-order kernel whose epilogues run between the GEMMs
+ * (w3_kernel) instead of the interleaved one (w3i_kernel). Same results. */
+#define SIREN_FLAG_W3_SERIAL 4
 
 /* Network description. Mirrors SingleBVPNet(out_features, type='sine', in_features, mode='mlp',
  * hidden_features, num_hidden_layers) (modules.py:122-123) and the notebook Siren(in_features,

@@ -89,7 +89,19 @@ void launch_w3(bool theta, dim3 grid, hipStream_t st, const float* ws, const flo
                const float* u, float* ydot, int o, int64_t n, float* gx, float* spill, float* A, float* At, float* D,
                float* Dt, int64_t n_pad, int d, int lh, float w0, float w, const float* kA = nullptr,
                const float* kC = nullptr, unsigned long long* prof = nullptr, int64_t ws_bs = 0, int64_t spill_bs = 0,
-               int64_t buf_bs = 0);
+               int64_t buf_bs = 0, bool serial = false);
+// tu_w3i_*.hip: the interleaved W3 (w3i_kernel.hpp), one translation unit per (THETA, KEPT); launch_w3 dispatches to
+// them unless serial (SIREN_FLAG_W3_SERIAL A/B, or a phase profile, which only w3_kernel records)
+#define SIREN_W3I_DECL(TK)                                                                                             \
+    void launch_w3i_##TK(dim3 grid, hipStream_t st, const float* ws, const float* x, const float* v, const float* gy, \
+                         const float* u, float* ydot, int o, int64_t n, float* gx, float* spill, float* A, float* At, \
+                         float* D, float* Dt, int64_t n_pad, int d, int lh, float w0, float w, const float* kA,         \
+                         const float* kC, int64_t ws_bs, int64_t spill_bs, int64_t buf_bs);
+SIREN_W3I_DECL(tt)
+SIREN_W3I_DECL(tf)
+SIREN_W3I_DECL(ft)
+SIREN_W3I_DECL(ff)
+#undef SIREN_W3I_DECL
 void launch_small_w3(dim3 grid, hipStream_t st, const float* At, const float* D, const float* Dt, const float* AL,
                      const float* x, const float* v, const float* gy, const float* u, int64_t n, int64_t n_pad, int64_t tps,
                      float* eslab, int64_t E, int d, int o, int lh, int64_t bstride_act = 0, int64_t bstride_e = 0);

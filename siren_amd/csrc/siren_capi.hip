@@ -966,7 +966,8 @@ static int32_t second_order_impl(const siren_cfg* cfg, const float* ws, const fl
     }
     const dim3 grid((unsigned)(plan.n_pad / siren::TILE));
     siren::launch_w3(theta, grid, st, ws, x, v, gy, u, ydot, cfg->d_out, n, gx, spill, A, At, D, Dt, plan.n_pad,
-                     cfg->d_in, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, kA, kC, g_w3_prof);
+                     cfg->d_in, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, kA, kC, g_w3_prof, 0, 0, 0,
+                     (cfg->reserved & SIREN_FLAG_W3_SERIAL) != 0);
     if (int rc = hip_status("siren_second_order (w3)")) return rc;
     if (!theta) return SIREN_OK;
     const dim3 wgrid((unsigned)plan.splits, (unsigned)cfg->n_hidden);
@@ -1187,7 +1188,8 @@ int32_t siren_second_order_batched(const siren_cfg* cfg, const float* ws, const 
         float* partial = Dt + batch * plan.buf_floats;
         siren::launch_w3(theta, dim3((unsigned)(plan.n_pad / siren::TILE), (unsigned)batch), st, ws, x, v, gy, u, ydot,
                          o, n, gx, spill, A, At, D, Dt, plan.n_pad, d, cfg->n_hidden, cfg->omega_first,
-                         cfg->omega_hidden, nullptr, nullptr, nullptr, W, plan.spill_floats, plan.buf_floats);
+                         cfg->omega_hidden, nullptr, nullptr, nullptr, W, plan.spill_floats, plan.buf_floats,
+                         (cfg->reserved & SIREN_FLAG_W3_SERIAL) != 0);
         if (int rc = hip_status("siren_second_order_batched (grouped w3)")) return rc;
         if (!theta) return SIREN_OK;
         const dim3 wgrid((unsigned)plan.splits, (unsigned)cfg->n_hidden, (unsigned)batch);

@@ -314,6 +314,13 @@ __device__ __forceinline__ float sum_groups(float v) {
     return v;
 }
 
+// s * v + z with one rounding per element (an explicit fma chain: hipcc's contraction of a*b + c*d may fuse either
+// product, which made two kernels with the same arithmetic differ in the last bit)
+__device__ __forceinline__ f32x4 fma4(float s, const f32x4& v, const f32x4& z) {
+    return f32x4{__builtin_fmaf(s, v[0], z[0]), __builtin_fmaf(s, v[1], z[1]), __builtin_fmaf(s, v[2], z[2]),
+                 __builtin_fmaf(s, v[3], z[3])};
+}
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }

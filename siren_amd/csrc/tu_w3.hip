@@ -9,7 +9,23 @@ namespace siren {
 void launch_w3(bool theta, dim3 grid, hipStream_t st, const float* ws, const float* x, const float* v, const float* gy,
                const float* u, float* ydot, int o, int64_t n, float* gx, float* spill, float* A, float* At, float* D,
                float* Dt, int64_t n_pad, int d, int lh, float w0, float w, const float* kA, const float* kC,
-               unsigned long long* prof, int64_t ws_bs, int64_t spill_bs, int64_t buf_bs) {
+               unsigned long long* prof, int64_t ws_bs, int64_t spill_bs, int64_t buf_bs, bool serial) {
+    const bool kept = kA != nullptr && kC != nullptr;
+    if (!serial && prof == nullptr) {
+#define SIREN_I(TK)                                                                                                 \
+    launch_w3i_##TK(grid, st, ws, x, v, gy, u, ydot, o, n, gx, spill, A, At, D, Dt, n_pad, d, lh, w0, w, kA, kC, ws_bs, \
+                    spill_bs, buf_bs)
+        if (theta && kept)
+            SIREN_I(tt);
+        else if (theta)
+            SIREN_I(tf);
+        else if (kept)
+            SIREN_I(ft);
+        else
+            SIREN_I(ff);
+#undef SIREN_I
+        return;
+    }
 #define SIREN_L(LHV, TH, KP)                                                                                    \
     hipLaunchKernelGGL((w3_kernel<LHV, TH, KP>), grid, dim3(THREADS), 0, st, ws, x, v, gy, u, ydot, o, n, gx, spill, A, \
                        At, D, Dt, n_pad, d, w0, w, kA, kC, prof, ws_bs, spill_bs, buf_bs)
@@ -19,7 +35,6 @@ void launch_w3(bool theta, dim3 grid, hipStream_t st, const float* ws, const flo
         case 2: SIREN_L(2, TH, KP); break; \
         default: SIREN_L(3, TH, KP); break; \
     }
-    const bool kept = kA != nullptr && kC != nullptr;
     if (theta && kept) {
         SIREN_LH(true, true);
     } else if (theta) {

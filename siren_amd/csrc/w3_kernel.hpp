@@ -183,8 +183,9 @@ __global__ __launch_bounds__(THREADS, 1) void w3_kernel(const float* __restrict_
         for (int k = 0; k < MAXD; ++k) {
             if (k < d) {
                 const f32x4 wk = *(const f32x4*)(sm + SM_W0 + k * H + nb);
-                zx = k == 0 ? xv[0] * wk : zx + xv[k] * wk;
-                zd = zd + vv[k] * wk;
+                // explicit fma chain (w3i_kernel's FIRST epilogue runs the same one over all MAXD rows)
+                zx = k == 0 ? xv[0] * wk : fma4(xv[k], wk, zx);
+                zd = fma4(vv[k], wk, zd);
             }
         }
         z = zx + z;

@@ -1,6 +1,7 @@
 """Static race check on the compiled kernels (no GPU): every translation unit whose kernels read LDS by inline asm
 (or pipeline LDS loads across MFMAs) is compiled for gfx950 to ISA, and tools/check_asm_waits.py verifies that no
-instruction reads, copies or overwrites a register of an LDS load before the s_waitcnt lgkmcnt that retires it.
+instruction reads, copies or overwrites a register of an LDS load before the s_waitcnt lgkmcnt that retires it, or
+of a vector-memory load before its s_waitcnt vmcnt (the saddr-form asm reloads of the W1 REV and W3i epilogues).
 hipcc does not count inline-asm loads, so a register copy it inserts ahead of a hand-placed wait reads stale data
 on some waves and launches only (found this way in the W1 tile seam, the wgrad reload and the first split-W1 build).
 """
@@ -16,7 +17,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, 'siren_amd', 'csrc')
 TUS = ['tu_w1.hip', 'tu_w0.hip', 'tu_w4.hip', 'tu_w3.hip', 'tu_wide.hip', 'tu_jet.hip', 'tu_wide_jet.hip',
-       'tu_train.hip', 'tu_w1x.hip']
+       'tu_train.hip', 'tu_w1x.hip', 'tu_hess.hip', 'tu_w3i_tt.hip', 'tu_w3i_tf.hip', 'tu_w3i_ft.hip', 'tu_w3i_ff.hip']
 
 sys.path.insert(0, os.path.join(ROOT, 'tools'))
 
@@ -46,7 +47,8 @@ def test_no_read_of_inflight_lds_load_registers():
             for nm in re.findall(r'\n(_Z\w+):', s):
                 i = s.find('\n' + nm + ':')
                 j = s.find('.Lfunc_end', i)
-                probs = C.check(s[i:j].split('\n'), nm)
+                body = s[i:j].split('\n')
+                probs = C.check(body, nm) + C.check_vmem(body, nm)
                 if probs:
                     bad.append('%s %s: %d (first: %s)' % (tu, nm, len(probs), probs[0][1]))
         assert not bad, '\n'.join(bad)

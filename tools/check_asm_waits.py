@@ -72,6 +72,49 @@ def check(body, name):
     return problems
 
 
+VMEM = ('global_', 'buffer_', 'scratch_')
+
+
+def check_vmem(body, name):
+    """The same walk for vector-memory loads (the saddr-form asm loads of w1_kernel's REV cos prefetch and
+    w3i_kernel's epilogue reloads): every global_/buffer_/scratch_ op counts in vmcnt in issue order (stores and
+    LDS-DMA loads too, with no register destination), s_waitcnt vmcnt(N) keeps the N youngest outstanding, and an
+    instruction that touches a load's destination before the wait that retires it is reported."""
+    pending = []
+    problems = []
+    for no, line in enumerate(body):
+        t = line.split(';')[0].strip()
+        if not t or t.endswith(':') or t.startswith('.'):
+            if t.endswith(':'):
+                pending = []
+            continue
+        op = t.split()[0]
+        if op == 's_waitcnt':
+            m = re.search(r'vmcnt\((\d+)\)', t)
+            if m:
+                keep = int(m.group(1))
+                pending = pending[len(pending) - keep:] if 0 < keep < len(pending) else ([] if keep == 0 else pending)
+            continue
+        if op.startswith('s_'):
+            continue
+        operands = t[len(op):]
+        if op.startswith(VMEM):
+            parts = operands.split(',')
+            is_load = '_load' in op and '_lds' not in op
+            dst = regs(parts[0]) if is_load else set()
+            src = regs(','.join(parts[1:])) if is_load else regs(operands)
+            for ln, rs in pending:
+                if rs & (dst | src):
+                    problems.append((no, t, ln))
+            pending.append((no, dst))
+            continue
+        used = regs(operands)
+        for ln, rs in pending:
+            if rs & used:
+                problems.append((no, t, ln))
+    return problems
+
+
 def main():
     path = sys.argv[1]
     want = sys.argv[2] if len(sys.argv) > 2 else ''
@@ -84,8 +127,8 @@ def main():
         i = s.find('\n' + nm + ':')
         j = s.find('.Lfunc_end', i)
         body = s[i:j].split('\n')
-        probs = check(body, nm)
-        print('%-70s %d reads of in-flight LDS-load registers' % (nm[:70], len(probs)))
+        probs = check(body, nm) + check_vmem(body, nm)
+        print('%-70s %d reads of in-flight load registers' % (nm[:70], len(probs)))
         for no, t, ln in probs[:8]:
             print('    line %d: %s   (load at line %d: %s)' % (no, t, ln, body[ln].strip()))
         bad += len(probs)
