@@ -29,6 +29,8 @@
 //     pair, counted lgkmcnt waits: w1_kernel's slice machinery (ring_issue4, lds_read4, lgkm_wait).
 #pragma once
 #include "w1_kernel.hpp"
+// W3I_EXP: timing probes for tools/variant_build.sh (results numerically meaningless when set): 1 no reloads, 2 no tile
+// stores, 4 no spill stores, 16 no per-slice scheduling barrier, 32 mid-slice waits that do not count the epilogue ops
 #ifndef W3I_EXP
 #define W3I_EXP 0
 #endif
@@ -127,9 +129,12 @@ __device__ __forceinline__ const char* w3_at(const char* base, int64_t off) {
     asm volatile("" : "+s"(base));
     return base + off;
 }
+// The s_nop after a 16-byte store: a VALU may not overwrite a store's data VGPRs in the next two wait states (the
+// store reads them late; gfx940+ store-data hazard). hipcc inserts those for its own stores, not for inline asm — without
+// it the coordinates of lanes 12..15 of every 16-lane row came back wrong once the allocator reused a stored register.
 __device__ __forceinline__ void w3_store16(const char* base, unsigned voff, const f32x4& v) {
     if (W3I_EXP & 4) return;
-    asm volatile("global_store_dwordx4 %0, %1, %2" ::"v"(voff), "v"(v), "s"(base));
+    asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" ::"v"(voff), "v"(v), "s"(base));
 }
 // A block of the wgrad tile layout (element (neuron 16 rb + 4 g + r, coordinate c) at rb 256 + neuron 16 + c, what
 // store_block writes as four dword stores of 64 B pieces) goes out as ONE coalesced 1 KiB global_store_dwordx4: the
@@ -157,7 +162,8 @@ __device__ __forceinline__ void w3_stage_store(const char* base, const f32x4& v,
         "ds_write_b32 %1, %5 offset:240\n\t"
         "ds_read_b128 %0, %6\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
-        "global_store_dwordx4 %7, %0, %8"
+        "global_store_dwordx4 %7, %0, %8\n\t"
+        "s_nop 1"
         : "=&v"(t)
         : "v"(tw), "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(tr), "v"(voff), "s"(base));
 }
@@ -183,9 +189,6 @@ template <int E, int LH, bool THETA, bool KEPT>
 __device__ __forceinline__ void w3_reload_issue(W3iState<LH>& st, const W3iCtx& cx) {
     constexpr int G = E / NB, B = E % NB;
     constexpr int KIND = w3_epi_kind<G, LH>();
-#ifndef W3I_EXP
-#define W3I_EXP 0
-#endif
     if constexpr (G < 2 * LH && w3_reloads<KIND, KEPT>() && !(W3I_EXP & 1)) {
         constexpr int M = KIND == W3E_REV ? 2 * LH - G : G;  // the layer whose forward values are reloaded
         if constexpr (KEPT)
@@ -456,16 +459,6 @@ __device__ __forceinline__ void w3i_slice(W3iState<LH>& st, const W3iCtx& cx) {
 template <int G, int LH, bool THETA, bool KEPT>
 __device__ __forceinline__ void w3i_gemm(W3iState<LH>& st, const W3iCtx& cx) {
     constexpr int KIND = w3_epi_kind<G, LH>();
-    if constexpr (G > 0 && !(W3I_EXP & 8)) {
-        // GEMM G-1's output moves to VGPRs for its epilogue (from_agpr), so the accumulator half of the register file
-        // holds one accumulator set (2 x 64 registers) instead of two
-        constexpr bool TWO_PREV = w3_streams<G - 1, LH, KEPT>() == 2;
-#pragma unroll
-        for (int ob = 0; ob < NB; ++ob) {
-            if constexpr (TWO_PREV) st.accp[(G + 1) & 1][ob] = from_agpr(st.accp[(G + 1) & 1][ob]);
-            st.acct[(G + 1) & 1][ob] = from_agpr(st.acct[(G + 1) & 1][ob]);
-        }
-    }
 #pragma unroll
     for (int ob = 0; ob < NB; ++ob) {
         st.accp[G & 1][ob] = f32x4{0.f, 0.f, 0.f, 0.f};

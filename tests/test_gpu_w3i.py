@@ -88,19 +88,23 @@ def test_w3i_vs_fp64(cuda):
     assert np.max(np.abs(gp.cpu().numpy() - rgp)) <= 1e-4 * np.max(np.abs(rgp))
 
 
-@pytest.mark.parametrize('L', [1, 3])
-def test_w3i_grouped_bitwise(cuda, L):
-    """The grouped launch over batched weights (siren_second_order_batched, grid.y = element)."""
-    d, o, B, n = 2, 1, 5, 777
+@pytest.mark.parametrize('L,B,n', [(1, 5, 777), (3, 5, 777), (3, 3, 512), (2, 2, 64), (3, 4, 100)])
+def test_w3i_grouped_bitwise(cuda, L, B, n):
+    """The grouped launch over batched weights (siren_second_order_batched, grid.y = element), with and without the
+    output weighting u, the seed gy and ydot (the batched HVP node's forward is want_theta=False with u)."""
+    d, o = 2, 1
     ei, es = engines(d, L, o)
     flats = torch.stack([to_dev(O.flatten(random_layers(d, L, o, seed=40 + b)), cuda) for b in range(B)])
     wi, wsr = ei.pack_batched(flats, full=True), es.pack_batched(flats, full=True)
-    rng = np.random.default_rng(L)
+    rng = np.random.default_rng(L + n)
     x = to_dev(rng.uniform(-1, 1, (B, n, d)), cuda)
     v = to_dev(rng.normal(size=(B, n, d)), cuda)
+    u = to_dev(rng.normal(size=(B, n, o)), cuda)
+    gy = to_dev(rng.normal(size=(B, n, o)), cuda)
     for theta in (False, True):
-        ri = ei.second_order_batched(wi, x, v, want_theta=theta)
-        rs = es.second_order_batched(wsr, x, v, want_theta=theta)
-        for k, (a, b) in enumerate(zip(ri, rs)):
-            if a is not None:
-                same(a, b, 'grouped L%d theta %s output %d' % (L, theta, k))
+        for kw in ({}, {'u': u}, {'gy': gy, 'u': u, 'want_ydot': True}):
+            ri = ei.second_order_batched(wi, x, v, want_theta=theta, **kw)
+            rs = es.second_order_batched(wsr, x, v, want_theta=theta, **kw)
+            for k, (a, b) in enumerate(zip(ri, rs)):
+                if a is not None:
+                    same(a, b, 'grouped L%d B%d n%d theta %s %s output %d' % (L, B, n, theta, sorted(kw), k))

@@ -1,7 +1,9 @@
 """Static race check on the compiled kernels (no GPU): every translation unit whose kernels read LDS by inline asm
 (or pipeline LDS loads across MFMAs) is compiled for gfx950 to ISA, and tools/check_asm_waits.py verifies that no
 instruction reads, copies or overwrites a register of an LDS load before the s_waitcnt lgkmcnt that retires it, or
-of a vector-memory load before its s_waitcnt vmcnt (the saddr-form asm reloads of the W1 REV and W3i epilogues).
+of a vector-memory load before its s_waitcnt vmcnt (the saddr-form asm reloads of the W1 REV and W3i epilogues), or
+overwrites the data registers of a 16-byte store within the two wait states the store still reads them (the W3i
+inline-asm stores must pad themselves; hipcc only pads its own).
 hipcc does not count inline-asm loads, so a register copy it inserts ahead of a hand-placed wait reads stale data
 on some waves and launches only (found this way in the W1 tile seam, the wgrad reload and the first split-W1 build).
 """
@@ -48,7 +50,7 @@ def test_no_read_of_inflight_lds_load_registers():
                 i = s.find('\n' + nm + ':')
                 j = s.find('.Lfunc_end', i)
                 body = s[i:j].split('\n')
-                probs = C.check(body, nm) + C.check_vmem(body, nm)
+                probs = C.check(body, nm) + C.check_vmem(body, nm) + C.check_store_data(body, nm)
                 if probs:
                     bad.append('%s %s: %d (first: %s)' % (tu, nm, len(probs), probs[0][1]))
         assert not bad, '\n'.join(bad)

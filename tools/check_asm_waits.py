@@ -104,7 +104,9 @@ def check_vmem(body, name):
             dst = regs(parts[0]) if is_load else set()
             src = regs(','.join(parts[1:])) if is_load else regs(operands)
             for ln, rs in pending:
-                if rs & (dst | src):
+                # a later load may overwrite an in-flight load's destination (vector memory returns in order: hipcc
+                # does this for partially used results); reading it as an address or as store data may not
+                if rs & src:
                     problems.append((no, t, ln))
             pending.append((no, dst))
             continue
@@ -112,6 +114,37 @@ def check_vmem(body, name):
         for ln, rs in pending:
             if rs & used:
                 problems.append((no, t, ln))
+    return problems
+
+
+def check_store_data(body, name, wait_states=2):
+    """gfx940+ store-data hazard: a VALU (or v_accvgpr / v_mfma) may not write a data VGPR of a preceding
+    global_/buffer_/scratch_ store wider than 64 bits within two wait states (the store reads its data late). hipcc
+    pads its own stores; inline-asm stores are invisible to it, so they must carry the s_nop themselves."""
+    problems = []
+    recent = []  # (line, data regs, wait states still needed)
+    for no, line in enumerate(body):
+        t = line.split(';')[0].strip()
+        if not t or t.startswith('.') or t.endswith(':'):
+            continue
+        op = t.split()[0]
+        operands = t[len(op):]
+        if op == 's_nop':
+            n = int(operands.strip() or '0', 0) + 1
+            recent = [(ln, rs, w - n) for ln, rs, w in recent if w - n > 0]
+            continue
+        if op.startswith('v_'):
+            dst = regs(operands.split(',')[0])
+            for ln, rs, w in recent:
+                if rs & dst:
+                    problems.append((no, t, ln))
+        if op.startswith(VMEM) and '_store_dwordx' in op and op[-1] in '34':
+            parts = operands.split(',')
+            data = regs(parts[1]) if len(parts) > 1 else set()
+            recent = [(ln, rs, w - 1) for ln, rs, w in recent if w - 1 > 0]
+            recent.append((no, data, wait_states))
+            continue
+        recent = [(ln, rs, w - 1) for ln, rs, w in recent if w - 1 > 0]
     return problems
 
 
@@ -127,7 +160,7 @@ def main():
         i = s.find('\n' + nm + ':')
         j = s.find('.Lfunc_end', i)
         body = s[i:j].split('\n')
-        probs = check(body, nm) + check_vmem(body, nm)
+        probs = check(body, nm) + check_vmem(body, nm) + check_store_data(body, nm)
         print('%-70s %d reads of in-flight load registers' % (nm[:70], len(probs)))
         for no, t, ln in probs[:8]:
             print('    line %d: %s   (load at line %d: %s)' % (no, t, ln, body[ln].strip()))
