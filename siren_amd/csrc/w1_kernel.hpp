@@ -40,6 +40,12 @@
 namespace siren {
 
 constexpr int W1_NBUF = 4;  // ring slots of this kernel (64 KiB)
+#ifndef W1_EXP
+#define W1_EXP 0  // A/B probes (tools/variant_build.sh): 1 = epilogue as one VALU cluster at the slice end, 2 = after
+#endif               // operand pair W1_EPI_PAIR
+#ifndef W1_EPI_PAIR
+#define W1_EPI_PAIR 2
+#endif
 
 enum { EPI_FIRST = 0, EPI_SINCOS = 1, EPI_SEED = 2, EPI_DELTA = 3 };
 
@@ -345,6 +351,13 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
 #pragma unroll
             for (int i = 0; i < epi_nparams<KIND>(); ++i) asm volatile("" : "+v"(ep.v[i]));
         }
+#if W1_EXP & 2
+        if constexpr (p == W1_EPI_PAIR && EPI) {
+            __builtin_amdgcn_sched_barrier(0);
+            w1_epilogue<G, LH, MODE>(st, cx, KB + 1, ep);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#endif
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             acc[2 * p] = mfma4(a0[r], bop[r], acc[2 * p]);
@@ -359,7 +372,13 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
     });
     st.pa0 = a0;
     st.pa1 = a1;
+#if W1_EXP & 1
+    __builtin_amdgcn_sched_barrier(0);
     if constexpr (EPI) w1_epilogue<G, LH, MODE>(st, cx, KB + 1, ep);
+    __builtin_amdgcn_sched_barrier(0);
+#else
+    if constexpr (EPI && !(W1_EXP & 2)) w1_epilogue<G, LH, MODE>(st, cx, KB + 1, ep);
+#endif
 }
 
 template <int G, int LH, int MODE>
