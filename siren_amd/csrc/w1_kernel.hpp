@@ -40,12 +40,20 @@
 namespace siren {
 
 constexpr int W1_NBUF = 4;  // ring slots of this kernel (64 KiB)
-#ifndef W1_EXP
-#define W1_EXP 0  // A/B probes (tools/variant_build.sh): 1 = epilogue as one VALU cluster at the slice end, 2 = after
-#endif               // operand pair W1_EPI_PAIR
+
+// Where a slice runs its epilogue block (w1_slice). An f32 MFMA and the VALU share the wave's issue: a VALU placed
+// singly between MFMAs costs ~14.5 cycles, in a cluster ~6-8.5 (tools/micro/mfma_valu_cluster.hip). The W1 mode (no
+// loads or stores in its epilogue) runs the block as ONE cluster fenced by scheduling barriers after operand pair 1
+// (A/B over pairs 0 / 1 / 2 / 5 / slice end: pair 1 -2.1 % kernel time, profiles/r03x_epilogue_placement.log); the
+// other modes keep it at the slice end, interleaved by hipcc (their REV cos prefetch lands at the mid-slice wait, and
+// their stores would be waited for by it).
 #ifndef W1_EPI_PAIR
-#define W1_EPI_PAIR 2
+#define W1_EPI_PAIR 1
 #endif
+template <int MODE>
+constexpr int w1_epi_pair() {
+    return (MODE & MODE_BASE) == MODE_W1 ? W1_EPI_PAIR : NB / 2;
+}
 
 enum { EPI_FIRST = 0, EPI_SINCOS = 1, EPI_SEED = 2, EPI_DELTA = 3 };
 
@@ -296,6 +304,7 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
     constexpr int NSLOT = ((S + 1) % W1_NBUF) * SLICE * 4;
     constexpr int KIND = epi_kind<G, LH>();
     constexpr bool EPI = KB + 1 < NB;
+    constexpr int EPI_AT = w1_epi_pair<MODE>();
     f32x4 (&acc)[NB] = st.acc[G & 1];
     const f32x4 bop = st.act[KB];
     EpiParams<KIND, G, LH> ep;
@@ -351,13 +360,11 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
 #pragma unroll
             for (int i = 0; i < epi_nparams<KIND>(); ++i) asm volatile("" : "+v"(ep.v[i]));
         }
-#if W1_EXP & 2
-        if constexpr (p == W1_EPI_PAIR && EPI) {
+        if constexpr (p == EPI_AT && EPI) {
             __builtin_amdgcn_sched_barrier(0);
             w1_epilogue<G, LH, MODE>(st, cx, KB + 1, ep);
             __builtin_amdgcn_sched_barrier(0);
         }
-#endif
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             acc[2 * p] = mfma4(a0[r], bop[r], acc[2 * p]);
@@ -372,13 +379,7 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
     });
     st.pa0 = a0;
     st.pa1 = a1;
-#if W1_EXP & 1
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (EPI) w1_epilogue<G, LH, MODE>(st, cx, KB + 1, ep);
-    __builtin_amdgcn_sched_barrier(0);
-#else
-    if constexpr (EPI && !(W1_EXP & 2)) w1_epilogue<G, LH, MODE>(st, cx, KB + 1, ep);
-#endif
+    if constexpr (EPI && EPI_AT >= NB / 2) w1_epilogue<G, LH, MODE>(st, cx, KB + 1, ep);
 }
 
 template <int G, int LH, int MODE>

@@ -34,9 +34,13 @@
 #ifndef W3I_EXP
 #define W3I_EXP 0
 #endif
+// The epilogue block runs as one VALU cluster after operand pair W3I_EPI_PAIR (>= 4: after the mid-slice wait its
+// reloads land at; A/B pairs 4 / 5 / slice end interleaved by hipcc: pair 5 -1.4 % on w3_theta,
+// profiles/r03x_epilogue_placement.log; cf. w1_kernel.hpp w1_epi_pair)
 #ifndef W3I_EPI_PAIR
-#define W3I_EPI_PAIR 1
+#define W3I_EPI_PAIR 5
 #endif
+static_assert(W3I_EPI_PAIR >= 4 && W3I_EPI_PAIR < siren::NB / 2, "the REV reloads land at the mid-slice wait (pair 4)");
 
 namespace siren {
 
@@ -434,13 +438,11 @@ __device__ __forceinline__ void w3i_slice(W3iState<LH>& st, const W3iCtx& cx) {
         }
         // the tile blocks epilogue S staged at the end of the previous slice: retired by the same wait
         if constexpr (p == 0) w3_tile_flush<S, LH, THETA, KEPT>(st, cx);
-#if W3I_EXP & 64
-        if constexpr (p == W3I_EPI_PAIR && EPI) {  // A/B: the epilogue as one VALU cluster after pair W3I_EPI_PAIR
+        if constexpr (p == W3I_EPI_PAIR && EPI) {  // the epilogue block as one VALU cluster after this pair's wait
             __builtin_amdgcn_sched_barrier(0);
             w3i_epilogue<G, LH, THETA, KEPT>(st, cx, KB + 1, ep, (S + 1) % 3);
             __builtin_amdgcn_sched_barrier(0);
         }
-#endif
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             if constexpr (TWO) {
@@ -460,7 +462,7 @@ __device__ __forceinline__ void w3i_slice(W3iState<LH>& st, const W3iCtx& cx) {
     });
     st.pa0 = a0;
     st.pa1 = a1;
-    if constexpr (EPI && !(W3I_EXP & 64)) w3i_epilogue<G, LH, THETA, KEPT>(st, cx, KB + 1, ep, (S + 1) % 3);
+
     // one scheduling region per slice: the epilogue interleaves with this slice's MFMAs, but hipcc may not hoist later
     // blocks' epilogue arithmetic (whose inputs are all ready when the GEMM starts) into it
     if (!(W3I_EXP & 16)) __builtin_amdgcn_sched_barrier(0);
