@@ -44,16 +44,29 @@ constexpr int W1_NBUF = 4;  // ring slots of this kernel (64 KiB)
 // Where a slice runs its epilogue block (w1_slice). An f32 MFMA and the VALU share the wave's issue: a VALU placed
 // singly between MFMAs costs ~14.5 cycles, in a cluster ~6-8.5 (tools/micro/mfma_valu_cluster.hip). The W1 mode (no
 // loads or stores in its epilogue) runs the block as ONE cluster fenced by scheduling barriers after operand pair 1
-// (A/B over pairs 0 / 1 / 2 / 5 / slice end: pair 1 -2.1 % kernel time, profiles/r03x_epilogue_placement.log); the
-// other modes keep it at the slice end, interleaved by hipcc (their REV cos prefetch lands at the mid-slice wait, and
-// their stores would be waited for by it).
+// (A/B over pairs 0 / 1 / 2 / 5 / slice end: pair 1 -2.1 % kernel time, profiles/r03x_epilogue_placement.log); so
+// does the forward-only W0; the modes with loads or stores in the epilogue (STORE / FWDS / REV: the REV cos prefetch
+// lands at the mid-slice wait, and stores issued before it would be waited for by it) run it after pair 4.
 #ifndef W1_EPI_PAIR
 #define W1_EPI_PAIR 1
 #endif
+#ifndef W1_EPI_FWD
+#define W1_EPI_FWD 1  // W0 3.29 -> 3.22 ms (profiles/r03x_epilogue_placement.log)
+#endif
+#ifndef W1_EPI_JET
+#define W1_EPI_JET 8  // pair 1 measured neutral on the Poisson step
+#endif
+#ifndef W1_EPI_MEM
+#define W1_EPI_MEM 4  // STORE / FWDS / REV (>= 4: after the mid-slice wait): hypernet step -2.5 %, image_w2 / sdf neutral
+#endif
 template <int MODE>
 constexpr int w1_epi_pair() {
-    return (MODE & MODE_BASE) == MODE_W1 ? W1_EPI_PAIR : NB / 2;
+    return (MODE & MODE_BASE) == MODE_W1    ? W1_EPI_PAIR
+           : (MODE & MODE_BASE) == MODE_FWD ? W1_EPI_FWD
+           : (MODE & MODE_BASE) == MODE_JET ? W1_EPI_JET
+                                             : W1_EPI_MEM;
 }
+static_assert(W1_EPI_MEM >= 4, "the REV cos prefetch lands at the mid-slice wait (pair 4)");
 
 enum { EPI_FIRST = 0, EPI_SINCOS = 1, EPI_SEED = 2, EPI_DELTA = 3 };
 

@@ -41,7 +41,12 @@ constexpr int X_OBS = 8;                            // output blocks per slice (
 constexpr int X_SLICE = 3 * X_OBS * 256;            // 32-bit words per slice: 8 blocks x (hi, mid, lo) x 1 KiB
 constexpr int X_NBUF = 4;                           // ring slots (96 KiB)
 #ifndef X_EPI_AT
+#ifndef X_EPI_AT
 #define X_EPI_AT 7                                  // slice block after which the slice's epilogue block is issued
+#endif
+#ifndef X_EPI_FENCE
+#define X_EPI_FENCE 0  // 1: the epilogue block as one VALU cluster (scheduling barriers around it; A/B probe)
+#endif
 #endif
 constexpr int X_KSTEPS = H / 32;                    // K-steps of one 256-wide GEMM
 constexpr int X_SPG = 2 * X_KSTEPS;                 // slices per GEMM
@@ -287,7 +292,11 @@ __device__ __forceinline__ void x_slice(XState<LH>& st, const XCtx& cx) {
         }
         // the epilogue block of K-step KS + 1, placed early in the slice so its VALU spreads over the remaining
         // blocks' MFMAs (after the last block it ran as a cluster with the matrix pipe idle)
-        if constexpr (obl == X_EPI_AT && KS + 1 < X_KSTEPS) x_epilogue<G, 2 * (KS + 1) + HALF, LH, D, FWD>(st, cx);
+        if constexpr (obl == X_EPI_AT && KS + 1 < X_KSTEPS) {
+            if (X_EPI_FENCE) __builtin_amdgcn_sched_barrier(0);
+            x_epilogue<G, 2 * (KS + 1) + HALF, LH, D, FWD>(st, cx);
+            if (X_EPI_FENCE) __builtin_amdgcn_sched_barrier(0);
+        }
     });
 }
 
