@@ -35,10 +35,10 @@
 #define W3I_EXP 0
 #endif
 // The epilogue block runs as one VALU cluster after operand pair W3I_EPI_PAIR (>= 4: after the mid-slice wait its
-// reloads land at; A/B pairs 4 / 5 / slice end interleaved by hipcc: pair 5 -1.4 % on w3_theta,
-// profiles/r03x_epilogue_placement.log; cf. w1_kernel.hpp w1_epi_pair)
+// reloads land at; A/B pairs 4 / 5 / 6 / 7 / slice end interleaved by hipcc: pair 5 -1.4 % on w3_theta, pair 7 the
+// same there and -1.4 % more on the sdf step, profiles/r03x_epilogue_placement.log; cf. w1_kernel.hpp w1_epi_pair)
 #ifndef W3I_EPI_PAIR
-#define W3I_EPI_PAIR 5
+#define W3I_EPI_PAIR 7
 #endif
 static_assert(W3I_EPI_PAIR >= 4 && W3I_EPI_PAIR < siren::NB / 2, "the REV reloads land at the mid-slice wait (pair 4)");
 
