@@ -226,12 +226,28 @@ class SirenHessian(torch.autograd.Function):
     GEMMs only."""
 
     KEEP_MAX_BYTES = 16 << 30  # kept jets: 4 (n_hidden + 1) 6 256 bytes per point (6 KiB / layer)
+    KEEP_FREE_FRACTION = 0.5   # ... and at most this share of the device's free memory at forward time
+
+    @staticmethod
+    def _keep_budget(x):
+        try:
+            free, _ = torch.cuda.mem_get_info(x.device)
+        except (RuntimeError, AssertionError):
+            free = 0
+        return min(SirenHessian.KEEP_MAX_BYTES, int(free * SirenHessian.KEEP_FREE_FRACTION))
 
     @staticmethod
     def forward(ctx, engine, ws, x, flat, u=None):
         per_point = 4 * (engine.cfg.n_hidden + 1) * 6 * 256
-        keep = x.shape[0] * per_point <= SirenHessian.KEEP_MAX_BYTES
-        hm, ctx.kept = engine.hessian(ws, x, u, keep=True) if keep else (engine.hessian(ws, x, u), None)
+        keep = x.shape[0] * per_point <= SirenHessian._keep_budget(x)
+        hm, ctx.kept = None, None
+        if keep:
+            try:
+                hm, ctx.kept = engine.hessian(ws, x, u, keep=True)
+            except torch.cuda.OutOfMemoryError:  # the backward then recomputes the forward jet
+                hm, ctx.kept = None, None
+        if hm is None:
+            hm = engine.hessian(ws, x, u)
         ctx.engine, ctx.ws = engine, ws
         ctx.save_for_backward(x, flat, u)
         return hm
@@ -251,6 +267,7 @@ class SirenHessian(torch.autograd.Function):
                                               kept=ctx.kept)
             ctx.kept = None
             return None, None, (gx if need_x else None), gp, gu
+        ctx.kept = None  # the differentiable recompute below does not read the kept jets
         rx, rp, ru = _torch_path.hessian_vjp(eng.cfg, x, flat, G, create_graph=True, u=u)
         return None, None, rx, rp, ru
 

@@ -1156,9 +1156,9 @@ bool grouped_w3(const siren_cfg* cfg, int64_t n) {
 
 int32_t siren_second_order_batched_ws_floats(const siren_cfg* cfg, int64_t n, int64_t batch, int32_t want_theta,
                                              int64_t* count) {
+    if (int rc = check_cfg(cfg, true)) return rc;
     if (batch < 0) return fail(SIREN_EINVAL, "batch < 0");
     if (batch > 1 && n > 0 && grouped_w3(cfg, n)) {
-        if (int rc = check_cfg(cfg, true)) return rc;
         if (count == nullptr) return fail(SIREN_EINVAL, "count is NULL");
         *count = batch * W3Plan(cfg, n, want_theta != 0, batch).total;
         return SIREN_OK;

@@ -330,10 +330,18 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
             // slot of slice S-1 (every wave is past its last read of it) for slice S+3. Slices past the end of the
             // tile are the next tile's slices 0..2 (NS is a multiple of the ring size, so the slots line up).
             if (S + 1 < NS || cx.more) {
-                if (S + 2 < NS || cx.more)
+                if constexpr (S + 2 < NS) {
                     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-                else
+                } else if constexpr (is_rev<MODE>() && S + 2 == NS) {
+                    // the last epilogue's cos block (issued at slice NS - 3) is retired whether or not the next
+                    // tile's ring slices were issued behind it: one wait shape on every path (a `more`-dependent
+                    // vmcnt(4) / vmcnt(0) pair compiles into branches the static ISA check cannot correlate)
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                } else if (cx.more) {
+                    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
                 if constexpr (is_rev<MODE>()) {
                     // the cos block issued one slice ago (epilogue S + 1) has landed; prefetch epilogue S + 2's
                     asm volatile("" : "+v"(st.cq[(S + 1) % 3]));

@@ -41,12 +41,10 @@ constexpr int X_OBS = 8;                            // output blocks per slice (
 constexpr int X_SLICE = 3 * X_OBS * 256;            // 32-bit words per slice: 8 blocks x (hi, mid, lo) x 1 KiB
 constexpr int X_NBUF = 4;                           // ring slots (96 KiB)
 #ifndef X_EPI_AT
-#ifndef X_EPI_AT
 #define X_EPI_AT 7                                  // slice block after which the slice's epilogue block is issued
 #endif
 #ifndef X_EPI_FENCE
 #define X_EPI_FENCE 0  // 1: the epilogue block as one VALU cluster (scheduling barriers around it; A/B probe)
-#endif
 #endif
 constexpr int X_KSTEPS = H / 32;                    // K-steps of one 256-wide GEMM
 constexpr int X_SPG = 2 * X_KSTEPS;                 // slices per GEMM

@@ -17,7 +17,10 @@ def pytest_configure(config):
 def load_golden(name):
     path = os.path.join(GOLDEN, 'golden_%s.npz' % name)
     if not os.path.exists(path):
-        pytest.skip('golden fixture %s missing (run tests/golden/make_golden.py in the build container)' % name)
+        # A missing fixture is a failure, never a skip: a push that drops a golden (e.g. a .gpurunignore edit)
+        # must not turn the parity tests it pins into silent skips.
+        pytest.fail('golden fixture %s missing (regenerate with tests/golden/make_golden.py in the build container)'
+                    % name, pytrace=False)
     return dict(np.load(path))
 
 

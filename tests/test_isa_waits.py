@@ -12,7 +12,6 @@ import shutil
 import subprocess
 import sys
 import tempfile
-from concurrent.futures import ThreadPoolExecutor
 
 import pytest
 
@@ -24,35 +23,111 @@ TUS = ['tu_w1.hip', 'tu_w0.hip', 'tu_w4.hip', 'tu_w3.hip', 'tu_wide.hip', 'tu_je
 sys.path.insert(0, os.path.join(ROOT, 'tools'))
 
 
-@pytest.mark.skipif(shutil.which('hipcc') is None and not os.path.exists('/opt/rocm/bin/hipcc'),
-                    reason='hipcc not available')
-def test_no_read_of_inflight_lds_load_registers():
+def _compile_and_check(tu):
+    """(tu, problems) for one translation unit: hipcc to ISA, then the three checks on every kernel in it."""
+    import re
     import check_asm_waits as C
     hipcc = shutil.which('hipcc') or '/opt/rocm/bin/hipcc'
     tmp = tempfile.mkdtemp(prefix='siren_isa_')
-
-    def compile_one(tu):
+    try:
         out = os.path.join(tmp, tu.replace('.hip', '.s'))
         subprocess.check_call([hipcc, '--offload-arch=gfx950', '-O3', '-std=c++17', '-mllvm',
                                '-pragma-unroll-threshold=1000000', '--cuda-device-only', '-S', '-I',
                                os.path.join(ROOT, 'include'), '-o', out, os.path.join(CSRC, tu)],
                               stderr=subprocess.DEVNULL)
-        return tu, out
-
-    try:
-        with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 2)) as ex:
-            outs = list(ex.map(compile_one, TUS))
-        bad = []
-        for tu, path in outs:
-            import re
-            s = open(path).read()
-            for nm in re.findall(r'\n(_Z\w+):', s):
-                i = s.find('\n' + nm + ':')
-                j = s.find('.Lfunc_end', i)
-                body = s[i:j].split('\n')
-                probs = C.check(body, nm) + C.check_vmem(body, nm) + C.check_store_data(body, nm)
-                if probs:
-                    bad.append('%s %s: %d (first: %s)' % (tu, nm, len(probs), probs[0][1]))
-        assert not bad, '\n'.join(bad)
+        s = open(out).read()
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+    bad = []
+    for nm in re.findall(r'\n(_Z\w+):', s):
+        i = s.find('\n' + nm + ':')
+        j = s.find('.Lfunc_end', i)
+        body = s[i:j].split('\n')
+        probs = C.check(body, nm) + C.check_vmem(body, nm) + C.check_store_data(body, nm)
+        if probs:
+            bad.append('%s %s: %d (first: %s)' % (tu, nm, len(probs), probs[0][1]))
+    return bad
+
+
+@pytest.mark.skipif(shutil.which('hipcc') is None and not os.path.exists('/opt/rocm/bin/hipcc'),
+                    reason='hipcc not available')
+def test_no_read_of_inflight_lds_load_registers():
+    from concurrent.futures import ProcessPoolExecutor
+    with ProcessPoolExecutor(max_workers=min(8, os.cpu_count() or 2)) as ex:
+        bad = [b for res in ex.map(_compile_and_check, TUS) for b in res]
+    assert not bad, '\n'.join(bad)
+
+
+def _walk_isa(text):
+    import check_asm_waits as C
+    body = ['_Zk:'] + [ln.strip() for ln in text.strip().split('\n')]
+    return C.check(body, 'k') + C.check_vmem(body, 'k')
+
+
+def test_checker_follows_fall_through_labels_and_back_edges():
+    # a load in flight across a fall-through label is still checked after it
+    assert _walk_isa("""
+        ds_read_b128 v[0:3], v10
+    .LBB0_1:
+        v_add_f32 v4, v0, v1
+        s_endpgm""")
+    # ... and across a loop back-edge (issued at the bottom, read at the head before any wait)
+    assert _walk_isa("""
+    .LBB0_1:
+        v_add_f32 v4, v0, v1
+        global_load_dwordx4 v[0:3], v12, s[0:1]
+        s_cbranch_scc1 .LBB0_1
+        s_waitcnt vmcnt(0)
+        s_endpgm""")
+    # a wait on every path retires it
+    assert not _walk_isa("""
+        ds_read_b128 v[0:3], v10
+        s_cbranch_scc1 .LBB0_2
+        s_waitcnt lgkmcnt(0)
+        s_branch .LBB0_3
+    .LBB0_2:
+        s_waitcnt lgkmcnt(0)
+    .LBB0_3:
+        v_add_f32 v4, v0, v1
+        s_endpgm""")
+    # a path that skips the wait is reported
+    assert _walk_isa("""
+        ds_read_b128 v[0:3], v10
+        s_cbranch_scc1 .LBB0_3
+        s_waitcnt lgkmcnt(0)
+    .LBB0_3:
+        v_add_f32 v4, v0, v1
+        s_endpgm""")
+
+
+def test_checker_correlates_flag_branches():
+    # hipcc's lowering of `if (c) wait(0) else wait(4)`: the flag pair set on one path makes the second branch's
+    # direction known, so the path that would skip both waits is infeasible and nothing is reported
+    assert not _walk_isa("""
+        global_load_dwordx4 v[0:3], v12, s[4:5]
+        s_mov_b64 s[0:1], -1
+        s_and_b64 vcc, exec, s[12:13]
+        s_cbranch_vccz .LBB0_2
+        s_waitcnt vmcnt(0)
+        s_mov_b64 s[0:1], 0
+    .LBB0_2:
+        s_andn2_b64 vcc, exec, s[0:1]
+        s_cbranch_vccnz .LBB0_4
+        s_waitcnt vmcnt(0)
+    .LBB0_4:
+        v_add_f32 v4, v0, v1
+        s_endpgm""")
+    # the same shape with the second wait missing is reported
+    assert _walk_isa("""
+        global_load_dwordx4 v[0:3], v12, s[4:5]
+        s_mov_b64 s[0:1], -1
+        s_and_b64 vcc, exec, s[12:13]
+        s_cbranch_vccz .LBB0_2
+        s_waitcnt vmcnt(0)
+        s_mov_b64 s[0:1], 0
+    .LBB0_2:
+        s_andn2_b64 vcc, exec, s[0:1]
+        s_cbranch_vccnz .LBB0_4
+    .LBB0_4:
+        v_add_f32 v4, v0, v1
+        s_endpgm""")

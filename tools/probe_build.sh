@@ -9,7 +9,8 @@ O=$R/build/probe$LVL
 mkdir -p $O $R/tools/probe
 FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -mllvm -pragma-unroll-threshold=1000000 -DSIREN_PROBE=$LVL $EXTRA"
 objs=""
-for tu in siren_capi tu_legacy tu_w1 tu_w0 tu_w3 tu_train tu_wide tu_w4 tu_jet tu_step tu_wide_jet layered marching tu_w1x; do
+TUS=$(cd $R && python -c "import __graft_entry__ as g; print(' '.join(t[:-4] for t in g.TUS))")
+for tu in $TUS; do
   /opt/rocm/bin/hipcc $FL -c -I $R/include -o $O/$tu.o $R/siren_amd/csrc/$tu.hip &
   objs="$objs $O/$tu.o"
 done
