@@ -231,17 +231,24 @@ PMC_FILE = os.path.join(ROOT, 'profiles', 'pmc_headline.json')
 
 
 def pmc_traffic(n):
-    """HBM bytes per launch of the headline kernel from the committed rocprofv3 PMC summary of the current kernel
+    """HBM bytes per launch of the headline kernel from the committed rocprofv3 PMC summary
     (profiles/pmc_headline.json: tools/gpu_round.sh's FETCH_SIZE / WRITE_SIZE passes through tools/pmc_summary.py),
-    if it holds this kernel at this N; else None."""
+    if it holds this kernel at this N AND was collected on a library built from the sources of this tree (its
+    `source_hash` stamp equals __graft_entry__._source_hash()); else None — a profile of an older kernel is never
+    reported as this one's traffic. Returns (bytes or None, provenance note)."""
     try:
         rec = json.load(open(PMC_FILE))
     except Exception:
-        return None
+        return None, 'no profiles/pmc_headline.json'
+    import __graft_entry__
+    if rec.get('source_hash') != __graft_entry__._source_hash():
+        return None, 'profiles/pmc_headline.json was collected on another build (source_hash %s)' % (
+            str(rec.get('source_hash'))[:12])
     k = rec.get('kernels', {}).get(HEADLINE_KERNEL)
     if k and rec.get('n') == n and 'hbm_bytes_per_launch' in k:
-        return round(k['hbm_bytes_per_launch'])
-    return None
+        return round(k['hbm_bytes_per_launch']), 'profiles/pmc_headline.json (source_hash %s, FETCH_SIZE x2 + ' \
+            'WRITE_SIZE per MI355X_MICROARCH.md)' % rec['source_hash'][:12]
+    return None, 'profiles/pmc_headline.json lacks %s at n=%d' % (HEADLINE_KERNEL, n)
 
 
 def train_step_rate(device, n=1 << 18, steps=5):
@@ -643,6 +650,8 @@ def main():
     extra = {}
     if rank == 0 and not args.no_extra:
         extra['w2_image_mse_train_mcoords_s'] = round(train_step_rate(device), 3)
+        # config 2's own N (2^20 coordinates per step) beside the 2^18 leg the per-path profile is taken at
+        extra['w2_image_mse_train_n2p20_mcoords_s'] = round(train_step_rate(device, n=1 << 20), 3)
         extra['configs'] = config_rates(device)
         cr, dpr = extra['configs'], dp or {}
         extra['roofline_by_path'] = path_rooflines({
@@ -661,7 +670,7 @@ def main():
         cpu = cpu_baseline()
 
     if rank == 0:
-        traffic = pmc_traffic(args.n)
+        traffic, traffic_src = pmc_traffic(args.n)
         line = {
             'metric': 'Mcoords/sec fwd+∇ (5×256 SIREN) at 1/2/4/8 MI355X; PSNR vs ref',
             'value': round(value, 3), 'unit': 'Mcoords/s', 'n_gpus': n_ranks, 'steps': args.steps,
@@ -672,7 +681,7 @@ def main():
                        'coords_per_gpu': args.n, 'parallelism': 'dp%d' % n_ranks},
             'roofline': {'bound': 'mfma', 'achieved': round(achieved, 3), 'peak': PEAK_FP32_MFMA_TFLOPS,
                          'unit': 'TFLOP/s', 'frac': round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
-                         'traffic': traffic, 'kernel_ms': round(kms, 4),
+                         'traffic': traffic, 'traffic_source': traffic_src, 'kernel_ms': round(kms, 4),
                          'flop_per_coord': W1_FLOP},
             'cpu_baseline': cpu,
             'split_bf16x6': split,

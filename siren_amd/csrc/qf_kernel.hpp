@@ -1,0 +1,269 @@
+#pragma once
+// qf_kernel.hpp — the backward of the Hessian node reading its forward jets from the node's KEEP scratch
+// (siren_hessian_backward_kept): the reverse-only quadratic-form jet, laid out like the node's forward
+// (hess_kernel.hpp) instead of the W4 jet's 4 coordinates x 4 streams per 16-column tile.
+//
+// Math (jet_kernel.hpp QG): with Q = sym(G) per coordinate and the kept pre-activation streams z, z_1, z_2, z_11, z_12,
+// z_22 of layer l, the forward jet it differentiates is
+//     a_0 = s,  a_i = w c z_i,  a_3 = w c z_3 - w^2 s z^T Q z,     z_3 = sum_ij Q_ij z_ij     (s, c = sin, cos(w z))
+// and, for the cotangent u of the a-jet, the cotangent of the z-jet is
+//     zb_3 = w c u_3,  zb_i = w c u_i - w^2 s (2 Q z)_i u_3,  zb_0 = w c u_0 - w^2 s (u_1 z_1 + u_2 z_2) - u_3 K,
+//     K = w^2 s z_3 + w^3 c z^T Q z.
+// The reverse GEMMs carry the 4 zb streams back through W_l^T; the a-jets of every layer and the zb-jets go to the
+// MFMA wgrad (4 n columns) and the edge kernel (EDGE_Q8) for the parameter gradient.
+//
+// Layout ("Q8"): one wave owns 8 coordinates in TWO 16-column MFMA tiles that share every A operand (8 MFMAs per
+// ds_read_b128): column c of tile 0 holds stream 0 (value) of coordinate c & 7 for c < 8 ("lo" lanes) and stream 1
+// (d/dx_1) for c >= 8 ("hi"); tile 1 holds stream 2 (lo) and stream 3 (the Q stream, hi). The kept scratch has the
+// same 8-coordinate lo / hi split (lo: z, z_2, z_12; hi: z_1, z_11, z_22), so one DPP row_ror:8 hands a lane its
+// partner's value of a stream: per element 5 DPP moves (z, z_1 / z_2, the z_3 partial sum, two cotangents) produce
+// two output streams, where the W4 jet layout spends 9 quad broadcasts per output stream (4.6 VALU per
+// MFMA, 0.47 MFMA busy). Tiles in HBM: [layer][tile pair 2 grp, 2 grp + 1][neuron][16 columns] (4 n_pad columns
+// per layer, n_pad a multiple of 32); the wgrad's bias takes the value columns (jet_bias 3: even tiles, columns < 8).
+#include "hess_kernel.hpp"
+#include "lds_ops.h"
+#include "ring.hpp"
+#include "siren_common.h"
+#include "siren_params.h"
+
+namespace siren {
+
+#ifndef QF_PROBE
+#define QF_PROBE 0  // timing probes (tools/qf_probe.sh; numerically meaningless): 1 no epilogue arithmetic, 2 also no
+                    // kept loads, 3 also no tile stores
+#endif
+#ifndef QF_PREFETCH_N
+#define QF_PREFETCH_N 3
+#endif
+constexpr int QF_PREFETCH = QF_PREFETCH_N;
+#ifndef QF_STAGGER
+#define QF_STAGGER 0  // first-round start delay per CU quarter, in s_sleep(127) units (~3.4 us each)
+#endif  // kept blocks loaded ahead of the epilogue element that consumes them
+
+// this lane's three kept streams of block rb (tiles 0..2 of hess_kept_off), one 16 B global load each
+struct QfKept {
+    f32x4 k[3];
+};
+__device__ __forceinline__ QfKept qf_load(const float* p) {
+    typedef const __attribute__((address_space(1))) f32x4 gf32x4;
+    QfKept r;
+#if QF_PROBE >= 2 || defined(QF_NOLOAD)
+    r.k[0] = r.k[1] = r.k[2] = f32x4{0.5f, 0.25f, 0.125f, 1.f};
+    asm volatile("" : "+v"(r.k[0]), "+v"(r.k[1]), "+v"(r.k[2]));
+    return r;
+#endif
+    r.k[0] = *(gf32x4*)p;
+    r.k[1] = *(gf32x4*)(p + 256);
+    r.k[2] = *(gf32x4*)(p + 512);
+    return r;
+}
+
+// per-coordinate coefficients of the quadratic form (lane constants): q11 = G_11, q12 = G_12 + G_21, q22 = G_22
+struct QfCoef {
+    float q11, q12, q22;
+    float e1, e2;  // own z_3 partial: lo e2 z_12 (e1 = 0), hi e1 z_11 + e2 z_22
+    float ca, cb;  // own (2 Q z) row: lo (2 Q z)_2 = q12 z_1 + 2 q22 z_2, hi (2 Q z)_1 = 2 q11 z_1 + q12 z_2
+};
+
+// one layer's epilogue for one element (row r of block rb): kept streams k0..k2, cotangents ua (tile 0), ub (tile 1)
+// -> a-jet (aa, ab) and z-jet cotangent (za, zb) of this lane's two streams
+__device__ __forceinline__ void qf_elem(float k0, float k1, float k2, float ua, float ub, float wl, float wl2,
+                                        const QfCoef& q, bool hi, float& aa, float& ab, float& za, float& zb) {
+#if QF_PROBE >= 1
+    aa = k0 + ua;
+    ab = k1 + ub;
+    za = k2 * ua;
+    zb = k0 * ub;
+    return;
+#endif
+    const float p0 = row_ror8(k0), p1 = row_ror8(k1);
+    const float zp = __builtin_fmaf(q.e1, k1, q.e2 * k2);
+    const float z3 = zp + row_ror8(zp);
+    const float pa = row_ror8(ua), pb = row_ror8(ub);
+    const float z = hi ? p0 : k0;
+    const float z1 = hi ? k0 : p0;
+    const float z2 = hi ? p1 : k1;
+    float sn, cs;
+    sincos_fast(wl * z, sn, cs);
+    const float wc = wl * cs, w2s = wl2 * sn;
+    const float qz = __builtin_fmaf(z1, __builtin_fmaf(q.q11, z1, q.q12 * z2), (q.q22 * z2) * z2);  // z^T Q z
+    const float lin = __builtin_fmaf(q.ca, z1, q.cb * z2);                                       // (2 Q z)_own
+    const float u3 = hi ? ub : pb;
+    aa = hi ? wc * z1 : sn;                                       // a_1 | a_0
+    ab = hi ? __builtin_fmaf(wc, z3, -w2s * qz) : wc * z2;        // a_3 | a_2
+    const float t3 = w2s * (lin * u3);                            // w^2 s (2 Q z)_i u_3
+    zb = hi ? wc * ub : __builtin_fmaf(wc, ub, -t3);              // zb_3 | zb_2
+    const float K = __builtin_fmaf(w2s, z3, (wl2 * wc) * qz);     // w^2 s z_3 + w^3 c z^T Q z
+    const float t0 = __builtin_fmaf(w2s, __builtin_fmaf(pa, z1, ub * z2), u3 * K);
+    za = __builtin_fmaf(wc, ua, -(hi ? t3 : t0));                 // zb_1 | zb_0
+}
+
+// gx (n, d) = W0^T zb_0,value; gu (n, o) nullable = D2 y_j[Q]; tu (n, o) nullable output weighting (NULL = ones);
+// G (n, d, d); kept = the Hessian node's KEEP scratch of the same (ws, x, n); abuf / dbuf: a- / zb-jet tiles of layers
+// 0..L. Grid: hess_groups(n) / 4 workgroups of 4 waves (8 coordinates each).
+__global__ __launch_bounds__(THREADS, 1) void qf_rev_kernel(const float* __restrict__ ws, const float* __restrict__ x,
+                                                            int64_t n, const float* __restrict__ G,
+                                                            const float* __restrict__ tu,
+                                                            const float* __restrict__ kept, float* __restrict__ gx,
+                                                            float* __restrict__ gu, int d, int o, int lh, float w0,
+                                                            float w, float* __restrict__ abuf, float* __restrict__ dbuf,
+                                                            int64_t n_pad) {
+    __shared__ __attribute__((aligned(16))) float lds[NBUF * SLICE + SMALL_MAX];
+    float* ring = lds;
+    float* sm = lds + NBUF * SLICE;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane >> 4, c = lane & 15;
+    const bool hi = c >= 8;
+    const int nslices = 2 * lh * NB;
+    const float* stream = ws + small_pad(lh);
+    {
+        const int nf4 = (small_floats(lh) + 3) / 4;
+        for (int e = threadIdx.x; e < nf4; e += THREADS) ((f32x4*)sm)[e] = ((const f32x4*)ws)[e];
+    }
+    const int64_t ngroups = hess_groups(n);
+    const int64_t grp = (int64_t)blockIdx.x * WAVES + wave;
+    const int64_t coord = grp * 8 + (c & 7);
+    const bool valid = coord < n;
+    const int64_t lstride = 4 * n_pad * H;                  // floats per layer of abuf / dbuf
+    const int64_t toff = 2 * grp * (H * 16) + 4 * g * 16 + c;  // tile 0 of the pair; tile 1 at + H * 16
+    const float* kp = kept + hess_kept_off(ngroups, 0, grp, 0, 0, lane);
+    const int64_t kl = ngroups * NB * 3 * 256;  // floats per layer of the kept scratch
+    QfCoef q;
+    {
+        const float* gq = G + coord * d * d;
+        q.q11 = valid ? gq[0] : 0.f;
+        q.q12 = (valid && d > 1) ? gq[1] + gq[2] : 0.f;
+        q.q22 = (valid && d > 1) ? gq[3] : 0.f;
+        q.e1 = hi ? q.q11 : 0.f;
+        q.e2 = hi ? q.q22 : q.q12;
+        q.ca = hi ? 2.f * q.q11 : q.q12;
+        q.cb = hi ? q.q12 : 2.f * q.q22;
+    }
+    __syncthreads();
+    if (QF_STAGGER > 0 && blockIdx.x < 256) {
+        // de-phase the CUs: one workgroup per CU runs the tiles back to back, so without an offset every CU reaches its
+        // epilogues (the kept loads and tile stores) at the same time and the HBM bursts queue behind each other
+        const int k = (blockIdx.x >> 3) & 3;
+        for (int i = 0; i < k * QF_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+    }
+    // the ring starts at the first reverse slice (the stream's transposed layers)
+    int s = lh * NB;
+    ring_issue(stream, ring, s, nslices, wave, lane);
+    ring_issue(stream, ring, s + 1, nslices, wave, lane);
+
+    f32x4 act[2][NB], acc[2][NB];
+    // one layer's epilogue: acc (cotangent of the a-jet of layer lm) + kept z-jet -> a-jet (abuf) and zb (act, dbuf);
+    // the kept blocks are loaded QF_PREFETCH blocks ahead
+    auto epilogue = [&](int lm, auto seed) {
+        constexpr bool SEED = decltype(seed)::value;
+        const float wl = lm == 0 ? w0 : w, wl2 = wl * wl;
+        const float* kr = kp + lm * kl;
+        float* ap = abuf + (int64_t)lm * lstride + toff;
+        float* dp = dbuf + (int64_t)lm * lstride + toff;
+        QfKept kq[QF_PREFETCH];
+#pragma unroll
+        for (int i = 0; i < QF_PREFETCH; ++i) kq[i] = qf_load(kr + i * 768);
+        float uw[MAXO], gup[MAXO];
+#pragma unroll
+        for (int j = 0; j < MAXO; ++j) {
+            uw[j] = (SEED && valid && j < o) ? (tu != nullptr ? tu[coord * o + j] : 1.f) : 0.f;
+            gup[j] = 0.f;
+        }
+#pragma unroll
+        for (int rb = 0; rb < NB; ++rb) {
+            const QfKept kc = kq[rb % QF_PREFETCH];
+            asm volatile("" ::: "memory");  // keep the prefetch distance: no hoisting of the layer's 48 loads
+            if (rb + QF_PREFETCH < NB) kq[rb % QF_PREFETCH] = qf_load(kr + (rb + QF_PREFETCH) * 768);
+            f32x4 ua, ub;
+            if constexpr (SEED) {
+                // the cotangent of the a_L jet lives on the Q stream only: u_3 = sum_j u_j Wout_j (hi lanes, tile 1)
+                const float* wo = sm + SM_WO + 16 * rb + 4 * g;  // WoT rows j >= o are zero padded
+                const f32x4 sd = uw[0] * *(const f32x4*)wo + uw[1] * *(const f32x4*)(wo + H) +
+                                 uw[2] * *(const f32x4*)(wo + 2 * H) + uw[3] * *(const f32x4*)(wo + 3 * H);
+                const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+                ua = zero;
+                ub = hi ? sd : zero;
+            } else {
+                ua = acc[0][rb];
+                ub = acc[1][rb];
+            }
+            f32x4 aa, ab;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float ea, eb, za, zb;
+                qf_elem(kc.k[0][r], kc.k[1][r], kc.k[2][r], ua[r], ub[r], wl, wl2, q, hi, ea, eb, za, zb);
+                aa[r] = ea;
+                ab[r] = eb;
+                act[0][rb][r] = za;
+                act[1][rb][r] = zb;
+            }
+#if QF_PROBE < 3 && !defined(QF_NOSTORE)
+            if constexpr (!SEED) store_block(ap, 0, aa);  // a_L's value / d/dx_1 streams feed no gradient
+            store_block(ap + H * 16, 0, ab);
+            store_block(dp, 0, act[0][rb]);
+            store_block(dp + H * 16, 0, act[1][rb]);
+#endif
+            ap += 256;
+            dp += 256;
+            asm volatile("" : "+v"(ap), "+v"(dp));
+            if constexpr (SEED) {  // gu_j = Wout_j . a_L,3 (hi lanes' tile-1 a-jet)
+#pragma unroll
+                for (int j = 0; j < MAXO; ++j) {
+                    const f32x4 wj = *(const f32x4*)(sm + SM_WO + j * H + 16 * rb + 4 * g);
+                    gup[j] += wj[0] * ab[0] + wj[1] * ab[1] + wj[2] * ab[2] + wj[3] * ab[3];
+                }
+            }
+        }
+        if constexpr (SEED) {
+            if (gu != nullptr) {
+#pragma unroll
+                for (int j = 0; j < MAXO; ++j) {
+                    const float pj = sum_groups(gup[j]);
+                    if (j < o && valid && g == 0 && hi) gu[coord * o + j] = pj;
+                }
+            }
+        }
+    };
+
+    // seed at layer L from the kept z_L jet (no forward sweep), then the L reverse GEMMs
+    epilogue(lh, std::true_type{});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // slice s landed (and the seed's stores): publish it
+    __builtin_amdgcn_s_barrier();
+#pragma unroll 1
+    for (int p = lh; p < 2 * lh; ++p) {
+#pragma unroll
+        for (int ob = 0; ob < NB; ++ob) acc[0][ob] = acc[1][ob] = f32x4{0.f, 0.f, 0.f, 0.f};
+        {
+            const unsigned rbase = lds_addr(ring) + 16u * lane;
+            f32x4 a = lds_read4<0>(rbase + (s % NBUF) * SLICE * 4);
+#pragma unroll
+            for (int kb = 0; kb < NB; ++kb) {
+                const unsigned va = rbase + (s % NBUF) * SLICE * 4, vn = rbase + ((s + 1) % NBUF) * SLICE * 4;
+                auto mid = [&]() { ring_mid(stream, ring, s, nslices, wave, lane); };
+                if (kb + 1 < NB)
+                    slice_mma2_mid<NB, NB / 2, true>(va, vn, act[0][kb], act[1][kb], acc[0], acc[1], a, a, mid);
+                else
+                    slice_mma2_mid<NB, NB / 2, false>(va, vn, act[0][kb], act[1][kb], acc[0], acc[1], a, a, mid);
+                ++s;
+            }
+        }
+        epilogue(2 * lh - p - 1, std::false_type{});
+    }
+
+    // ---- gx = W0^T zb_0,value (tile 0, lo lanes) ---------------------------------------------------------------
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k) {
+        if (k < d) {
+            float qk = 0.f;
+#pragma unroll
+            for (int rb = 0; rb < NB; ++rb) {
+                const f32x4 wk = *(const f32x4*)(sm + SM_W0 + k * H + 16 * rb + 4 * g);
+                qk += wk[0] * act[0][rb][0] + wk[1] * act[0][rb][1] + wk[2] * act[0][rb][2] + wk[3] * act[0][rb][3];
+            }
+            qk = sum_groups(qk);
+            if (valid && g == 0 && !hi) gx[coord * d + k] = qk;
+        }
+    }
+}
+
+}  // namespace siren

@@ -564,11 +564,14 @@ int check_jet(const siren_cfg* cfg) {
 }
 
 // jet tiles are 16 columns = 4 coordinates x 4 streams: a-jets, zb-jets and z-jets of every layer + S slabs
+// q8: the Hessian node's kept backward (qf_kernel.hpp): n_pad a multiple of 32 (8 coordinates per wave), the edge
+// kernel's tiles are Q8 tile pairs (8 coordinates); otherwise W4 jet tiles of 4 coordinates, n_pad a multiple of 16
 struct JetPlan {
     int64_t n_pad, cols, tiles, splits, tps, buf_floats, partial_floats, total, eslab_off;
     EdgeSplit es;
-    JetPlan(const siren_cfg* cfg, int64_t n) : es(cfg, (n + 15) / 16 * 16 / 4) {
-        n_pad = (n + 15) / 16 * 16;
+    static int64_t pad(int64_t n, bool q8) { return q8 ? (n + 31) / 32 * 32 : (n + 15) / 16 * 16; }
+    JetPlan(const siren_cfg* cfg, int64_t n, bool q8 = false) : es(cfg, pad(n, q8) / (q8 ? 8 : 4)) {
+        n_pad = pad(n, q8);
         cols = 4 * n_pad;
         tiles = cols / 16;
         const int64_t want = wgrad_splits(cfg);
@@ -788,7 +791,7 @@ int check_quad(const siren_cfg* cfg) {
 int32_t siren_hessian_backward_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count) {
     if (int rc = check_quad(cfg)) return rc;
     if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
-    *count = JetPlan(cfg, n).total;
+    *count = std::max(JetPlan(cfg, n).total, JetPlan(cfg, n, true).total);  // recomputing / kept (Q8) backward
     return SIREN_OK;
 }
 
@@ -831,6 +834,28 @@ int32_t siren_hessian_backward_kept(const siren_cfg* cfg, const float* ws, const
     }
     if (ws == nullptr || tws == nullptr || gx == nullptr || x == nullptr || G == nullptr)
         return fail(SIREN_EINVAL, "ws/x/G/tws/gx is NULL");
+    if (kept != nullptr) {
+        // reverse-only quadratic-form jet on the node's own 8-coordinate layout (qf_kernel.hpp), then the MFMA wgrad
+        // over the Q8 tile pairs (value-column bias: jet_bias 3) and EDGE_Q8
+        if (n > (int64_t)0x7fffffff * 8) return fail(SIREN_EINVAL, "n exceeds the grid");
+        const JetPlan qp(cfg, n, true);
+        float* qa = tws;
+        float* qd = qa + qp.buf_floats;
+        float* qpart = qd + qp.buf_floats;
+        siren::launch_qf_rev(dim3((unsigned)(siren::hess_groups(n) / siren::WAVES)), st, ws, x, n, G, u, kept, gx, gu,
+                             cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, qa, qd,
+                             qp.n_pad);
+        if (int rc = hip_status("siren_hessian_backward (kept quadratic-form jet)")) return rc;
+        if (gparams == nullptr) return SIREN_OK;
+        siren::launch_wgrad(dim3((unsigned)qp.splits, (unsigned)cfg->n_hidden), st, qa, qd, qp.cols, qp.tps, qpart, P,
+                            cfg->d_in, cfg->d_out, cfg->n_hidden, 1, siren::H, 3);
+        if (int rc = hip_status("siren_hessian_backward (wgrad)")) return rc;
+        siren::launch_small_q8(qp.es.grid(cfg), st, qa, qd, x, u, n, qp.n_pad, qp.es.tps, qpart + qp.eslab_off,
+                               qp.es.E, cfg->d_in, cfg->d_out, cfg->n_hidden);
+        if (int rc = hip_status("siren_hessian_backward (small)")) return rc;
+        return finish_grads(cfg, st, qpart, qp.splits, 0, qpart + qp.eslab_off, qp.es, gparams,
+                            "siren_hessian_backward (reduce)");
+    }
     float* abuf = tws;
     float* dbuf = abuf + plan.buf_floats;
     float* spill = dbuf + plan.buf_floats;

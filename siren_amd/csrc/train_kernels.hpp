@@ -103,7 +103,10 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
     // bias partial sums: lane (g, i) accumulates the value columns of delta row 128 wr + 16 rb + i among
     // coordinates 4g..4g+3 (jet tiles: column 4g only; two-stream tiles: 4g, 4g + 2) -- m1..m3 are exact 0/1 masks
     float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const float m1 = jet_bias ? 0.f : 1.f, m2 = jet_bias == 1 ? 0.f : 1.f, m3 = m1;
+    // jet_bias 3 (qf_kernel.hpp Q8 tiles: 8 coordinates x 4 streams over a tile pair): the value columns are columns
+    // 0..7 of the even tile of each pair, i.e. lane groups g < 2 of even tiles (mt, per tile)
+    const float m1 = (jet_bias == 1 || jet_bias == 2) ? 0.f : 1.f, m2 = jet_bias == 1 ? 0.f : 1.f, m3 = m1;
+    float mt = 1.f;
 
     f32x4 av[8], bv[8];
     // Operands are reloaded for the next tile as soon as their last MFMA of this tile has issued: A block rb after
@@ -116,7 +119,7 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
     auto block = [&](auto RB, int vn) {
         constexpr int rb = decltype(RB)::value;
         const f32x4 v = av[rb];
-        bs[rb] += (v[0] + m2 * v[2]) + (m1 * v[1] + m3 * v[3]);
+        bs[rb] += mt * ((v[0] + m2 * v[2]) + (m1 * v[1] + m3 * v[3]));
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -126,7 +129,7 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
     };
     auto last_block = [&](int vn) {
         const f32x4 v = av[7];
-        bs[7] += (v[0] + m2 * v[2]) + (m1 * v[1] + m3 * v[3]);
+        bs[7] += mt * ((v[0] + m2 * v[2]) + (m1 * v[1] + m3 * v[3]));
         av[7] = rv[vn + ra + 7 * 64];
         __builtin_amdgcn_sched_barrier(0);
         // cb pairs outermost (a dependent MFMA two issues behind clears the 16x16x4 f32 latency); B block cb is
@@ -175,6 +178,7 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_barrier" ::: "memory");  // also a compiler barrier for the LDS loads
         wg_issue(dsrc, asrc, ring, t + 3, t1, k + 3, wave, swz, tstride);
+        if (jet_bias == 3) mt = ((t & 1) == 0 && g < 2) ? 1.f : 0.f;
         const int vn = ((k + 1) % WG_NBUF) * (WG_SLOT / 4);
         block(std::integral_constant<int, 0>{}, vn);
         block(std::integral_constant<int, 1>{}, vn);
@@ -231,7 +235,10 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
 //             rows zb_0 jet, a_L jet; scalars x, v (sc), gy (sgy, nullable), u (su, NULL = ones):
 //             dW0[:, k] = sum zb_0,val x_k + zb_0,tan v_k, db0 = sum zb_0,val, dWout_j = sum gy_j a_L,val + u_j a_L,tan,
 //             dbout_j = sum gy_j
-enum { EDGE_W2 = 0, EDGE_W3 = 1, EDGE_JET = 2, EDGE_MIX = 3, EDGE_J2 = 4 };
+//   EDGE_Q8 : the Hessian node's backward on Q8 tile pairs (qf_kernel.hpp: 8 coordinates x 4 streams over two 16-column
+//             tiles; pair p = tiles 2p (value | d/dx_1) and 2p + 1 (d/dx_2 | Q stream)), tangents along the axes:
+//             dW0[:, k] = sum zb_0,value x_k + zb_0,k, db0 = sum zb_0,value, dWout_j = sum u_j a_L,Q, dbout = 0
+enum { EDGE_W2 = 0, EDGE_W3 = 1, EDGE_JET = 2, EDGE_MIX = 3, EDGE_J2 = 4, EDGE_Q8 = 5 };
 constexpr int EDGE_CHUNK = 16;  // tiles per LDS staging chunk
 // Thread groups per workgroup: group g walks its own quarter of the split's tile range (the split is the wgrad
 // kernel's, so one workgroup per split: 42 of them at hidden 512) and the groups' per-neuron sums are combined in
@@ -239,7 +246,7 @@ constexpr int EDGE_CHUNK = 16;  // tiles per LDS staging chunk
 // §3.11); four keep 4x the row loads in flight.
 // The jet kinds keep ~120 VGPRs at four groups; EDGE_W2 / EDGE_W3 (16 column scalars and up to four row streams per
 // tile) need their 256-VGPR budget, so they run two groups (512 threads).
-constexpr int edge_groups(int kind) { return kind == 2 || kind == 3 ? 4 : 2; }
+constexpr int edge_groups(int kind) { return kind == 2 || kind == 3 || kind == 5 ? 4 : 2; }
 constexpr int edge_threads(int kind) { return edge_groups(kind) * THREADS; }
 constexpr int EDGE_ACC = 14;  // per-thread sums: gw0[4], gb0, gwo[4], gbo, gbj[4]
 
@@ -258,8 +265,9 @@ __global__ __launch_bounds__(edge_threads(KIND)) void edge_kernel(const float* _
     // su == nullptr)
     constexpr bool JETK = KIND == EDGE_JET || KIND == EDGE_MIX;
     constexpr int EDGE_GROUPS = edge_groups(KIND);
-    constexpr int CPT = JETK ? 4 : (KIND == EDGE_J2 ? 8 : 16);  // coordinates per tile
-    constexpr int NSC = (KIND == EDGE_W3 || KIND == EDGE_MIX || KIND == EDGE_J2) ? 16 : 9;
+    constexpr bool Q8 = KIND == EDGE_Q8;  // a "tile" is a Q8 tile pair (8 coordinates)
+    constexpr int CPT = JETK ? 4 : (KIND == EDGE_J2 || Q8 ? 8 : 16);  // coordinates per tile
+    constexpr int NSC = (KIND == EDGE_W3 || KIND == EDGE_MIX || KIND == EDGE_J2 || Q8) ? 16 : 9;
     constexpr int SCAL = EDGE_CHUNK * CPT * NSC;  // floats of one group's staging area
     constexpr int SMEM = EDGE_GROUPS * SCAL > EDGE_GROUPS * THREADS * EDGE_ACC ? EDGE_GROUPS * SCAL
                                                                               : EDGE_GROUPS * THREADS * EDGE_ACC;
@@ -291,7 +299,7 @@ __global__ __launch_bounds__(edge_threads(KIND)) void edge_kernel(const float* _
         }
         eslab += b * bstride_e;
     }
-    const int64_t tstride = (int64_t)h * 16;
+    const int64_t tstride = (int64_t)h * 16 * (Q8 ? 2 : 1);
     const int ns = KIND == EDGE_W2 ? o : ((KIND == EDGE_W3 || KIND == EDGE_MIX || KIND == EDGE_J2) ? d : 1);
     // this split's compact edge slab: [W0 (h, d) | b0 (h) | Wout (o, h) | bout (o)] (edge_reduce_kernel maps it back
     // to the parameter order); grid.y = the 256-neuron block
@@ -313,7 +321,7 @@ __global__ __launch_bounds__(edge_threads(KIND)) void edge_kernel(const float* _
                 for (int k = 0; k < MAXD; ++k) scal[e][k] = (ok && k < d) ? x[cd * d + k] : 0.f;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    if (KIND == EDGE_MIX && sc == nullptr)  // QUAD (Hessian node): v = e_1 for every coordinate
+                    if ((KIND == EDGE_MIX && sc == nullptr) || Q8)  // QUAD (Hessian node): v = e_1 everywhere
                         scal[e][4 + j] = (ok && j == 0) ? 1.f : 0.f;
                     else
                         scal[e][4 + j] = (ok && j < ns) ? sc[cd * ns + j] : 0.f;
@@ -330,6 +338,10 @@ __global__ __launch_bounds__(edge_threads(KIND)) void edge_kernel(const float* _
                         scal[e][8 + j] = (ok && sgy != nullptr && j < o) ? sgy[cd * o + j] : 0.f;
                         scal[e][12 + j] = (ok && j < o) ? (su != nullptr ? su[cd * o + j] : 1.f) : 0.f;
                     }
+                } else if constexpr (Q8) {
+#pragma unroll
+                    for (int j = 0; j < MAXO; ++j)
+                        scal[e][12 + j] = (ok && j < o) ? (su != nullptr ? su[cd * o + j] : 1.f) : 0.f;
                 } else if constexpr (KIND == EDGE_MIX) {
 #pragma unroll
                     for (int k = 0; k < MAXD; ++k)  // QUAD: g = e_2 (d = 2) when sgy == nullptr
@@ -343,9 +355,35 @@ __global__ __launch_bounds__(edge_threads(KIND)) void edge_kernel(const float* _
             }
             __syncthreads();
             if (t < h) {
-#pragma unroll(JETK ? 8 : (KIND == EDGE_J2 ? 2 : 1))
+#pragma unroll(JETK ? 8 : (KIND == EDGE_J2 || Q8 ? 2 : 1))
                 for (int i = 0; i < nt; ++i) {
                     const int64_t tile = c0 + i;
+                    if constexpr (Q8) {
+                        // row t of tile 2p: value (cols 0..7) | zb d/dx_1 (8..15); tile 2p + 1: zb d/dx_2 (0..7) and
+                        // the a_L jet's Q stream (r1, cols 8..15)
+                        const f32x4* za = (const f32x4*)(r0 + tile * tstride + t * 16);
+                        const f32x4* zc = (const f32x4*)(r0 + tile * tstride + h * 16 + t * 16);
+                        const f32x4* aq = (const f32x4*)(r1 + tile * tstride + h * 16 + t * 16 + 8);
+                        f32x4 zv[2], z1[2], z2[2], a3[2];
+#pragma unroll
+                        for (int hh = 0; hh < 2; ++hh) {
+                            zv[hh] = za[hh];
+                            z1[hh] = za[2 + hh];
+                            z2[hh] = zc[hh];
+                            a3[hh] = aq[hh];
+                        }
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) {
+                            const float* sv = scal[i * 8 + e];
+                            const float v0 = zv[e >> 2][e & 3];
+                            gb0 += v0;
+                            gw0[0] += v0 * sv[0] + z1[e >> 2][e & 3];
+                            gw0[1] += v0 * sv[1] + z2[e >> 2][e & 3];
+#pragma unroll
+                            for (int j = 0; j < MAXO; ++j) gwo[j] += sv[12 + j] * a3[e >> 2][e & 3];
+                        }
+                        continue;
+                    }
                     const f32x4* a = (const f32x4*)(r0 + tile * tstride + t * 16);
                     const f32x4* b = (const f32x4*)(r1 + tile * tstride + t * 16);
                     f32x4 av[4], bv[4], cv[4], ev[4];
@@ -459,7 +497,7 @@ __global__ __launch_bounds__(edge_threads(KIND)) void edge_kernel(const float* _
                     if (j < o) out[ewo + (int64_t)j * h + t] = gwo[j];
                     if (j < o && t == j) out[ebo + t] = gbj[j];
                 }
-            } else if constexpr (KIND == EDGE_MIX) {
+            } else if constexpr (KIND == EDGE_MIX || Q8) {
 #pragma unroll
                 for (int j = 0; j < MAXO; ++j)
                     if (j < o) out[ewo + (int64_t)j * h + t] = gwo[j];

@@ -45,6 +45,13 @@ void launch_small_mix(dim3 grid, hipStream_t st, const float* abuf, const float*
                        h, (int64_t)0, (int64_t)0);
 }
 
+void launch_small_q8(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* u,
+                     int64_t n, int64_t n_pad, int64_t tps, float* eslab, int64_t E, int d, int o, int lh) {
+    hipLaunchKernelGGL(edge_kernel<EDGE_Q8>, grid, dim3(edge_threads(EDGE_Q8)), 0, st, dbuf,
+                       abuf + (int64_t)lh * 4 * n_pad * H, NOF, NOF, x, NOF, NOF, u, n, n_pad / 8, tps, eslab, E, d, o,
+                       lh, H, (int64_t)0, (int64_t)0);
+}
+
 // rows: zb_0 jet (dbuf layer 0), a_L jet (abuf layer L) of the two-stream tiles (2 n_pad columns per layer, h = 512)
 void launch_small_j2(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* v,
                      const float* gy, const float* u, int64_t n, int64_t n_pad, int64_t tps, float* eslab, int64_t E,

@@ -48,7 +48,11 @@ def main(d, n, out):
         if 'SQ_VALU_MFMA_BUSY_CYCLES' in avg and 'GRBM_GUI_ACTIVE' in vals[k]:
             pass
         res[k] = r
-    json.dump({'n': n, 'kernels': res}, open(out, 'w'), indent=1, sort_keys=True)
+    # stamp: the sources of the library the profiled process ran (bench.py reports traffic only for a matching build)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import __graft_entry__
+    json.dump({'n': n, 'kernels': res, 'source_hash': __graft_entry__._source_hash()}, open(out, 'w'), indent=1,
+              sort_keys=True)
     print(json.dumps({k: {kk: vv for kk, vv in v.items() if kk != 'counters_avg_per_dispatch'} for k, v in res.items()},
                      indent=1))
     for k, v in res.items():
