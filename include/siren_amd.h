@@ -96,8 +96,10 @@ int32_t siren_forward(const siren_cfg* cfg, const float* ws, const float* x, int
 /* W1 (forward + coordinate vector-Jacobian product) in ONE launch:
  *   y  = Phi(x)                       (skipped when y == NULL)
  *   gx = sum_j gy_j * dPhi_j/dx       (gy == NULL means gy = ones: diff_operators.gradient, d.o.py:39-43)
- * hidden 256: n_hidden must be 1..3 (cos(w z_l) of every layer stays in registers; tws may be NULL); hidden 512:
- * 1..8 (cos is spilled to the caller's workspace tws, siren_forward_grad_ws_floats(cfg, n) floats). */
+ * hidden 256: n_hidden 1..3 keeps cos(w z_l) of every layer in registers (ONE launch; tws may be NULL); 4..5 (linear
+ * output, nonzero omegas) runs the stored split's forward half (y + lane-major cos of every layer into tws) and its
+ * reverse half (two launches); hidden 512: 1..8 (cos is spilled to tws). tws: siren_forward_grad_ws_floats(cfg, n)
+ * floats (0 for hidden 256 with 1..3 hidden layers). */
 int32_t siren_forward_grad_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count);
 int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x, int64_t n,
                            const float* gy, float* y, float* gx, float* tws, void* stream);
@@ -112,7 +114,8 @@ int32_t siren_forward_laplace(const siren_cfg* cfg, const float* ws, const float
                               float* gx, float* lap, void* stream);
 
 /* fp32 values of backward workspace siren_backward() needs for n coordinates (sin activations and deltas of
- * every sine layer, plus the split-K partial gradient slabs). */
+ * every sine layer, plus the split-K partial gradient slabs; hidden 256 with 4..5 hidden layers: + the stored split's
+ * cos buffer, siren_backward then runs siren_forward_store + siren_backward_stored internally). */
 int32_t siren_train_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count);
 
 /* W2 backward for one coordinate batch: given gy = dL/dy (n, d_out), writes
@@ -337,10 +340,10 @@ int32_t siren_forward_store_batched(const siren_cfg* cfg, const float* ws, const
 int32_t siren_backward_stored_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
                                       const float* gy, float* tws, float* gx, float* gparams, void* stream);
 
-/* ---- stored-forward W2 split (linear output; hidden 256: 1..3 hidden layers, hidden 512: 1..8) --------------
+/* ---- stored-forward W2 split (linear output; hidden 256: 1..5 hidden layers, hidden 512: 1..8) --------------
  * The training forward (model(model_input), training.py:72) keeps what the backward needs, so
  * train_loss.backward() (training.py:96) runs the L reverse GEMMs only instead of recomputing the forward:
- *   siren_forward_store : W0 (y) + a_l tiles and cos(w z_l) of every sine layer into tws
+ *   siren_forward_store : W0 (y, nullable at hidden 256) + a_l tiles and cos(w z_l) of every sine layer into tws
  *   siren_backward_stored: reverse sweep from the stored cos + split-K MFMA wgrad + edge layers + slab reduction,
  *                          same outputs as siren_backward (gx, gparams); tws must hold siren_forward_store's output
  * tws: siren_train_stored_ws_floats(cfg, n) floats (siren_train_ws_floats + the cos buffer). */

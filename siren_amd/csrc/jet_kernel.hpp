@@ -37,7 +37,6 @@
 // per-coordinate quadratic form Q (jet_sin_q / jet_sin_adjoint_q); tq (n, d, d) = G; gu_j = D2 y_j[Q].
 #include <type_traits>
 
-#include "hess_kernel.hpp"
 #include "lds_ops.h"
 #include "ring.hpp"
 #include "siren_common.h"
@@ -81,21 +80,17 @@ enum { JET_BOTH = 0, JET_FWD = 1, JET_REV = 2 };
 // JET_FWD: glap is unused and the outputs go to y (n, o) / gx (n, d) / lap (n) (each nullable)
 // MIX: tv / tg (n, d) the tangents v / g, tu (n, o) the output weighting (NULL = ones); gv (n, d) and gu (n, o)
 // nullable outputs; glap unused (JET_BOTH only)
-// KEPT (QG only): the forward jets come from the Hessian node's forward (hess_kernel.hpp KEEP scratch `kept`): no
-// forward sweep at all. Each reverse epilogue loads the z-jet of its layer (stream 3: z_3 = sum_ij Q_ij d2z/dx_i dx_j
-// of the kept second-order streams) and forms both the a-jet (abuf, for the weight gradient) and the adjoint
-// (jet_sin_q_both), so neither the z-jet scratch round trip nor the forward GEMMs remain.
-template <int PHASE, bool MIX = false, bool QG = false, bool KEPT = false>
+// (The backward of a Hessian node that kept its forward jets is qf_kernel.hpp: reverse GEMMs only, on the node's own
+// 8-coordinate layout.)
+template <int PHASE, bool MIX = false, bool QG = false>
 __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
     const float* __restrict__ ws, const float* __restrict__ x, int64_t n, const float* __restrict__ glap,
     float* __restrict__ gx, int d, int o, int lh, float w0, float w, float* __restrict__ spill,
     float* __restrict__ abuf, float* __restrict__ dbuf, int64_t n_pad, float* __restrict__ y,
     float* __restrict__ lap, const float* __restrict__ tv, const float* __restrict__ tg,
-    const float* __restrict__ tu, float* __restrict__ gv, float* __restrict__ gu, const float* __restrict__ tq = nullptr,
-    const float* __restrict__ kept = nullptr) {
+    const float* __restrict__ tu, float* __restrict__ gv, float* __restrict__ gu, const float* __restrict__ tq = nullptr) {
     static_assert(!MIX || PHASE == JET_BOTH, "the mixed jet runs as one launch");
     static_assert(!QG || MIX, "the quadratic-form jet is the mixed jet's variant");
-    static_assert(!KEPT || QG, "the kept forward is the Hessian node's");
     __shared__ __attribute__((aligned(16))) float lds[NBUF * SLICE + SMALL_MAX];
     float* ring = lds;
     float* sm = lds + NBUF * SLICE;
@@ -145,49 +140,9 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
         }
     }
     auto qload = [&]() -> f32x2 { return qreg; };
-    // KEPT: this lane's stream of the kept jet (hess_kernel.hpp layout: stream -> (tile, column) of its 8-coordinate
-    // group; lanes of stream 3 combine the three second-order streams with (G_11, G_12 + G_21, G_22))
-    const float* kb0p = nullptr;
-    int64_t kd1 = 0, kd2 = 0, kls = 0;
-    float kc0 = 1.f, kc1 = 0.f, kc2 = 0.f;
-    if constexpr (KEPT) {
-        const int64_t ng = hess_groups(n), grp = coord >> 3;
-        const int cc = (int)(coord & 7);
-        const int t0 = js == 3 ? 1 : js >> 1, col0 = (js == 1 || js == 3) ? cc + 8 : cc;
-        kb0p = kept + hess_kept_off(ng, 0, grp, 0, t0, 0) + (16 * g + col0) * 4;
-        if (js == 3) {  // d2z/dx_1dx_2 at (2, cc), d2z/dx_2^2 at (2, cc + 8)
-            kd1 = hess_kept_off(ng, 0, grp, 0, 2, 0) + (16 * g + cc) * 4 - (kb0p - kept);
-            kd2 = kd1 + 8 * 4;
-            if (valid) {
-                const float* gq = tq + coord * d * d;
-                kc0 = gq[0];
-                kc1 = d > 1 ? gq[1] + gq[2] : 0.f;
-                kc2 = d > 1 ? gq[3] : 0.f;
-            } else {
-                kc0 = 0.f;
-            }
-        }
-        kls = ng * NB * 3 * 256;
-    }
-    // layer l's reader: blocks in order, the pointer stepped through an opaque register (as LaneBlocks) so the
-    // compiler cannot hoist a whole layer's loads (3 x 16 f32x4) ahead of their use
-    typedef const __attribute__((address_space(1))) f32x4 gf32x4;  // global (not flat) loads
-    struct KeptReader {
-        const float* p;
-        int64_t d1, d2;
-        float c0, c1, c2;
-        __device__ __forceinline__ f32x4 next() {
-            asm volatile("" ::: "memory");  // one block's loads at a time (no hoisting of the layer's 48 loads)
-            const f32x4 v = c0 * *(gf32x4*)p + c1 * *(gf32x4*)(p + d1) + c2 * *(gf32x4*)(p + d2);
-            p += 768;
-            asm volatile("" : "+v"(p));
-            return v;
-        }
-    };
-    auto kreader = [&](int l) { return KeptReader{kb0p + l * kls, kd1, kd2, kc0, kc1, kc2}; };
     __syncthreads();
     const int p0 = PHASE == JET_REV ? lh : 0, p1 = PHASE == JET_FWD ? lh : 2 * lh;
-    int s = (KEPT ? lh : p0) * NB;  // KEPT: the ring starts at the first reverse slice
+    int s = p0 * NB;
     ring_issue(stream, ring, s, nslices, wave, lane);
     ring_issue(stream, ring, s + 1, nslices, wave, lane);
     // slice s0 published before the first pass (its successors are published by the mid-slice barriers)
@@ -196,50 +151,7 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
 
     // ---- first layer: z_0 jet (VALU, K = d_in) ---------------------------------------------------------------
     f32x4 act[NB], acc[NB];
-    if constexpr (KEPT) {
-        // no forward sweep: the seed at layer L from the kept z_L jet (a_L jet -> abuf, gu), then the reverse GEMMs
-        const f32x2 qc = qload();
-        float uw[MAXO], gup[MAXO];
-#pragma unroll
-        for (int j = 0; j < MAXO; ++j) {
-            uw[j] = j < o ? (tu != nullptr ? (valid ? tu[coord * o + j] : 0.f) : 1.f) : 0.f;
-            gup[j] = 0.f;
-        }
-        auto seed_blocks = [&](auto with_gu) {
-            float* ap = abuf + (int64_t)lh * lstride + toff;
-            KeptReader kr = kreader(lh);
-#pragma unroll
-            for (int rb = 0; rb < NB; ++rb) {
-                const float* wo = sm + SM_WO + 16 * rb + 4 * g;  // WoT rows j >= o are zero padded
-                const f32x4 sd = uw[0] * *(const f32x4*)wo + uw[1] * *(const f32x4*)(wo + H) +
-                                 uw[2] * *(const f32x4*)(wo + 2 * H) + uw[3] * *(const f32x4*)(wo + 3 * H);
-                f32x4 a;
-                act[rb] = jet_sin_q_both(gl * sd, kr.next(), w, val, kb, kg, qc[0], qc[1], val, m12, a);
-                store_block(ap, 0, a);
-                ap += 256;
-                asm volatile("" : "+v"(ap));
-                if constexpr (decltype(with_gu)::value) {
-#pragma unroll
-                    for (int j = 0; j < MAXO; ++j) {
-                        const f32x4 wj = *(const f32x4*)(wo + j * H);
-                        gup[j] += wj[0] * a[0] + wj[1] * a[1] + wj[2] * a[2] + wj[3] * a[3];
-                    }
-                }
-            }
-        };
-        if (gu != nullptr)
-            seed_blocks(std::true_type{});
-        else
-            seed_blocks(std::false_type{});
-        if (gu != nullptr) {  // gu_j = D2 y_j[Q] = Wout_j . a_L,second (stream-3 lanes)
-#pragma unroll
-            for (int j = 0; j < MAXO; ++j) {
-                const float pj = sum_groups(gup[j]);
-                if (j < o && valid && g == 0 && js == 3) gu[coord * o + j] = pj;
-            }
-        }
-        jstore_tile(dbuf + (int64_t)lh * lstride + toff, act);
-    } else if (PHASE == JET_REV) {
+    if (PHASE == JET_REV) {
         // seed from the stored z_L jet (the JET_FWD launch's scratch)
         LaneBlocks zl{sp + (int64_t)lh * lstride};
 #pragma unroll
@@ -271,7 +183,7 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
     }
 
 #pragma unroll 1
-    for (int p = KEPT ? lh : p0; p < p1; ++p) {
+    for (int p = p0; p < p1; ++p) {
         {
 #pragma unroll
             for (int ob = 0; ob < NB; ++ob) acc[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -389,19 +301,7 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
             LaneBlocks zl{sp + (int64_t)lm * lstride};
             const float wl = lm == 0 ? w0 : w;
             const f32x2 qc = qload();
-            if constexpr (KEPT) {  // the a_lm jet (-> abuf) and the adjoint from the kept z_lm jet, one pass
-                const float kbl = lm == 0 ? kb0 : kb, kgl = lm == 0 ? kg0 : kg;
-                float* ap = abuf + (int64_t)lm * lstride + toff;
-                KeptReader kr = kreader(lm);
-#pragma unroll
-                for (int rb = 0; rb < NB; ++rb) {
-                    f32x4 a;
-                    act[rb] = jet_sin_q_both(acc[rb], kr.next(), wl, val, kbl, kgl, qc[0], qc[1], val, m12, a);
-                    store_block(ap, 0, a);
-                    ap += 256;
-                    asm volatile("" : "+v"(ap));
-                }
-            } else {
+            {
 #pragma unroll
                 for (int rb = 0; rb < NB; ++rb) {
 #if SIREN_PROBE >= 1  // timing probe (tools/probe_build.sh): no epilogue arithmetic

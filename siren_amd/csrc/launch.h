@@ -32,6 +32,8 @@ void launch_legacy_grad(bool store, dim3 grid, hipStream_t st, const FusedArgs& 
 // launch_w0s = MODE_FWDS
 void launch_w1(int mode, dim3 grid, hipStream_t st, const FusedArgs& a);
 void launch_w0(dim3 grid, hipStream_t st, const FusedArgs& a);
+// tu_w1deep.hip: MODE_FWDS / MODE_REV of the W1 kernel at 4..5 hidden layers (hidden 256)
+void launch_w1_deep(int mode, dim3 grid, hipStream_t st, const FusedArgs& a);
 void launch_w0s(dim3 grid, hipStream_t st, const FusedArgs& a);
 // tu_w1x.hip: split-bf16 W1 (bf16x6 products on the bf16 matrix pipe; 3 hidden layers, d_in 2 / 3, d_out 1,
 // gy = ones); the stream holds split_stream_words(lh) 32-bit words
@@ -62,7 +64,7 @@ void launch_jet_mix(dim3 grid, hipStream_t st, const float* ws, const float* x, 
                     float w, float* spill, float* abuf, float* dbuf, int64_t n_pad);
 void launch_jet_quad(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* G,
                      const float* u, float* gx, float* gu, int d, int o, int lh, float w0, float w, float* spill,
-                     float* abuf, float* dbuf, int64_t n_pad, const float* kept = nullptr);
+                     float* abuf, float* dbuf, int64_t n_pad);
 // tu_hess.hip: the Hessian node's forward, Hm (n, d, d) = sum_j u_j H_j (d <= 2) in one 6-stream forward jet sweep
 // (grid = hess_groups(n) / 4 workgroups); kept (nullable) receives the per-layer jets for launch_jet_quad
 void launch_hess(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* u, int d, int o,

@@ -126,8 +126,8 @@ __global__ __launch_bounds__(THREADS, 1) void qf_rev_kernel(const float* __restr
     const bool valid = coord < n;
     const int64_t lstride = 4 * n_pad * H;                  // floats per layer of abuf / dbuf
     const int64_t toff = 2 * grp * (H * 16) + 4 * g * 16 + c;  // tile 0 of the pair; tile 1 at + H * 16
-    const float* kp = kept + hess_kept_off(ngroups, 0, grp, 0, 0, lane);
-    const int64_t kl = ngroups * NB * 3 * 256;  // floats per layer of the kept scratch
+    const float* kp = kept + hess_kept_off(ngroups, lh, 0, grp, 0, 0, lane);
+    const int64_t kl = hess_kept_lstride(ngroups);  // floats between layers of the kept scratch
     QfCoef q;
     {
         const float* gq = G + coord * d * d;

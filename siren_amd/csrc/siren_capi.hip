@@ -73,6 +73,13 @@ int64_t ws_floats(const siren_cfg* cfg) {
 bool w1_ok(const siren_cfg* cfg) {
     return !wide(cfg) && !layered(cfg) && cfg->omega_first != 0.f && cfg->omega_hidden != 0.f;
 }
+// hidden 256 with 4..5 hidden layers (FCBlock builds any depth, modules.py:65-80): cos(w z_l) of every layer no longer
+// fits the register file, so W1 / W2 / the kept W3 run the stored split through HBM (MODE_FWDS + MODE_REV,
+// tu_w1deep.hip) and W3 the serial kernel's layer loops
+bool deep(const siren_cfg* cfg) {
+    return w1_ok(cfg) && cfg->outermost_linear && (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0 &&
+           cfg->n_hidden > siren::MAX_LH_GRAD && cfg->n_hidden <= siren::MAX_LH_DEEP;
+}
 int layered_call(int mode, const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* gy, float* y,
                  float* gx, float* gp, float* tws, void* stream, const char* what) {
     const siren::LayeredPlan plan(cfg->d_in, cfg->hidden, cfg->n_hidden, cfg->d_out, n);
@@ -258,18 +265,37 @@ int32_t siren_forward_grad_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* c
     if (int rc = check_cfg(cfg, true)) return rc;
     if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
     const int64_t n_pad = (n + siren::TILE - 1) / siren::TILE * siren::TILE;
-    *count = wide(cfg) ? (int64_t)cfg->n_hidden * n_pad * cfg->hidden : 0;
+    *count = wide(cfg)   ? (int64_t)cfg->n_hidden * n_pad * cfg->hidden
+             : deep(cfg) ? (int64_t)(cfg->n_hidden + 1) * n_pad * siren::H  // lane-major cos of layers 0..L
+                         : 0;
     return SIREN_OK;
 }
 
 int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* gy,
                            float* y, float* gx, float* tws, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
-    if (cfg->n_hidden > siren::MAX_LH_GRAD && !wide(cfg) && !layered(cfg))
-        return fail(SIREN_EUNSUPPORTED, "siren_forward_grad needs 1 <= num_hidden_layers <= 3 at hidden 256");
+    if (cfg->n_hidden > siren::MAX_LH_GRAD && !wide(cfg) && !layered(cfg) && !deep(cfg))
+        return fail(SIREN_EUNSUPPORTED, "siren_forward_grad needs 1 <= num_hidden_layers <= 5 at hidden 256 (linear "
+                                        "output, nonzero omegas beyond 3)");
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
     if (n == 0) return SIREN_OK;
     if (ws == nullptr || x == nullptr || gx == nullptr) return fail(SIREN_EINVAL, "ws/x/gx is NULL");
+    if (deep(cfg)) {
+        // forward half (y + the lane-major cos of every layer into tws; no a_l tiles), then the reverse GEMMs from
+        // that cos with the output cotangent gy (no delta tiles)
+        if (tws == nullptr)
+            return fail(SIREN_EINVAL, "siren_forward_grad at 4..5 hidden layers needs tws (siren_forward_grad_ws_floats)");
+        const int64_t blocks = (n + siren::TILE - 1) / siren::TILE;
+        if (blocks > 0x7fffffffll) return fail(SIREN_EINVAL, "n too large");
+        const int64_t n_pad = blocks * siren::TILE;
+        siren::FusedArgs ff{w1_ws(cfg, ws), x, n, nullptr, y, nullptr, cfg->d_in, cfg->d_out, cfg->n_hidden,
+                            cfg->omega_first, cfg->omega_hidden, 0, nullptr, tws, n_pad};
+        siren::launch_w0s(dim3((unsigned)blocks), (hipStream_t)stream, ff);
+        siren::FusedArgs fr{w1_ws(cfg, ws), x, n, gy, nullptr, gx, cfg->d_in, cfg->d_out, cfg->n_hidden,
+                            cfg->omega_first, cfg->omega_hidden, 0, tws, nullptr, n_pad};
+        siren::launch_w1(siren::MODE_REV, tile_grid(cfg, blocks, 1), (hipStream_t)stream, fr);
+        return hip_status("siren_forward_grad (4..5 hidden layers)");
+    }
     if (layered(cfg))
         return layered_call(siren::LAY_FWD | siren::LAY_Y | siren::LAY_GX, cfg, ws, x, n, gy, y, gx, nullptr, nullptr,
                             stream, "siren_forward_grad");
@@ -390,7 +416,12 @@ int32_t siren_forward_laplace(const siren_cfg* cfg, const float* ws, const float
 int32_t siren_train_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
-    *count = layered(cfg) ? 0 : TrainPlan(cfg, n).total;
+    if (layered(cfg)) {
+        *count = 0;
+    } else {
+        const TrainPlan plan(cfg, n);
+        *count = plan.total + (deep(cfg) ? plan.act_floats : 0);  // deep: + the stored split's lane-major cos
+    }
     return SIREN_OK;
 }
 
@@ -398,9 +429,19 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
                        float* tws, void* reserved, float* gx, float* gparams, void* stream) {
     (void)reserved;
     if (int rc = check_cfg(cfg, true)) return rc;
-    if (cfg->n_hidden > siren::MAX_LH_GRAD && !wide(cfg) && !layered(cfg))
-        return fail(SIREN_EUNSUPPORTED, "siren_backward needs 1 <= num_hidden_layers <= 3 at hidden 256");
+    if (cfg->n_hidden > siren::MAX_LH_GRAD && !wide(cfg) && !layered(cfg) && !deep(cfg))
+        return fail(SIREN_EUNSUPPORTED, "siren_backward needs 1 <= num_hidden_layers <= 5 at hidden 256 (linear "
+                                        "output, nonzero omegas beyond 3)");
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    if (deep(cfg)) {  // the stored split in one call: forward half into tws, then the reverse-only backward
+        if (n == 0) {  // empty tensors may carry NULL data pointers: only gparams is written
+            if (gparams == nullptr) return fail(SIREN_EINVAL, "gparams is NULL");
+            (void)hipMemsetAsync(gparams, 0, param_count(cfg) * sizeof(float), (hipStream_t)stream);
+            return hip_status("siren_backward");
+        }
+        if (int rc = siren_forward_store(cfg, ws, x, n, nullptr, tws, stream)) return rc;
+        return siren_backward_stored(cfg, ws, x, n, gy, tws, gx, gparams, stream);
+    }
     if (layered(cfg)) {  // the chunk scratch lives in ws; tws is not used
         if (n == 0) {  // empty tensors may carry NULL data pointers: only gparams is written
             if (gparams == nullptr) return fail(SIREN_EINVAL, "gparams is NULL");
@@ -452,7 +493,7 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
 // ---- stored-forward W2 split: the training forward keeps a_l and cos(w z_l) so the backward is reverse-only ----
 bool stored_ok(const siren_cfg* cfg) {
     if (!cfg->outermost_linear || (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) != 0) return false;
-    return wide(cfg) || layered(cfg) || (w1_ok(cfg) && cfg->n_hidden <= siren::MAX_LH_GRAD);
+    return wide(cfg) || layered(cfg) || (w1_ok(cfg) && cfg->n_hidden <= siren::MAX_LH_DEEP);
 }
 // stored-split workspace: [a_l tiles][delta_l tiles][partial slabs][hidden 512: cos scratch of L + 1 layers]
 // [hidden 256: lane-major cos of L + 1 layers]; layered path: [a_0..a_L][cos_0..cos_L], n x H rows each
@@ -463,7 +504,7 @@ float* stored_cos(const siren_cfg* cfg, const TrainPlan& plan, float* tws) {
 int32_t siren_train_stored_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (!stored_ok(cfg))
-        return fail(SIREN_EUNSUPPORTED, "the stored-forward W2 split needs a linear output layer (hidden 256: 1..3 "
+        return fail(SIREN_EUNSUPPORTED, "the stored-forward W2 split needs a linear output layer (hidden 256: 1..5 "
                                         "hidden layers)");
     if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
     if (layered(cfg)) {
@@ -481,10 +522,12 @@ int32_t siren_forward_store(const siren_cfg* cfg, const float* ws, const float* 
                             void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (!stored_ok(cfg))
-        return fail(SIREN_EUNSUPPORTED, "the stored-forward W2 split covers hidden 256, linear output, 1..3 hidden layers");
+        return fail(SIREN_EUNSUPPORTED, "the stored-forward W2 split covers hidden 256, linear output, 1..5 hidden layers");
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
     if (n == 0) return SIREN_OK;
-    if (ws == nullptr || x == nullptr || y == nullptr || tws == nullptr) return fail(SIREN_EINVAL, "ws/x/y/tws is NULL");
+    // y may be NULL (siren_backward's internal forward half at 4..5 hidden layers needs no output)
+    if (ws == nullptr || x == nullptr || tws == nullptr || (y == nullptr && (wide(cfg) || layered(cfg))))
+        return fail(SIREN_EINVAL, "ws/x/y/tws is NULL");
     if (layered(cfg))
         return layered_call(siren::LAY_FWD | siren::LAY_Y | siren::LAY_TWS, cfg, ws, x, n, nullptr, y, nullptr,
                             nullptr, tws, stream, "siren_forward_store");
@@ -508,7 +551,7 @@ int32_t siren_backward_stored(const siren_cfg* cfg, const float* ws, const float
                               float* tws, float* gx, float* gparams, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (!stored_ok(cfg))
-        return fail(SIREN_EUNSUPPORTED, "the stored-forward W2 split covers hidden 256, linear output, 1..3 hidden layers");
+        return fail(SIREN_EUNSUPPORTED, "the stored-forward W2 split covers hidden 256, linear output, 1..5 hidden layers");
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
     if (n == 0 && layered(cfg)) {  // empty tensors may carry NULL data pointers: only gparams is written
         if (gparams == nullptr) return fail(SIREN_EINVAL, "gparams is NULL");
@@ -861,7 +904,7 @@ int32_t siren_hessian_backward_kept(const siren_cfg* cfg, const float* ws, const
     float* spill = dbuf + plan.buf_floats;
     float* partial = spill + plan.buf_floats;
     siren::launch_jet_quad(dim3((unsigned)(plan.n_pad / 16)), st, ws, x, n, G, u, gx, gu, cfg->d_in, cfg->d_out,
-                           cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, spill, abuf, dbuf, plan.n_pad, kept);
+                           cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, spill, abuf, dbuf, plan.n_pad);
     if (int rc = hip_status("siren_hessian_backward (quadratic-form jet)")) return rc;
     if (gparams == nullptr) return SIREN_OK;
     siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden), st, abuf, dbuf, plan.cols, plan.tps,
@@ -963,8 +1006,9 @@ static int32_t second_order_impl(const siren_cfg* cfg, const float* ws, const fl
         if (kept != nullptr) return fail(SIREN_EUNSUPPORTED, "the kept-forward W3 covers hidden 256");
         return second_order_wide(cfg, ws, x, n, v, u, gy, tws, gx, gparams, ydot, stream);
     }
-    if (cfg->n_hidden > siren::MAX_LH_GRAD)
-        return fail(SIREN_EUNSUPPORTED, "siren_second_order needs 1 <= num_hidden_layers <= 3 at hidden 256");
+    if (cfg->n_hidden > siren::MAX_LH_GRAD && !deep(cfg))
+        return fail(SIREN_EUNSUPPORTED, "siren_second_order needs 1 <= num_hidden_layers <= 5 at hidden 256 (nonzero "
+                                        "omegas beyond 3)");
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
     if (ws == nullptr || tws == nullptr || gx == nullptr || (n > 0 && (x == nullptr || v == nullptr)))
         return fail(SIREN_EINVAL, "ws/x/v/tws/gx is NULL");
@@ -1323,7 +1367,8 @@ int32_t siren_train_batched_ws_floats(const siren_cfg* cfg, int64_t n, int64_t b
     if (count == nullptr || n < 0 || batch < 0) return fail(SIREN_EINVAL, "count is NULL or n / batch < 0");
     const bool grouped = grouped_w2(cfg, n);
     const TrainPlan plan(cfg, n, grouped ? batch : 1);
-    *count = grouped ? batch * plan.total : plan.total;
+    // element by element: one siren_backward workspace, reused (4..5 hidden layers: + the stored split's cos)
+    *count = grouped ? batch * plan.total : plan.total + (deep(cfg) ? plan.act_floats : 0);
     return SIREN_OK;
 }
 

@@ -29,6 +29,7 @@ constexpr int MAXD = 4;           // max in_features of the fused kernels
 constexpr int MAXO = 4;           // max out_features of the fused kernels
 constexpr int MAX_LH_FWD = 8;     // max hidden layers of the forward-only kernel
 constexpr int MAX_LH_GRAD = 3;    // max hidden layers of the forward+grad kernel (cos kept in VGPRs)
+constexpr int MAX_LH_DEEP = 5;    // hidden 256, 4..5 hidden layers: derivatives through the stored split (cos to HBM)
 
 // w1_kernel modes: W1 (forward + vjp_x), STORE (W2 backward stage 1: also writes a_l, delta_l), FWD (W0: forward
 // only, sin epilogues without cos, output layer folded into a final serial epilogue).
@@ -251,31 +252,6 @@ __device__ __forceinline__ f32x4 jet_sin_adjoint_q(const f32x4& u, const f32x4& 
         sincos_fast(w * z0, sn, cs);
         const float wc = w * cs, w2s = w * w * sn;
         const float t12 = w2s * (__builtin_fmaf(c1, z1, c2 * z2) * u3);
-        const float t0 = __builtin_fmaf(w2s, __builtin_fmaf(u1, z1, u2 * z2), u3 * K);
-        out[r] = __builtin_fmaf(wc, u[r], -__builtin_fmaf(m12, t12, m0 * t0));
-    }
-    return out;
-}
-
-// jet_sin_q and jet_sin_adjoint_q of one layer in one pass (the KEPT quadratic-form jet, whose forward jets come from
-// the Hessian node's kept scratch and are only consumed by the reverse): returns the adjoint zb of the pre-activation
-// jet z for the cotangent u, and the a-jet (for the weight gradient) in a; one sincos, K formed in registers
-__device__ __forceinline__ f32x4 jet_sin_q_both(const f32x4& u, const f32x4& z, float w, float ka, float kb, float kg,
-                                                float c1, float c2, float m0, float m12, f32x4& a) {
-    f32x4 out;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const float z0 = quad_bcast<0>(z[r]), z1 = quad_bcast<1>(z[r]), z2 = quad_bcast<2>(z[r]);
-        const float lin = __builtin_fmaf(c1, z1, c2 * z2);  // (2 Q z)_i on the stream-1 / 2 lanes
-        const float q2 = 0.5f * __builtin_fmaf(z1, quad_bcast<1>(lin), z2 * quad_bcast<2>(lin));
-        float sn, cs;
-        sincos_fast(w * z0, sn, cs);
-        a[r] = __builtin_fmaf(ka, sn, __builtin_fmaf(kb * cs, z[r], -(kg * sn) * q2));
-        // stream-3 lane: K = w^2 s z_3 + w^3 c z^T Q z (kg = w^2 there)
-        const float K = quad_bcast<3>(__builtin_fmaf(kg * sn, z[r], (kg * w * cs) * q2));
-        const float u1 = quad_bcast<1>(u[r]), u2 = quad_bcast<2>(u[r]), u3 = quad_bcast<3>(u[r]);
-        const float wc = w * cs, w2s = w * w * sn;
-        const float t12 = w2s * (lin * u3);
         const float t0 = __builtin_fmaf(w2s, __builtin_fmaf(u1, z1, u2 * z2), u3 * K);
         out[r] = __builtin_fmaf(wc, u[r], -__builtin_fmaf(m12, t12, m0 * t0));
     }

@@ -34,16 +34,13 @@ void launch_jet_mix(dim3 grid, hipStream_t st, const float* ws, const float* x, 
                        w, spill, abuf, dbuf, n_pad, NUL, NUL, v, g, u, gv, gu);
 }
 
-// backward of a Hessian node (QG: quadratic form G (n, d, d) per coordinate, tangents the coordinate axes, d <= 2)
+// backward of a Hessian node recomputing its forward jet (QG: quadratic form G (n, d, d) per coordinate, tangents the
+// coordinate axes, d <= 2); the kept-forward backward is qf_kernel.hpp (tu_hess.hip)
 void launch_jet_quad(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* G,
                      const float* u, float* gx, float* gu, int d, int o, int lh, float w0, float w, float* spill,
-                     float* abuf, float* dbuf, int64_t n_pad, const float* kept) {
-    if (kept != nullptr)  // the forward jets from the Hessian node's forward (hess_kernel.hpp KEEP)
-        hipLaunchKernelGGL((jet_store_kernel<JET_BOTH, true, true, true>), grid, dim3(THREADS), 0, st, ws, x, n, NOF,
-                           gx, d, o, lh, w0, w, spill, abuf, dbuf, n_pad, NUL, NUL, NOF, NOF, u, NUL, gu, G, kept);
-    else
-        hipLaunchKernelGGL((jet_store_kernel<JET_BOTH, true, true>), grid, dim3(THREADS), 0, st, ws, x, n, NOF, gx, d,
-                           o, lh, w0, w, spill, abuf, dbuf, n_pad, NUL, NUL, NOF, NOF, u, NUL, gu, G, NOF);
+                     float* abuf, float* dbuf, int64_t n_pad) {
+    hipLaunchKernelGGL((jet_store_kernel<JET_BOTH, true, true>), grid, dim3(THREADS), 0, st, ws, x, n, NOF, gx, d, o,
+                       lh, w0, w, spill, abuf, dbuf, n_pad, NUL, NUL, NOF, NOF, u, NUL, gu, G);
 }
 
 }  // namespace siren

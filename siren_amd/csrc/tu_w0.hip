@@ -27,7 +27,8 @@ void launch_w0s(dim3 grid, hipStream_t st, const FusedArgs& a) {
     switch (a.lh) {
         case 1: SIREN_L(1); break;
         case 2: SIREN_L(2); break;
-        default: SIREN_L(3); break;
+        case 3: SIREN_L(3); break;
+        default: launch_w1_deep(MODE_FWDS, grid, st, a); break;
     }
 #undef SIREN_L
 }

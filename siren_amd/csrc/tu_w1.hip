@@ -18,7 +18,8 @@ void launch_w1(int mode, dim3 grid, hipStream_t st, const FusedArgs& a) {
         switch (a.lh) {
             case 1: SIREN_L(1, MODE_REV); break;
             case 2: SIREN_L(2, MODE_REV); break;
-            default: SIREN_L(3, MODE_REV); break;
+            case 3: SIREN_L(3, MODE_REV); break;
+            default: launch_w1_deep(MODE_REV, grid, st, a); break;
         }
     } else if (mode == (MODE_W1 | MODE_PROF)) {
         SIREN_L(3, MODE_W1 | MODE_PROF);

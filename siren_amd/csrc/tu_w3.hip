@@ -11,7 +11,7 @@ void launch_w3(bool theta, dim3 grid, hipStream_t st, const float* ws, const flo
                float* Dt, int64_t n_pad, int d, int lh, float w0, float w, const float* kA, const float* kC,
                unsigned long long* prof, int64_t ws_bs, int64_t spill_bs, int64_t buf_bs, bool serial) {
     const bool kept = kA != nullptr && kC != nullptr;
-    if (!serial && prof == nullptr) {
+    if (!serial && prof == nullptr && lh <= MAX_LH_GRAD) {  // 4..5 hidden layers: the serial kernel's layer loops
 #define SIREN_I(TK)                                                                                                 \
     launch_w3i_##TK(grid, st, ws, x, v, gy, u, ydot, o, n, gx, spill, A, At, D, Dt, n_pad, d, lh, w0, w, kA, kC, ws_bs, \
                     spill_bs, buf_bs)
@@ -33,7 +33,9 @@ void launch_w3(bool theta, dim3 grid, hipStream_t st, const float* ws, const flo
     switch (lh) {                          \
         case 1: SIREN_L(1, TH, KP); break; \
         case 2: SIREN_L(2, TH, KP); break; \
-        default: SIREN_L(3, TH, KP); break; \
+        case 3: SIREN_L(3, TH, KP); break; \
+        case 4: SIREN_L(4, TH, KP); break; \
+        default: SIREN_L(5, TH, KP); break; \
     }
     if (theta && kept) {
         SIREN_LH(true, true);

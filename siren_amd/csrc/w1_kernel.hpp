@@ -145,6 +145,7 @@ struct W1Ctx {
     float* cst;   // FWDS: this lane's cos store base (cos_off(tile, wave, LH, 0, 0, lane))
     const char* cbase;  // REV: wave-uniform cos base of (tile, wave) (SGPRs), + 16 * lane per lane
     bool dstore;        // REV: store the delta tiles (false: gx only — the stored jet forward's dPhi/dx)
+    bool astore;  // FWDS: a_l tiles wanted (abuf != NULL; the deep W1's forward half keeps only the lane-major cos)
     bool more;    // persistent grid: this workgroup runs another coordinate tile after the current one, so the
                   // ring keeps streaming (slices 0..2 of the next tile are issued during the last 3 slices)
     int64_t lstride;
@@ -246,7 +247,10 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
             cs4[r] = cs;
         }
         if constexpr (!FWD) st.C[0][b] = pin(cs4);
-        if constexpr (STORE || FWDS) store_block(cx.abuf, b, st.act[b]);
+        if constexpr (STORE) store_block(cx.abuf, b, st.act[b]);
+        if constexpr (FWDS) {
+            if (cx.astore) store_block(cx.abuf, b, st.act[b]);
+        }
         if constexpr (FWDS) *(f32x4*)(cx.cst + b * 256) = cs4;
     } else if constexpr (KIND == EPI_SINCOS) {
         const f32x4 z = st.acc[(G + 1) & 1][b] + ep.v[0];
@@ -259,7 +263,10 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
             cs4[r] = cs;
         }
         if constexpr (!FWD) st.C[G][b] = to_agpr(cs4);
-        if constexpr (STORE || FWDS) store_block(cx.abuf + G * cx.lstride, b, st.act[b]);
+        if constexpr (STORE) store_block(cx.abuf + G * cx.lstride, b, st.act[b]);
+        if constexpr (FWDS) {
+            if (cx.astore) store_block(cx.abuf + G * cx.lstride, b, st.act[b]);
+        }
         if constexpr (FWDS) *(f32x4*)(cx.cst + (G * NB + b) * 256) = cs4;
     } else if constexpr (KIND == EPI_SEED && REV) {
         // delta_L = (gy Wout) . cos(w z_L) . w with cos from the forward's store
@@ -492,6 +499,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
     cx.dstore = dbuf != nullptr;
     cx.abuf = cx.dbuf = nullptr;
     cx.more = false;
+    cx.astore = abuf != nullptr;
     cx.prof = nullptr;
     cx.stream = ws + small_pad(LH) + (REV ? (int64_t)LH * NB * SLICE : 0);
     cx.lstride = n_pad * H;
@@ -625,7 +633,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
                     cs4[r] = cc;
                 }
                 if constexpr (FWDS) {
-                    store_block(cx.abuf + LH * cx.lstride, rb, sn);
+                    if (cx.astore) store_block(cx.abuf + LH * cx.lstride, rb, sn);
                     *(f32x4*)(cx.cst + (LH * NB + rb) * 256) = cs4;
                 }
 #pragma unroll
@@ -640,7 +648,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
             for (int j = 0; j < MAXO; ++j) {
                 if (j < o) {
                     const float yj = sum_groups(st.yp[j]) + sm[SM_BOUT + j];
-                    if (valid && cx.g == 0) y[coord * o + j] = yj;
+                    if (y != nullptr && valid && cx.g == 0) y[coord * o + j] = yj;
                 }
             }
         } else {

@@ -43,7 +43,12 @@ class SirenEngine:
         # hidden 256 keeps cos(w z_l) of every layer in registers (1..3 hidden layers); hidden 512 spills it; other
         # widths run the layered path (layered.hip: rocBLAS layer GEMMs + fused epilogues, W0 / W1 / W2 only)
         self.layered = int(hidden) not in (256, 512)
-        self.grad_supported = self.supported and (1 <= n_hidden <= 3 or int(hidden) == 512 or self.layered)
+        # hidden 256 at 4..5 hidden layers: cos no longer fits the registers, so W1 / W2 / the kept W3 run the stored
+        # split through HBM (siren_capi.hip deep(): MODE_FWDS + MODE_REV) and W3 the serial kernel
+        self.deep = (int(hidden) == 256 and 4 <= n_hidden <= 5 and bool(outermost_linear) and omega_first != 0
+                     and omega_hidden != 0 and not (int(flags) & 1))
+        self.grad_supported = self.supported and (1 <= n_hidden <= 3 or int(hidden) == 512 or self.layered
+                                                  or self.deep)
         # the W3 second-order kernel: hidden 256, d_out <= 4 (vector outputs via an output weighting), linear output
         # the W4 jet kernel (fused Laplacian): hidden 256, d_in <= 2, linear output, 1..5 hidden layers
         self.laplace_supported = (self.supported and int(hidden) == 256 and int(d_in) <= 2 and 1 <= n_hidden <= 5
@@ -51,11 +56,12 @@ class SirenEngine:
         # stored-forward W2 split: training forward keeps a_l / cos, backward is reverse-only
         # (layered widths: a_l / cos_l of every layer over all n rows, see stored_for)
         self.stored_supported = (self.supported and bool(outermost_linear) and not (int(flags) & 1) and
-                                 (int(hidden) == 512 or self.layered or (1 <= n_hidden <= 3 and omega_first != 0
+                                 (int(hidden) == 512 or self.layered or (1 <= n_hidden <= 5 and omega_first != 0
                                                                          and omega_hidden != 0)))
         # hidden 512: the two-stream jet kernel (wide_jet_kernel.hpp), 1..8 hidden layers
         self.second_order_supported = (self.supported and int(d_out) <= 4 and bool(outermost_linear)
-                                       and ((int(hidden) == 256 and 1 <= n_hidden <= 3) or int(hidden) == 512))
+                                       and ((int(hidden) == 256 and (1 <= n_hidden <= 3 or self.deep))
+                                            or int(hidden) == 512))
         # the third-order adjoint (mixed jet, siren_hvp_backward): linear output, hidden 256 with 1..5 hidden layers
         # or hidden 512 (wide_jet_kernel<4>)
         self.hvp_backward_supported = (self.supported and bool(outermost_linear)
@@ -125,7 +131,7 @@ class SirenEngine:
         diff_operators.gradient returns, diff_operators.py:39-43)."""
         self._require()
         if not self.grad_supported:
-            raise _lib.SirenUnsupported('siren_forward_grad needs 1 <= num_hidden_layers <= 3 at hidden 256')
+            raise _lib.SirenUnsupported('siren_forward_grad needs 1 <= num_hidden_layers <= 5 at hidden 256')
         x = self._check_x(x)
         n = x.shape[0]
         if gy is not None:
@@ -372,7 +378,7 @@ class SirenEngine:
         """
         self._require()
         if not self.grad_supported:
-            raise _lib.SirenUnsupported('siren_backward needs 1 <= num_hidden_layers <= 3 at hidden 256')
+            raise _lib.SirenUnsupported('siren_backward needs 1 <= num_hidden_layers <= 5 at hidden 256')
         x = self._check_x(x)
         n = x.shape[0]
         gy = gy.contiguous()
@@ -480,7 +486,7 @@ class SirenEngine:
         """W1 over (B, n, d_in): (y | None, J^T gy) with per-element weights."""
         self._require()
         if not self.grad_supported:
-            raise _lib.SirenUnsupported('siren_forward_grad needs 1 <= num_hidden_layers <= 3 at hidden 256')
+            raise _lib.SirenUnsupported('siren_forward_grad needs 1 <= num_hidden_layers <= 5 at hidden 256')
         x = self._check_xb(x)
         B, n = x.shape[:2]
         if gy is not None:
@@ -499,7 +505,7 @@ class SirenEngine:
         """W2 per element: (gx (B, n, d_in), gparams (B, param_count))."""
         self._require()
         if not self.grad_supported:
-            raise _lib.SirenUnsupported('siren_backward needs 1 <= num_hidden_layers <= 3 at hidden 256')
+            raise _lib.SirenUnsupported('siren_backward needs 1 <= num_hidden_layers <= 5 at hidden 256')
         x = self._check_xb(x)
         B, n = x.shape[:2]
         gy = gy.contiguous()

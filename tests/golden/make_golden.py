@@ -30,6 +30,10 @@ Fixtures:
       and fp64) and a slice of the fp64 image_mse theta-grads (first / output layers whole, 4 rows of every hidden W).
   G11 second / third order through G7's batched weights: gradients_mse and laplace_mse (divergence(gradient()))
       on SingleBVPNet(params=hypernetwork output), fp64 gradients w.r.t. the predicted weights and model_in.
+  G12 depth beyond 3 hidden layers at hidden 256 (FCBlock builds any depth, modules.py:65-80): SingleBVPNet(
+      num_hidden_layers=4 and 5) seed 0, d2 o1, 1024 coords: model_out / gradient / laplace (fp32 and fp64) and fp64
+      theta-grads of image_mse, gradients_mse, laplace_mse; and a d3 sdf batch (256 on + 256 off surface) at 5 hidden
+      layers with its fp64 sdf theta-grads.
   G6  vector outputs / PML losses: 5x256 d2 o2 (helmholtz_pml, loss_functions.py:139-211)
       and 5x256 d3 o1 (wave_pml, loss_functions.py:112-136), 1024 coords each: jacobian / hessian
       (diff_operators.py:5-24, 46-59), the loss terms and their fp64 theta-grads.
@@ -399,6 +403,45 @@ def make_g10(modules, D, L, meta):
     np.savez_compressed(os.path.join(OUT, 'golden_g10.npz'), **store)
 
 
+def make_g12(modules, D, L, meta):
+    store = {}
+    gen = torch.Generator().manual_seed(12)
+    coords = torch.rand(1, 1024, 2, generator=gen) * 2 - 1
+    gt = {'img': synth_image(coords),
+          'gradients': torch.randn(1, 1024, 2, generator=gen) * 10.,
+          'laplace': torch.randn(1, 1024, 1, generator=gen) * 100.}
+    store['coords'] = coords.numpy()
+    for k in ('img', 'gradients', 'laplace'):
+        store['gt_' + k] = gt[k].numpy()
+    for depth in (4, 5):
+        torch.manual_seed(0)
+        net = modules.SingleBVPNet(type='sine', in_features=2, out_features=1, num_hidden_layers=depth)
+        for k, v in state_to_np(net.state_dict()).items():
+            store['L%d_w_%s' % (depth, k)] = v
+        fixture_outputs(modules, D, L, net, coords, gt, 'L%d' % depth, store, meta)
+    gen = torch.Generator().manual_seed(121)
+    on = torch.randn(256, 3, generator=gen, dtype=torch.float64)
+    on_n = on / on.norm(dim=-1, keepdim=True)
+    coords3 = torch.cat([on_n * 0.5, torch.rand(256, 3, generator=gen, dtype=torch.float64) * 2 - 1], 0).float()[None]
+    normals = torch.cat([on_n, -torch.ones(256, 3, dtype=torch.float64)], 0).float()[None]
+    sdf = torch.cat([torch.zeros(256, 1), -torch.ones(256, 1)], 0)[None]
+    store['S5_coords'], store['S5_gt_sdf'], store['S5_gt_normals'] = coords3.numpy(), sdf.numpy(), normals.numpy()
+    torch.manual_seed(0)
+    net3 = modules.SingleBVPNet(type='sine', in_features=3, out_features=1, num_hidden_layers=5)
+    for k, v in state_to_np(net3.state_dict()).items():
+        store['S5_w_' + k] = v
+    net3 = net3.double()
+    out = net3({'coords': coords3.double()})
+    store['S5_gradient_f64'] = D.gradient(out['model_out'], out['model_in']).detach().numpy()
+    ld = L.sdf(out, {'sdf': sdf.double(), 'normals': normals.double()})
+    for k, v in ld.items():
+        meta['G12_S5_sdf_%s_f64' % k] = float(v)
+    grads, total = grads_of(net3, ld)
+    for k, v in grads.items():
+        store['S5_sdf_grad_' + k] = v
+    np.savez_compressed(os.path.join(OUT, 'golden_g12.npz'), **store)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--skip-fit', action='store_true', help='reuse the G5 weights already in golden_fit.npz')
@@ -409,7 +452,7 @@ def main():
         with open(os.path.join(OUT, 'manifest.json')) as f:
             meta = json.load(f)
         for name in args.only.split(','):
-            {'g6': make_g6, 'g7': make_g7, 'g8': make_g8, 'g9': make_g9, 'g10': make_g10, 'g11': make_g11}[name](modules, D, L, meta)
+            {'g6': make_g6, 'g7': make_g7, 'g8': make_g8, 'g9': make_g9, 'g10': make_g10, 'g11': make_g11, 'g12': make_g12}[name](modules, D, L, meta)
         with open(os.path.join(OUT, 'manifest.json'), 'w') as f:
             json.dump(meta, f, indent=1, sort_keys=True)
         return
