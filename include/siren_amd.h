@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SIREN_ABI_VERSION 4
+#define SIREN_ABI_VERSION 5
 
 enum {
     SIREN_OK = 0,
@@ -81,17 +81,25 @@ const char* siren_last_error(void);
 /* Number of fp32 values in the flat parameter buffer. */
 int32_t siren_param_count(const siren_cfg* cfg, int64_t* count);
 
-/* Number of fp32 values of packed-weight workspace that siren_pack() fills. Hidden widths other than 256 / 512 (the
- * layered path: rocBLAS layer GEMMs + HIP epilogues over 16384-coordinate chunks) add the chunk scratch to it: the
- * entry points then write into ws beyond the parameters, so calls sharing one ws must be ordered on one stream. */
+/* Number of fp32 values of packed-weight workspace that siren_pack() fills. ws is immutable between packs: no entry
+ * point writes it, so one ws may serve calls on several streams. Hidden widths other than 256 / 512 (the layered
+ * path: rocBLAS layer GEMMs + HIP epilogues over 16384-coordinate chunks) hold the parameters and W_l^T; their chunk
+ * scratch is the caller's tws of each entry point (siren_forward_ws_floats, siren_forward_grad_ws_floats,
+ * siren_train_ws_floats, siren_train_stored_ws_floats). */
 int32_t siren_workspace_floats(const siren_cfg* cfg, int64_t* count);
 
 /* Repack params into the kernels' LDS-slice layout (workspace ws, siren_workspace_floats() floats). */
 int32_t siren_pack(const siren_cfg* cfg, const float* params, float* ws, void* stream);
 
-/* W0 (forward value): y = Phi(x). Replaces SingleBVPNet.forward's model_out (modules.py:143-160). */
+/* W0 (forward value): y = Phi(x). Replaces SingleBVPNet.forward's model_out (modules.py:143-160).
+ * Hidden widths other than 256 / 512 (the layered path) need the caller's chunk scratch: siren_forward_ex with
+ * tws of siren_forward_ws_floats(cfg, n) floats (0 elsewhere; siren_forward = siren_forward_ex with tws NULL, which
+ * fails with SIREN_EINVAL on a layered network). ABI 5: the packed workspace ws is never written by any call. */
 int32_t siren_forward(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y,
                       void* stream);
+int32_t siren_forward_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count);
+int32_t siren_forward_ex(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y, float* tws,
+                         void* stream);
 
 /* W1 (forward + coordinate vector-Jacobian product) in ONE launch:
  *   y  = Phi(x)                       (skipped when y == NULL)
@@ -317,6 +325,10 @@ int32_t siren_hvp_backward_batched(const siren_cfg* cfg, const float* ws, const 
  * other configurations run siren_forward element by element. */
 int32_t siren_forward_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
                               float* y, void* stream);
+/* the same with the per-element workspace of siren_forward_ex (siren_forward_ws_floats(cfg, n); reused element
+ * after element; needed at layered widths only) */
+int32_t siren_forward_batched_ex(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
+                                 float* y, float* tws, void* stream);
 /* W1 (y, J^T gy) for every element in ONE grouped launch (hidden 256, linear output, 1..3 hidden layers; the
  * persistent grid is split across the elements); gy (B, n, d_out) nullable = ones. tws: the per-element workspace of
  * siren_forward_grad (siren_forward_grad_ws_floats(cfg, n); reused element after element, NULL at hidden 256). */

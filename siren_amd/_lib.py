@@ -11,7 +11,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('SIREN_AMD_LIB', os.path.join(_HERE, 'libsiren_amd.so'))
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # Error codes (include/siren_amd.h)
 SIREN_OK, SIREN_EINVAL, SIREN_EUNSUPPORTED, SIREN_EHIP = 0, 1, 2, 3
@@ -38,6 +38,8 @@ _SIGS = {
     'siren_workspace_floats': [_CFG, ctypes.POINTER(_I64)],
     'siren_pack': [_CFG, _P, _P, _P],
     'siren_forward': [_CFG, _P, _P, _I64, _P, _P],
+    'siren_forward_ws_floats': [_CFG, _I64, ctypes.POINTER(_I64)],
+    'siren_forward_ex': [_CFG, _P, _P, _I64, _P, _P, _P],
     'siren_forward_grad_ws_floats': [_CFG, _I64, ctypes.POINTER(_I64)],
     'siren_forward_grad': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P],
     'siren_forward_laplace': [_CFG, _P, _P, _I64, _P, _P, _P, _P],
@@ -58,6 +60,7 @@ _SIGS = {
     'siren_train_batched_ws_floats': [_CFG, _I64, _I64, ctypes.POINTER(_I64)],
     'siren_pack_batched': [_CFG, _P, _I64, _P, _P],
     'siren_forward_batched': [_CFG, _P, _P, _I64, _I64, _P, _P],
+    'siren_forward_batched_ex': [_CFG, _P, _P, _I64, _I64, _P, _P, _P],
     'siren_forward_grad_batched': [_CFG, _P, _P, _I64, _I64, _P, _P, _P, _P, _P],
     'siren_backward_batched': [_CFG, _P, _P, _I64, _I64, _P, _P, _P, _P, _P],
     'siren_sample_sdf': [_P, _P, _I64, _I64, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P],

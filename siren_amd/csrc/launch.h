@@ -131,7 +131,7 @@ void launch_edge_reduce(dim3 grid, hipStream_t st, const float* eslab, int64_t S
                         int64_t wout, float* gp, int64_t P, int64_t bstride_e);
 
 // layered.hip: hidden widths other than 256 / 512, layer by layer over coordinate chunks (rocBLAS GEMMs + fused
-// epilogues); the packed workspace = [params][chunk scratch]
+// epilogues); the packed workspace = [params][W_l^T] (immutable), the chunk scratch is the caller's
 constexpr int64_t LAYERED_CHUNK = 16384;
 constexpr int LAYERED_RPB = 64;  // rows per workgroup of the bias-reducing epilogues (slab rows = chunk / 64)
 enum LayeredMode : int {
@@ -143,14 +143,17 @@ enum LayeredMode : int {
 };
 struct LayeredPlan {
     int d, H, lh, o;
-    int64_t P, P_pad, chunk, buf, R, wt, scratch;
+    int64_t P, P_pad, chunk, buf, R, wt, scratch, scratch_stored;
     LayeredPlan(int d_, int H_, int lh_, int o_, int64_t n);
 };
 int64_t layered_ws_floats(int d, int H, int lh, int o);
+// chunk scratch of a call over n coordinates (stored: the stored split keeps a_l / cos_l in the caller's n-row buffers)
+int64_t layered_scratch_floats(int d, int H, int lh, int o, int64_t n, bool stored);
 void layered_pack(const LayeredPlan& plan, const float* params, float* ws, hipStream_t st);
 inline int64_t layered_stored_floats(int H, int lh, int64_t n) { return 2 * (int64_t)(lh + 1) * n * H; }
 int layered_run(int mode, const LayeredPlan& plan, const float* ws, float w0, float w, const float* x, int64_t n,
-                const float* gy, float* y, float* gx, float* gparams, float* tws, hipStream_t st, std::string& err);
+                const float* gy, float* y, float* gx, float* gparams, float* tws, float* scr, hipStream_t st,
+                std::string& err);
 
 // marching.hip: device marching cubes over an (X, Y, Z) volume; ws in uint32 words
 int64_t mc_ws_words(int64_t X, int64_t Y, int64_t Z);

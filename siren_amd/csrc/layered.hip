@@ -307,15 +307,23 @@ LayeredPlan::LayeredPlan(int d_, int H_, int lh_, int o_, int64_t n) : d(d_), H(
     if (n >= 0 && n < chunk) chunk = (n + 63) / 64 * 64 > 0 ? (n + 63) / 64 * 64 : 64;
     buf = chunk * (int64_t)H;
     R = (chunk + LAYERED_RPB - 1) / LAYERED_RPB;
-    // [params][W_1^T .. W_L^T][a_0..a_L][cos_0..cos_L][u ping-pong x 2][bias slabs: L + 1 layers x R x H]
-    // [dWout slab: o x R x H][dW0 slab: d x R x H][output-bias slab: R x o]
+    // packed workspace (immutable after siren_pack): [params][W_1^T .. W_L^T]
+    // caller's chunk scratch: [u ping-pong x 2][bias slabs: L + 1 layers x R x H][dWout slab: o x R x H]
+    //                         [dW0 slab: d x R x H][output-bias slab: R x o][a_0..a_L][cos_0..cos_L] (the last two
+    //                         only without the stored split, whose a_l / cos_l live in the caller's n-row buffers)
     wt = (int64_t)lh * H * H;
-    scratch = wt + 2 * (lh + 1) * buf + 2 * buf + (lh + 1 + o + d) * R * H + R * o;
+    scratch_stored = 2 * buf + (lh + 1 + o + d) * R * H + R * o;
+    scratch = scratch_stored + 2 * (lh + 1) * buf;
 }
 
 int64_t layered_ws_floats(int d, int H, int lh, int o) {
     const LayeredPlan p(d, H, lh, o, -1);
-    return p.P_pad + p.scratch;
+    return p.P_pad + p.wt;
+}
+
+int64_t layered_scratch_floats(int d, int H, int lh, int o, int64_t n, bool stored) {
+    const LayeredPlan p(d, H, lh, o, n);
+    return stored ? p.scratch_stored : p.scratch;
 }
 
 void layered_pack(const LayeredPlan& pl, const float* params, float* ws, hipStream_t st) {
@@ -327,28 +335,29 @@ void layered_pack(const LayeredPlan& pl, const float* params, float* ws, hipStre
 }
 
 int layered_run(int mode, const LayeredPlan& pl, const float* ws, float w0, float w, const float* x, int64_t n,
-                const float* gy, float* y, float* gx, float* gparams, float* tws, hipStream_t st, std::string& err) {
+                const float* gy, float* y, float* gx, float* gparams, float* tws, float* scr, hipStream_t st,
+                std::string& err) {
     if (n <= 0) return 0;
     const int d = pl.d, H = pl.H, lh = pl.lh, o = pl.o;
     const ParamOffsets off(d, o, lh, H);
     const float* prm = ws;
     const float* WT = ws + pl.P_pad;                      // W_l^T at WT + (l - 1) H^2 (siren_pack)
-    float* scr = const_cast<float*>(ws) + pl.P_pad + pl.wt;  // the packed workspace is the caller's scratch
-    float* U0 = scr + 2 * (lh + 1) * pl.buf;
+    float* U0 = scr;                                      // the caller's chunk scratch (layered_scratch_floats)
     float* U1 = U0 + pl.buf;
     float* bslab = U1 + pl.buf;                          // bias slabs: layer l at bslab + l * R * H
     float* oslab = bslab + (lh + 1) * pl.R * H;           // dWout: o x R x H
     float* fslab = oslab + (int64_t)o * pl.R * H;         // dW0: d x R x H
     float* boslab = fslab + (int64_t)d * pl.R * H;        // dbout: R x o
+    float* acs = boslab + pl.R * o;                       // a_l / cos_l of the current chunk (no stored split)
     const bool stored = (mode & LAY_TWS) != 0, fwd = (mode & LAY_FWD) != 0;
     const bool gxm = (mode & LAY_GX) != 0, theta = (mode & LAY_THETA) != 0;
     const bool keep_cos = gxm || theta || stored;  // the forward keeps cos_l for a reverse sweep
     // a_l / cos_l of chunk c0: the caller's n-row buffers (stored split) or the chunk scratch
     auto A = [&](int l, int64_t c0) -> float* {
-        return stored ? tws + (int64_t)l * n * H + c0 * H : scr + (int64_t)l * pl.buf;
+        return stored ? tws + (int64_t)l * n * H + c0 * H : acs + (int64_t)l * pl.buf;
     };
     auto CS = [&](int l, int64_t c0) -> float* {
-        return stored ? tws + (int64_t)(lh + 1 + l) * n * H + c0 * H : scr + (int64_t)(lh + 1 + l) * pl.buf;
+        return stored ? tws + (int64_t)(lh + 1 + l) * n * H + c0 * H : acs + (int64_t)(lh + 1 + l) * pl.buf;
     };
     Blas blas(st);
     if (blas.h == nullptr) {

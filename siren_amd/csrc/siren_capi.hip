@@ -80,11 +80,18 @@ bool deep(const siren_cfg* cfg) {
     return w1_ok(cfg) && cfg->outermost_linear && (cfg->reserved & SIREN_FLAG_LEGACY_KERNEL) == 0 &&
            cfg->n_hidden > siren::MAX_LH_GRAD && cfg->n_hidden <= siren::MAX_LH_DEEP;
 }
+// scr: the caller's chunk scratch (layered_scratch); with LAY_TWS it follows the stored a_l / cos_l rows in tws
+int64_t layered_scratch(const siren_cfg* cfg, int64_t n, bool stored) {
+    return siren::layered_scratch_floats(cfg->d_in, cfg->hidden, cfg->n_hidden, cfg->d_out, n, stored);
+}
 int layered_call(int mode, const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* gy, float* y,
-                 float* gx, float* gp, float* tws, void* stream, const char* what) {
+                 float* gx, float* gp, float* tws, float* scr, void* stream, const char* what) {
+    if (n > 0 && scr == nullptr)
+        return fail(SIREN_EINVAL, std::string(what) + ": the layered path (hidden other than 256 / 512) needs the "
+                                  "caller's chunk scratch (tws; see the entry point's *_ws_floats query)");
     const siren::LayeredPlan plan(cfg->d_in, cfg->hidden, cfg->n_hidden, cfg->d_out, n);
     std::string err;
-    if (siren::layered_run(mode, plan, ws, cfg->omega_first, cfg->omega_hidden, x, n, gy, y, gx, gp, tws,
+    if (siren::layered_run(mode, plan, ws, cfg->omega_first, cfg->omega_hidden, x, n, gy, y, gx, gp, tws, scr,
                            (hipStream_t)stream, err) != 0)
         return fail(SIREN_EHIP, std::string(what) + ": " + err);
     return hip_status(what);
@@ -236,7 +243,19 @@ int32_t siren_pack(const siren_cfg* cfg, const float* params, float* ws, void* s
     return hip_status("siren_pack");
 }
 
+int32_t siren_forward_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count) {
+    if (int rc = check_cfg(cfg, true)) return rc;
+    if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
+    *count = layered(cfg) ? layered_scratch(cfg, n, false) : 0;
+    return SIREN_OK;
+}
+
 int32_t siren_forward(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y, void* stream) {
+    return siren_forward_ex(cfg, ws, x, n, y, nullptr, stream);
+}
+
+int32_t siren_forward_ex(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, float* y, float* tws,
+                         void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
     if (n == 0) return SIREN_OK;
@@ -245,7 +264,7 @@ int32_t siren_forward(const siren_cfg* cfg, const float* ws, const float* x, int
     if (blocks > 0x7fffffffll) return fail(SIREN_EINVAL, "n too large");
     const dim3 grid((unsigned)blocks);
     if (layered(cfg)) return layered_call(siren::LAY_FWD | siren::LAY_Y, cfg, ws, x, n, nullptr, y, nullptr, nullptr,
-                                          nullptr, stream, "siren_forward");
+                                          nullptr, tws, stream, "siren_forward");
     siren::FusedArgs fa{ws, x, n, nullptr, y, nullptr, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first,
                         cfg->omega_hidden, cfg->outermost_linear ? 0 : 1, nullptr, nullptr, 0};
     if (wide(cfg))
@@ -265,9 +284,10 @@ int32_t siren_forward_grad_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* c
     if (int rc = check_cfg(cfg, true)) return rc;
     if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
     const int64_t n_pad = (n + siren::TILE - 1) / siren::TILE * siren::TILE;
-    *count = wide(cfg)   ? (int64_t)cfg->n_hidden * n_pad * cfg->hidden
-             : deep(cfg) ? (int64_t)(cfg->n_hidden + 1) * n_pad * siren::H  // lane-major cos of layers 0..L
-                         : 0;
+    *count = wide(cfg)      ? (int64_t)cfg->n_hidden * n_pad * cfg->hidden
+             : deep(cfg)    ? (int64_t)(cfg->n_hidden + 1) * n_pad * siren::H  // lane-major cos of layers 0..L
+             : layered(cfg) ? layered_scratch(cfg, n, false)                   // the layered path's chunk scratch
+                            : 0;
     return SIREN_OK;
 }
 
@@ -298,7 +318,7 @@ int32_t siren_forward_grad(const siren_cfg* cfg, const float* ws, const float* x
     }
     if (layered(cfg))
         return layered_call(siren::LAY_FWD | siren::LAY_Y | siren::LAY_GX, cfg, ws, x, n, gy, y, gx, nullptr, nullptr,
-                            stream, "siren_forward_grad");
+                            tws, stream, "siren_forward_grad");
     const int64_t blocks = (n + siren::TILE - 1) / siren::TILE;
     if (blocks > 0x7fffffffll) return fail(SIREN_EINVAL, "n too large");
     const dim3 grid((unsigned)blocks);
@@ -417,7 +437,7 @@ int32_t siren_train_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
     if (layered(cfg)) {
-        *count = 0;
+        *count = layered_scratch(cfg, n, false);  // the layered path's chunk scratch
     } else {
         const TrainPlan plan(cfg, n);
         *count = plan.total + (deep(cfg) ? plan.act_floats : 0);  // deep: + the stored split's lane-major cos
@@ -442,7 +462,7 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
         if (int rc = siren_forward_store(cfg, ws, x, n, nullptr, tws, stream)) return rc;
         return siren_backward_stored(cfg, ws, x, n, gy, tws, gx, gparams, stream);
     }
-    if (layered(cfg)) {  // the chunk scratch lives in ws; tws is not used
+    if (layered(cfg)) {  // tws is the chunk scratch
         if (n == 0) {  // empty tensors may carry NULL data pointers: only gparams is written
             if (gparams == nullptr) return fail(SIREN_EINVAL, "gparams is NULL");
             (void)hipMemsetAsync(gparams, 0, param_count(cfg) * sizeof(float), (hipStream_t)stream);
@@ -451,7 +471,7 @@ int32_t siren_backward(const siren_cfg* cfg, const float* ws, const float* x, in
         if (ws == nullptr || x == nullptr || gy == nullptr || gx == nullptr || gparams == nullptr)
             return fail(SIREN_EINVAL, "ws/x/gy/gx/gparams is NULL");
         return layered_call(siren::LAY_FWD | siren::LAY_GX | siren::LAY_THETA, cfg, ws, x, n, gy, nullptr, gx,
-                            gparams, nullptr, stream, "siren_backward");
+                            gparams, nullptr, tws, stream, "siren_backward");
     }
     if (ws == nullptr || gy == nullptr || tws == nullptr || gx == nullptr || gparams == nullptr ||
         (n > 0 && x == nullptr))
@@ -507,8 +527,8 @@ int32_t siren_train_stored_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* c
         return fail(SIREN_EUNSUPPORTED, "the stored-forward W2 split needs a linear output layer (hidden 256: 1..5 "
                                         "hidden layers)");
     if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
-    if (layered(cfg)) {
-        *count = siren::layered_stored_floats(cfg->hidden, cfg->n_hidden, n);
+    if (layered(cfg)) {  // [a_0..a_L][cos_0..cos_L] n-row buffers, then the chunk scratch
+        *count = siren::layered_stored_floats(cfg->hidden, cfg->n_hidden, n) + layered_scratch(cfg, n, true);
         return SIREN_OK;
     }
     const TrainPlan plan(cfg, n);
@@ -530,7 +550,8 @@ int32_t siren_forward_store(const siren_cfg* cfg, const float* ws, const float* 
         return fail(SIREN_EINVAL, "ws/x/y/tws is NULL");
     if (layered(cfg))
         return layered_call(siren::LAY_FWD | siren::LAY_Y | siren::LAY_TWS, cfg, ws, x, n, nullptr, y, nullptr,
-                            nullptr, tws, stream, "siren_forward_store");
+                            nullptr, tws, tws + siren::layered_stored_floats(cfg->hidden, cfg->n_hidden, n), stream,
+                            "siren_forward_store");
     const TrainPlan plan(cfg, n);
     float* abuf = tws;
     float* cbuf = stored_cos(cfg, plan, tws);
@@ -563,7 +584,8 @@ int32_t siren_backward_stored(const siren_cfg* cfg, const float* ws, const float
         return fail(SIREN_EINVAL, "ws/x/gy/tws/gx/gparams is NULL");
     if (layered(cfg))
         return layered_call(siren::LAY_GX | siren::LAY_THETA | siren::LAY_TWS, cfg, ws, x, n, gy, nullptr, gx, gparams,
-                            tws, stream, "siren_backward_stored");
+                            tws, tws + siren::layered_stored_floats(cfg->hidden, cfg->n_hidden, n), stream,
+                            "siren_backward_stored");
     const TrainPlan plan(cfg, n);
     const hipStream_t st = (hipStream_t)stream;
     const int64_t P = param_count(cfg);
@@ -1308,6 +1330,11 @@ int32_t siren_hvp_backward_batched(const siren_cfg* cfg, const float* ws, const 
 
 int32_t siren_forward_batched(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
                               float* y, void* stream) {
+    return siren_forward_batched_ex(cfg, ws, x, n, batch, y, nullptr, stream);
+}
+
+int32_t siren_forward_batched_ex(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, int64_t batch,
+                                 float* y, float* tws, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (n < 0 || batch < 0 || batch > 65535) return fail(SIREN_EINVAL, "need n >= 0 and 0 <= batch <= 65535");
     if (n == 0 || batch == 0) return SIREN_OK;
@@ -1318,7 +1345,7 @@ int32_t siren_forward_batched(const siren_cfg* cfg, const float* ws, const float
     const int64_t cus = cu_count();
     if (!(grouped_ok(cfg) && cfg->n_hidden <= 5) || blocks >= 4 * cus) {
         for (int64_t b = 0; b < batch; ++b)
-            if (int rc = siren_forward(cfg, ws + b * W, x + b * n * cfg->d_in, n, y + b * n * cfg->d_out, stream))
+            if (int rc = siren_forward_ex(cfg, ws + b * W, x + b * n * cfg->d_in, n, y + b * n * cfg->d_out, tws, stream))
                 return rc;
         return SIREN_OK;
     }
@@ -1365,10 +1392,8 @@ bool grouped_w2(const siren_cfg* cfg, int64_t n) {
 int32_t siren_train_batched_ws_floats(const siren_cfg* cfg, int64_t n, int64_t batch, int64_t* count) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (count == nullptr || n < 0 || batch < 0) return fail(SIREN_EINVAL, "count is NULL or n / batch < 0");
-    const bool grouped = grouped_w2(cfg, n);
-    const TrainPlan plan(cfg, n, grouped ? batch : 1);
-    // element by element: one siren_backward workspace, reused (4..5 hidden layers: + the stored split's cos)
-    *count = grouped ? batch * plan.total : plan.total + (deep(cfg) ? plan.act_floats : 0);
+    if (!grouped_w2(cfg, n)) return siren_train_ws_floats(cfg, n, count);  // element by element: one reused
+    *count = batch * TrainPlan(cfg, n, batch).total;
     return SIREN_OK;
 }
 

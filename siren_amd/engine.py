@@ -122,8 +122,9 @@ class SirenEngine:
         x = self._check_x(x)
         n = x.shape[0]
         y = out if out is not None else torch.empty(n, self.cfg.d_out, dtype=torch.float32, device=x.device)
-        _lib.check(self.lib.siren_forward(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(y), _stream(x.device)),
-                   'siren_forward')
+        tws = self._fwd_workspace(n, x.device)
+        _lib.check(self.lib.siren_forward_ex(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(y), _ptr(tws),
+                                             _stream(x.device)), 'siren_forward_ex')
         return y
 
     def forward_grad(self, ws, x, gy=None, want_y=True, out_y=None, out_gx=None):
@@ -200,6 +201,13 @@ class SirenEngine:
         _lib.check(self.lib.siren_forward_split(ctypes.byref(self.cfg), _ptr(wsx), _ptr(x), n, _ptr(y),
                                                 _stream(x.device)), 'siren_forward_split')
         return y
+
+    def _fwd_workspace(self, n, device):
+        """siren_forward_ex's caller-owned scratch (the layered path's chunk scratch; None elsewhere)."""
+        cnt = ctypes.c_int64()
+        _lib.check(self.lib.siren_forward_ws_floats(ctypes.byref(self.cfg), n, ctypes.byref(cnt)),
+                   'siren_forward_ws_floats')
+        return torch.empty(cnt.value, dtype=torch.float32, device=device) if cnt.value > 0 else None
 
     def _fg_workspace(self, n, device):
         """siren_forward_grad's caller-owned scratch (hidden 512: the cos spill; hidden 256: none)."""
@@ -478,8 +486,9 @@ class SirenEngine:
         x = self._check_xb(x)
         B, n = x.shape[:2]
         y = torch.empty(B, n, self.cfg.d_out, dtype=torch.float32, device=x.device)
-        _lib.check(self.lib.siren_forward_batched(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, B, _ptr(y),
-                                                  _stream(x.device)), 'siren_forward_batched')
+        tws = self._fwd_workspace(n, x.device)
+        _lib.check(self.lib.siren_forward_batched_ex(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, B, _ptr(y), _ptr(tws),
+                                                     _stream(x.device)), 'siren_forward_batched_ex')
         return y
 
     def forward_grad_batched(self, ws, x, gy=None, want_y=True):

@@ -93,6 +93,43 @@ def test_layered_backward_vs_fp64(cuda, n, d, L, o, H):
     assert torch.equal(gp, gp3) and torch.equal(gx, gx3)
 
 
+def test_layered_ws_is_immutable_and_scratch_is_the_callers(cuda):
+    """ABI 5: the packed workspace of a layered network holds the parameters and W_l^T only and no entry point writes
+    it (the chunk scratch is each call's caller-owned tws, NaN-poisoned here), so one ws serves every call."""
+    from siren_amd.engine import SirenEngine
+    n, d, L, o, H = 20000, 3, 3, 3, 1024  # two chunks
+    layers = random_layers(d, L, o, H, seed=11)
+    eng = SirenEngine(d, H, L, o)
+    ws = eng.pack(to_dev(O.flatten(layers), cuda))
+    ws0 = ws.clone()
+    rng = np.random.default_rng(2)
+    x = to_dev(rng.uniform(-1, 1, (n, d)), cuda)
+    gy = to_dev(rng.normal(size=(n, o)) / n, cuda)
+    real_empty = torch.empty
+
+    def poisoned(*a, **k):
+        t = real_empty(*a, **k)
+        if t.is_floating_point() and t.is_cuda:
+            t.fill_(float('nan'))
+        return t
+    torch.empty = poisoned
+    try:
+        y = eng.forward(ws, x)
+        y2, gx = eng.forward_grad(ws, x, gy)
+        gx3, gp = eng.backward_params(ws, x, gy)
+        ys, tws = eng.forward_store(ws, x)
+        gx4, gp4 = eng.backward_stored(ws, x, gy, tws)
+    finally:
+        torch.empty = real_empty
+    torch.cuda.synchronize()
+    assert torch.equal(ws, ws0)
+    for t in (y, y2, gx, gx3, gp, ys, gx4, gp4):
+        assert torch.isfinite(t).all()
+    assert torch.equal(y, y2) and torch.equal(y, ys) and torch.equal(gx, gx3) and torch.equal(gp, gp4)
+    ry = O.forward(x.cpu().numpy(), layers)
+    assert np.max(np.abs(y.cpu().numpy() - ry)) <= tol(ry)
+
+
 def test_layered_n0(cuda):
     from siren_amd.engine import SirenEngine
     eng = SirenEngine(2, 1024, 3, 1)

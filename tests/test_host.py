@@ -52,18 +52,22 @@ def test_param_count_and_workspace(lib):
     bad = _lib.SirenCfg(2, 100, 3, 1, 30., 30., 1, 0)   # not a multiple of 64: no kernel path
     assert lib.siren_workspace_floats(ctypes.byref(bad), ctypes.byref(c)) == _lib.SIREN_EUNSUPPORTED
     assert b'256' in lib.siren_last_error()
-    # hidden 1024 (train_video.py's width): the layered path; ws = the parameters + the chunk scratch
+    # hidden 1024 (train_video.py's width): the layered path; ws = the parameters + W_l^T only (immutable, ABI 5)
     big = _lib.SirenCfg(3, 1024, 3, 3, 30., 30., 1, 0)
     assert lib.siren_param_count(ctypes.byref(big), ctypes.byref(c)) == 0
     P = c.value
     assert lib.siren_workspace_floats(ctypes.byref(big), ctypes.byref(c)) == 0
-    # [params, 256-byte aligned][W_l^T x 3][a_l, cos_l x 4 layers][u x 2] chunks of 16384 x 1024 + column-sum slabs
-    # (4 bias + 3 dWout + 3 dW0 matrices of 256 rows x 1024, dbout 256 x 3)
-    assert c.value == ((P + 63) // 64 * 64 + 3 * 1024 * 1024 + (2 * 4 + 2) * 16384 * 1024 + (4 + 3 + 3) * 256 * 1024
-                       + 256 * 3)
-    # the stored split keeps a_l / cos_l of every layer over all n rows
+    assert c.value == (P + 63) // 64 * 64 + 3 * 1024 * 1024
+    # the caller's chunk scratch: [u x 2] chunks of 16384 x 1024 + column-sum slabs (4 bias + 3 dWout + 3 dW0
+    # matrices of 256 rows x 1024, dbout 256 x 3) + [a_l, cos_l x 4 layers] chunks unless the split stores them
+    slabs = 2 * 16384 * 1024 + (4 + 3 + 3) * 256 * 1024 + 256 * 3
+    for q in ('siren_forward_ws_floats', 'siren_forward_grad_ws_floats', 'siren_train_ws_floats'):
+        assert getattr(lib, q)(ctypes.byref(big), 100000, ctypes.byref(c)) == 0
+        assert c.value == slabs + 2 * 4 * 16384 * 1024, q
+    # the stored split keeps a_l / cos_l of every layer over all n rows, then the chunk scratch without them
+    # (n = 1000 < one chunk: chunk 1024 rows, 16 slab rows)
     assert lib.siren_train_stored_ws_floats(ctypes.byref(big), 1000, ctypes.byref(c)) == 0
-    assert c.value == 2 * 4 * 1000 * 1024
+    assert c.value == 2 * 4 * 1000 * 1024 + 2 * 1024 * 1024 + (4 + 3 + 3) * 16 * 1024 + 16 * 3
     fs = _lib.SirenCfg(3, 1024, 3, 3, 30., 30., 0, 0)   # final sine: not on the layered path
     assert lib.siren_workspace_floats(ctypes.byref(fs), ctypes.byref(c)) == _lib.SIREN_EUNSUPPORTED
     assert lib.siren_second_order_ws_floats(ctypes.byref(big), 10, 1, ctypes.byref(c)) == _lib.SIREN_EUNSUPPORTED
