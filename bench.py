@@ -251,7 +251,7 @@ def pmc_traffic(n):
     return None, 'profiles/pmc_headline.json lacks %s at n=%d' % (HEADLINE_KERNEL, n)
 
 
-def train_step_rate(device, n=1 << 18, steps=5):
+def train_step_rate(device, n=1 << 18, steps=10, warmup=3):
     """W2: image_mse training steps (fused forward, fused backward + MFMA wgrad, Adam) in Mcoords/s."""
     from siren_amd.modules import SingleBVPNet
     torch.manual_seed(0)
@@ -265,7 +265,8 @@ def train_step_rate(device, n=1 << 18, steps=5):
         opt.zero_grad()
         loss.backward()
         opt.step()
-    step()
+    for _ in range(warmup):  # Adam state, allocator pools
+        step()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -284,7 +285,7 @@ def reference_laplace(y, x):
     return div
 
 
-def config_rates(device, steps=5):
+def config_rates(device, steps=10, warmup=3):
     """Secondary per-config rates (BASELINE.json configs[2..4]), one GPU, drop-in API end to end (model ->
     loss_functions -> backward -> Adam), inputs resident on the device. Mcoords/s per GPU."""
     from siren_amd.modules import SingleBVPNet
@@ -302,7 +303,8 @@ def config_rates(device, steps=5):
             opt.zero_grad()
             total.backward()
             opt.step()
-        step()
+        for _ in range(warmup):
+            step()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -334,11 +336,12 @@ def config_rates(device, steps=5):
         fopt.zero_grad()
         total.backward()
         fopt.step()
-    sdf_step(0)
+    for i in range(warmup):
+        sdf_step(i)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
-        sdf_step(1 + i)
+        sdf_step(warmup + i)
     torch.cuda.synchronize()
     res['sdf_5x256_d3_train_device_sampling_fused_adam_mcoords_s'] = round(
         (1 << 19) * steps / (time.perf_counter() - t0) / 1e6, 3)
@@ -369,7 +372,8 @@ def config_rates(device, steps=5):
     flat_b = torch.randn(32, eng_b.param_count, device=device) * 0.01
     xb = torch.rand(32, 4096, 2, device=device) * 2 - 1
     wsb = eng_b.pack_batched(flat_b)
-    eng_b.forward_grad_batched(wsb, xb)
+    for _ in range(warmup):
+        eng_b.forward_grad_batched(wsb, xb)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -384,7 +388,8 @@ def config_rates(device, steps=5):
         ws_step = eng_b.pack_batched(flat_b)
         _, tws = eng_b.forward_store_batched(ws_step, xb)
         eng_b.backward_stored_batched(ws_step, xb, gyb, tws)
-    hyper_w2()
+    for _ in range(warmup):
+        hyper_w2()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -410,7 +415,8 @@ def config_rates(device, steps=5):
     eng = SirenEngine(2, 256, 3, 1)
     ws = eng.pack(seed0_params(device))
     x2 = grid[0].contiguous()
-    eng.forward_laplace(ws, x2, True, True)
+    for _ in range(warmup):
+        eng.forward_laplace(ws, x2, True, True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):

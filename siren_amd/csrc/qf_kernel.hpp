@@ -58,6 +58,8 @@ __device__ __forceinline__ QfKept qf_load(const float* p) {
     return r;
 }
 
+__device__ __forceinline__ void qf_store_block(float* p, const f32x4& v) { store_block(p, 0, v); }
+
 // per-coordinate coefficients of the quadratic form (lane constants): q11 = G_11, q12 = G_12 + G_21, q22 = G_22
 struct QfCoef {
     float q11, q12, q22;
@@ -198,10 +200,10 @@ __global__ __launch_bounds__(THREADS, 1) void qf_rev_kernel(const float* __restr
                 act[1][rb][r] = zb;
             }
 #if QF_PROBE < 3 && !defined(QF_NOSTORE)
-            if constexpr (!SEED) store_block(ap, 0, aa);  // a_L's value / d/dx_1 streams feed no gradient
-            store_block(ap + H * 16, 0, ab);
-            store_block(dp, 0, act[0][rb]);
-            store_block(dp + H * 16, 0, act[1][rb]);
+            if constexpr (!SEED) qf_store_block(ap, aa);  // a_L's value / d/dx_1 streams feed no gradient
+            qf_store_block(ap + H * 16, ab);
+            qf_store_block(dp, act[0][rb]);
+            qf_store_block(dp + H * 16, act[1][rb]);
 #endif
             ap += 256;
             dp += 256;
@@ -225,8 +227,19 @@ __global__ __launch_bounds__(THREADS, 1) void qf_rev_kernel(const float* __restr
         }
     };
 
+#ifdef QF_PROF
+    // probe (numerically meaningless gx): s_memtime after each phase, wave 0 of the first 256 workgroups, into gx as
+    // u64 [block][event]: 0 start, 1 seed epilogue, then per reverse GEMM (end of GEMM, end of epilogue)
+    unsigned long long qst[2 + 2 * 8];
+    int qe = 0;
+    qst[qe++] = __builtin_amdgcn_s_memtime();
+#define QF_STAMP() qst[qe++] = __builtin_amdgcn_s_memtime()
+#else
+#define QF_STAMP()
+#endif
     // seed at layer L from the kept z_L jet (no forward sweep), then the L reverse GEMMs
     epilogue(lh, std::true_type{});
+    QF_STAMP();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // slice s landed (and the seed's stores): publish it
     __builtin_amdgcn_s_barrier();
 #pragma unroll 1
@@ -247,8 +260,17 @@ __global__ __launch_bounds__(THREADS, 1) void qf_rev_kernel(const float* __restr
                 ++s;
             }
         }
+        QF_STAMP();
         epilogue(2 * lh - p - 1, std::false_type{});
+        QF_STAMP();
     }
+#ifdef QF_PROF
+    if (wave == 0 && lane == 0 && blockIdx.x < 256) {
+        unsigned long long* out = (unsigned long long*)gx + blockIdx.x * 16;
+        for (int e = 0; e < qe && e < 16; ++e) out[e] = qst[e];
+    }
+    return;
+#endif
 
     // ---- gx = W0^T zb_0,value (tile 0, lo lanes) ---------------------------------------------------------------
 #pragma unroll
@@ -265,5 +287,6 @@ __global__ __launch_bounds__(THREADS, 1) void qf_rev_kernel(const float* __restr
         }
     }
 }
+
 
 }  // namespace siren

@@ -57,7 +57,8 @@ constexpr int W1_NBUF = 4;  // ring slots of this kernel (64 KiB)
 #define W1_EPI_JET 8  // pair 1 measured neutral on the Poisson step
 #endif
 #ifndef W1_EPI_MEM
-#define W1_EPI_MEM 4  // STORE / FWDS / REV (>= 4: after the mid-slice wait): hypernet step -2.5 %, image_w2 / sdf neutral
+#define W1_EPI_MEM 6  // STORE / FWDS / REV (>= 4: after the mid-slice wait): pair 6 vs 4 -1 .. -1.5 % on the REV / FWDS
+                      // kernels of the image-fit and hypernet steps (profiles/r04e_epilogue_mem.log)
 #endif
 template <int MODE>
 constexpr int w1_epi_pair() {
