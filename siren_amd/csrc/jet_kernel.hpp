@@ -63,13 +63,13 @@ __device__ __forceinline__ void jstore_tile(float* p, const f32x4 (&v)[NB]) {
 struct LaneBlocks {  // lane-major scratch: block rb of this lane at p + rb * 256
     float* p;
     __device__ __forceinline__ f32x4 next_load() {
-        const f32x4 v = *(const f32x4*)p;
+        const f32x4 v = *gmem4(p);
         p += 256;
         asm volatile("" : "+v"(p));
         return v;
     }
     __device__ __forceinline__ void next_store(const f32x4& v) {
-        *(f32x4*)p = v;
+        *gmem4(p) = v;
         p += 256;
         asm volatile("" : "+v"(p));
     }

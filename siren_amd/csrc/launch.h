@@ -71,7 +71,7 @@ void launch_hess(dim3 grid, hipStream_t st, const float* ws, const float* x, int
                  int lh, float w0, float w, float* hm, float* kept);
 // the kept Hessian-node backward on Q8 tile pairs (qf_kernel.hpp; grid = hess_groups(n) / 4, n_pad = hess_groups(n) * 8):
 // abuf / dbuf (L + 1) layers x 4 n_pad columns x 256 floats
-void launch_qf_rev(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* G,
+void launch_qf_rev(int64_t ngroups, hipStream_t st, const float* ws, const float* x, int64_t n, const float* G,
                    const float* u, const float* kept, float* gx, float* gu, int d, int o, int lh, float w0, float w,
                    float* abuf, float* dbuf, int64_t n_pad);
 // its edge layers (EDGE_Q8): rows zb_0 (dbuf layer 0) and the a_L jet (abuf layer L) over n_pad / 8 tile pairs

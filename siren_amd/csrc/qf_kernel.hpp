@@ -288,5 +288,4 @@ __global__ __launch_bounds__(THREADS, 1) void qf_rev_kernel(const float* __restr
     }
 }
 
-
 }  // namespace siren

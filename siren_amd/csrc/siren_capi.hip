@@ -202,7 +202,7 @@ int finish_grads(const siren_cfg* cfg, hipStream_t st, const float* partial, int
     const int64_t rblocks = std::max<int64_t>(1, std::min<int64_t>((off.wout - off.hidden0 + 255) / 256, cap));
     siren::launch_reduce(dim3((unsigned)rblocks, (unsigned)batch), st, partial, S, P, gparams, S2, off.hidden0,
                          off.wout, bpart, off.hidden0, off.wout);
-    const int64_t eblocks = std::max<int64_t>(1, std::min<int64_t>((es.E + 255) / 256, 1024));
+    const int64_t eblocks = std::max<int64_t>(1, (es.E + 15) / 16);  // 16 columns per workgroup
     siren::launch_edge_reduce(dim3((unsigned)eblocks, (unsigned)batch), st, eslab, es.splits, es.E, off.hidden0,
                               off.wout, gparams, P, bpart);
     return hip_status(what);
@@ -907,9 +907,8 @@ int32_t siren_hessian_backward_kept(const siren_cfg* cfg, const float* ws, const
         float* qa = tws;
         float* qd = qa + qp.buf_floats;
         float* qpart = qd + qp.buf_floats;
-        siren::launch_qf_rev(dim3((unsigned)(siren::hess_groups(n) / siren::WAVES)), st, ws, x, n, G, u, kept, gx, gu,
-                             cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, qa, qd,
-                             qp.n_pad);
+        siren::launch_qf_rev(siren::hess_groups(n), st, ws, x, n, G, u, kept, gx, gu, cfg->d_in, cfg->d_out,
+                             cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, qa, qd, qp.n_pad);
         if (int rc = hip_status("siren_hessian_backward (kept quadratic-form jet)")) return rc;
         if (gparams == nullptr) return SIREN_OK;
         siren::launch_wgrad(dim3((unsigned)qp.splits, (unsigned)cfg->n_hidden), st, qa, qd, qp.cols, qp.tps, qpart, P,

@@ -301,14 +301,24 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Global-memory views of generic pointers. A pointer stepped through an opaque register (asm "+v", to keep hipcc from
+// hoisting one 64-bit address per block) loses its address space, and hipcc then emits FLAT loads / stores — which
+// count in lgkmcnt as well as vmcnt, so every counted LDS-operand wait of the next MFMA slice also waited for the
+// epilogue's stores to reach memory (and a counted lgkmcnt with FLAT ops outstanding is not a valid LDS wait).
+typedef __attribute__((address_space(1))) float gfloat;
+typedef __attribute__((address_space(1))) f32x4 gf32x4_t;
+__device__ __forceinline__ gfloat* gmem(float* p) { return (gfloat*)p; }
+__device__ __forceinline__ const gf32x4_t* gmem4(const float* p) { return (const gf32x4_t*)p; }
+__device__ __forceinline__ gf32x4_t* gmem4(float* p) { return (gf32x4_t*)p; }
+
 // STORE-mode writers: element (neuron 16*rb + 4*g + r, coord c) of a 16-coordinate tile lives at
-// neuron*16 + c, so lane (g, c) writes 4 floats 64 B apart per block; p already points at 4*g*16 + c.
+// neuron*16 + c, so lane (g, c) writes 4 floats 64 B apart per block; p already points at 4*g*16 + c (global memory).
 __device__ __forceinline__ void store_block(float* p, int rb, const f32x4& v) {
-    p += 16 * rb * 16;
-    p[0] = v[0];
-    p[16] = v[1];
-    p[32] = v[2];
-    p[48] = v[3];
+    gfloat* q = gmem(p) + 16 * rb * 16;
+    q[0] = v[0];
+    q[16] = v[1];
+    q[32] = v[2];
+    q[48] = v[3];
 }
 // The same block as ONE coalesced global_store_dwordx4 per lane (1 KiB per instruction instead of four scattered
 // dword stores: epilogue store tails are store-ISSUE-bound, MI355X_MICROARCH.md), transposed through a per-wave LDS

@@ -537,20 +537,34 @@ __global__ void reduce_kernel(const float* __restrict__ partial, int64_t S, int6
 
 // The edge layers' gradient: sum of the SE compact edge slabs (edge_kernel) into the parameter order: compact index
 // c < hidden0 is W0 / b0 (parameter c), the rest Wout / bout (parameter wout + c - hidden0). grid.y = batch element.
-__global__ void edge_reduce_kernel(const float* __restrict__ eslab, int64_t SE, int64_t E, int64_t hidden0,
-                                   int64_t wout, float* __restrict__ gp, int64_t P, int64_t bstride_e) {
+// The slabs are few columns (E ~ 1 K) deep (SE ~ 512): 16 columns per workgroup with 16 threads each over interleaved
+// slabs (8 loads in flight per thread), combined through LDS in a fixed order — one thread per column walking all
+// slabs was a latency-bound 30 us per step (profiles/r04g_paths_summary.log).
+__global__ __launch_bounds__(256) void edge_reduce_kernel(const float* __restrict__ eslab, int64_t SE, int64_t E,
+                                                          int64_t hidden0, int64_t wout, float* __restrict__ gp,
+                                                          int64_t P, int64_t bstride_e) {
+    __shared__ float red[16][17];
     eslab += (int64_t)blockIdx.y * bstride_e;
     gp += (int64_t)blockIdx.y * P;
-    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < E; c += (int64_t)gridDim.x * blockDim.x) {
-        float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int cl = threadIdx.x & 15, k = threadIdx.x >> 4;
+    const int64_t c = (int64_t)blockIdx.x * 16 + cl;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (c < E) {
         const float* col = eslab + c;
-        int64_t s = 0;
-        for (; s + 8 <= SE; s += 8) {
+        int64_t s = k;
+        for (; s + 7 * 16 < SE; s += 8 * 16) {
 #pragma unroll
-            for (int q = 0; q < 8; ++q) a[q] += col[(s + q) * E];
+            for (int q = 0; q < 8; ++q) a[q] += col[(s + 16 * q) * E];
         }
-        for (; s < SE; ++s) a[0] += col[s * E];
-        gp[c < hidden0 ? c : wout + (c - hidden0)] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+        for (; s < SE; s += 16) a[0] += col[s * E];
+    }
+    red[k][cl] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    __syncthreads();
+    if (k == 0 && c < E) {
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) t += red[j][cl];
+        gp[c < hidden0 ? c : wout + (c - hidden0)] = t;
     }
 }
 

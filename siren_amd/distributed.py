@@ -53,15 +53,18 @@ def broadcast_parameters(module, src=0):
             off += p.numel()
 
 
-def allreduce_gradients(params, world=None, count=None):
+def allreduce_gradients(params, world=None, count=None, loss=None):
     """Reduce .grad of `params` over ranks with ONE all-reduce of a flat bucket (in place).
 
     count=None: plain average (equal shards). count = this rank's coordinate count: the bucket carries count * grad
     plus the count itself, so the result is sum_r n_r g_r / sum_r n_r — the full-batch gradient of a mean-over-
     coordinates loss for any split, including empty shards (count 0 contributes nothing; its NaN mean-loss gradient
-    must not have been back-propagated, see training.train)."""
+    must not have been back-propagated, see training.train).
+    loss = this rank's (mean) loss: it rides in the same bucket with the same weighting and the global loss is
+    returned (a detached scalar; an empty shard's NaN loss counts as 0) — what an LBFGS closure must return so every
+    rank's line search sees the same function. Without a process group the local loss (or None) is returned."""
     if not (dist.is_available() and dist.is_initialized()):
-        return
+        return loss
     world = world or dist.get_world_size()
     if count is not None:
         # every rank sends the full bucket of TRAINABLE parameters (so every rank must train the same set, for the
@@ -73,19 +76,27 @@ def allreduce_gradients(params, world=None, count=None):
                 p.grad = torch.zeros_like(p)
     else:
         params = [p for p in params if p.grad is not None]
-    if not params:
-        return
-    flat = torch.cat([p.grad.reshape(-1) for p in params] +
-                     ([p.grad.new_full((1,), float(count))] if count is not None else []))
+    if not params and loss is None:
+        return None
+    dev = params[0].grad if params else torch.as_tensor(loss)
+    extra = []
+    if loss is not None:
+        lv = torch.as_tensor(loss).detach().reshape(1).to(dev.device, torch.float32)
+        extra.append(torch.zeros_like(lv) if count == 0 else lv)
     if count is not None:
-        flat[:-1].mul_(float(count))
+        extra.append(dev.new_full((1,), float(count)))
+    flat = torch.cat([p.grad.reshape(-1) for p in params] + extra)
+    body = flat[:flat.numel() - (1 if count is not None else 0)]  # gradients (+ loss): the count-weighted part
+    if count is not None:
+        body.mul_(float(count))
     dist.all_reduce(flat, op=dist.ReduceOp.SUM)
     if count is not None:
-        flat = flat[:-1].div_(flat[-1:].clamp_min(1.))
+        body.div_(flat[-1:].clamp_min(1.))
     else:
-        flat.div_(world)
+        body.div_(world)
     off = 0
     for p in params:
         n = p.numel()
         p.grad.copy_(flat[off:off + n].view_as(p.grad))
         off += n
+    return flat[off].clone() if loss is not None else None

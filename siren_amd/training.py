@@ -85,8 +85,11 @@ def train(model, train_dataloader, epochs, lr, steps_til_summary, epochs_til_che
                     count = _coord_count(model_input) if world > 1 else None
                     if count != 0:
                         loss.backward()
-                    distributed.allreduce_gradients(list(model.parameters()), world, count)
-                    return loss
+                    if world == 1:
+                        return loss
+                    # the line search must see the GLOBAL loss on every rank (the gradient already is global), or
+                    # the ranks' strong-Wolfe searches take different steps and the replicas drift apart
+                    return distributed.allreduce_gradients(list(model.parameters()), world, count, loss=loss)
                 optim.step(closure)
             model_output, train_loss = step_losses(model_input, gt, total_steps)
             train_losses.append(train_loss.detach())  # device scalar: no per-step host sync (training.py:86)

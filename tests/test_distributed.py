@@ -146,3 +146,37 @@ def test_shard_covers_range():
             sizes = [b - a for a, b in parts]
             if n >= 64 * world:
                 assert max(sizes) - min(sizes) < 64 + n % 64 + 64
+
+
+def _loss_worker(rank, world, port, ret):
+    _env(rank, world, port)
+    from siren_amd import distributed as sd
+    sd.init('gloo')
+    torch.manual_seed(0)
+    p = torch.nn.Parameter(torch.randn(5))
+    x, t = _batch(100)
+    a, b = sd.shard(100, world, rank, align=64)  # (64, 36): unequal shares
+    loss = ((x[0, a:b, 0] * p.sum() - t[0, a:b, 0]) ** 2).mean()
+    loss.backward()
+    g = sd.allreduce_gradients([p], world, b - a, loss=loss)
+    ret['l%d' % rank] = float(g)
+    ret['g%d' % rank] = p.grad.clone()
+    torch.distributed.destroy_process_group()
+
+
+def test_dp_closure_loss_is_global():
+    """The LBFGS closure under DP (training.train, use_lbfgs) returns the count-weighted GLOBAL loss from the same
+    all-reduce as the gradient, so every rank's strong-Wolfe line search sees the same function:
+    with unequal shards both ranks get the full-batch loss and gradient."""
+    world, port = 2, _free_port()
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_loss_worker, args=(world, port, ret), nprocs=world, join=True)
+    torch.manual_seed(0)
+    p = torch.nn.Parameter(torch.randn(5))
+    x, t = _batch(100)
+    loss = ((x[0, :, 0] * p.sum() - t[0, :, 0]) ** 2).mean()
+    loss.backward()
+    lf = float(loss.detach())
+    assert ret['l0'] == ret['l1'] and abs(ret['l0'] - lf) <= 1e-6 * lf
+    assert torch.equal(ret['g0'], ret['g1']) and torch.allclose(ret['g0'], p.grad, rtol=1e-5, atol=0)

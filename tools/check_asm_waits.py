@@ -335,6 +335,20 @@ def check_store_data(body, name, wait_states=2):
     return problems
 
 
+def check_flat(body, name):
+    """FLAT memory instructions (flat_load / flat_store / flat_atomic): hipcc emits them for a generic pointer whose
+    address space it cannot prove (one stepped through an opaque asm register). A FLAT op counts in lgkmcnt as well
+    as vmcnt and may retire out of order with the LDS reads there, so every counted `s_waitcnt lgkmcnt(N)` of the
+    MFMA operand prefetch behind it is both slow (it waits for the store to reach memory) and not a valid wait for
+    the LDS read it guards. Every kernel here addresses global memory through global_ ops (siren_common.h gmem)."""
+    problems = []
+    for no, line in enumerate(body):
+        t = line.split(';')[0].strip()
+        if t.startswith('flat_'):
+            problems.append((no, t, None))
+    return problems
+
+
 def main():
     path = sys.argv[1]
     want = sys.argv[2] if len(sys.argv) > 2 else ''
@@ -347,7 +361,7 @@ def main():
         i = s.find('\n' + nm + ':')
         j = s.find('.Lfunc_end', i)
         body = s[i:j].split('\n')
-        probs = check(body, nm) + check_vmem(body, nm) + check_store_data(body, nm)
+        probs = check(body, nm) + check_vmem(body, nm) + check_store_data(body, nm) + check_flat(body, nm)
         print('%-70s %d reads of in-flight load registers' % (nm[:70], len(probs)))
         for no, t, ln in probs[:8]:
             print('    line %d: %s   (load at line %d: %s)' % (no, t, ln, body[ln].strip()))
