@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SIREN_ABI_VERSION 5
+#define SIREN_ABI_VERSION 6
 
 enum {
     SIREN_OK = 0,
@@ -225,6 +225,11 @@ int32_t siren_hessian_backward(const siren_cfg* cfg, const float* ws, const floa
 int32_t siren_hessian_ws_floats(const siren_cfg* cfg, int64_t n, int32_t keep, int64_t* count);
 int32_t siren_hessian(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* u, float* kept,
                       float* hm, void* stream);
+/* siren_hessian that also returns, from the same sweep (its value and first-order streams), y (n, d_out) = Phi(x)
+ * and gx (n, d_in) = sum_j u_j dPhi_j/dx — what siren_forward_grad gives — each nullable (ABI 6). A training step of
+ * the reference's laplace_mse recipe (model(x), gradient(), divergence()) then needs one forward sweep, not two. */
+int32_t siren_hessian_ex(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* u, float* kept,
+                         float* hm, float* y, float* gx, void* stream);
 /* siren_hessian_backward reading its forward jets from a siren_hessian kept buffer of the same (ws, x, n) (kept
  * NULL: recompute, = siren_hessian_backward). */
 int32_t siren_hessian_backward_kept(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* G,

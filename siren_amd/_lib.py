@@ -11,7 +11,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('SIREN_AMD_LIB', os.path.join(_HERE, 'libsiren_amd.so'))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # Error codes (include/siren_amd.h)
 SIREN_OK, SIREN_EINVAL, SIREN_EUNSUPPORTED, SIREN_EHIP = 0, 1, 2, 3
@@ -86,6 +86,7 @@ _SIGS = {
     'siren_hessian_backward': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P],
     'siren_hessian_ws_floats': [_CFG, _I64, ctypes.c_int32, ctypes.POINTER(_I64)],
     'siren_hessian': [_CFG, _P, _P, _I64, _P, _P, _P, _P],
+    'siren_hessian_ex': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P, _P],
     'siren_hessian_backward_kept': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
     'siren_pack_batched_ex': [_CFG, _P, _I64, _P, ctypes.c_int32, _P],
     'siren_second_order_batched_ws_floats': [_CFG, _I64, _I64, ctypes.c_int32, ctypes.POINTER(_I64)],

@@ -49,15 +49,23 @@ def _will_execute(ctx, i):
 
 
 class JetState:
-    """Per-module switch for jet mode ('auto' turns it on after the first create_graph x-gradient request)."""
+    """Per-module switch for jet mode ('auto' turns it on after the first create_graph x-gradient request). hessian:
+    a Hessian node was built from this module's jet node (divergence() / hessian() of its gradient: the reference's
+    laplace_mse recipe); from then on the jet forward is the Hessian node's own sweep (siren_hessian_ex: y, dPhi/dx,
+    the Hessian and its kept jets at once) and the node reuses it instead of running a second forward."""
 
     def __init__(self, mode='auto'):
         self.mode = mode
         self.active = mode is True
+        self.hessian = False
 
     def observe_x_gradient_request(self):
         if self.mode == 'auto':
             self.active = True
+
+    def observe_hessian_request(self):
+        if self.mode in ('auto', True):
+            self.hessian = True
 
 
 class SirenFunction(torch.autograd.Function):
@@ -114,10 +122,19 @@ class SirenJetFunction(torch.autograd.Function):
     for the gradient terms)."""
 
     @staticmethod
-    def forward(ctx, engine, x, flat, store=False, split=False):
+    def forward(ctx, engine, x, flat, store=False, split=False, jet=None):
         ws = engine.pack(flat)
         ctx.tws = None
-        if split and engine.split_supported:
+        ctx.jet, ctx.pre_hessian = jet, None
+        pre = None
+        if jet is not None and jet.hessian and not split and engine.hessian_backward_supported:
+            pre = SirenHessian.forward_sweep(engine, ws, x, None, want_yg=True)
+        if pre is not None:
+            # the Hessian node of this module's gradient will be requested again (it was last step): run its sweep
+            # now — y and dPhi/dx come from the same jet — and hand (Hm, kept) to that node (_hessian_product)
+            hm, kept, y, J = pre
+            ctx.pre_hessian = (hm, kept)
+        elif split and engine.split_supported:
             # precision 'bf16x6': the split-bf16 W1 kernel (fp32-level error); a backward recomputes from the fp32 ws
             y, J = engine.forward_grad_split(engine.pack_split(flat), x)
         elif store and engine.stored_supported and engine.cfg.hidden == 256 and STORED_FORWARD:
@@ -138,7 +155,7 @@ class SirenJetFunction(torch.autograd.Function):
         need_x = ctx.needs_input_grad[1] and _will_execute(ctx, 0)
         need_p = ctx.needs_input_grad[2] and _will_execute(ctx, 1)
         if (gy is None and gJ is None) or not (need_x or need_p):
-            return None, None, None, None, None
+            return None, None, None, None, None, None
         gy = gy.contiguous() if gy is not None else None
         gJ = gJ.contiguous() if gJ is not None else None
         gx = gp = None
@@ -159,7 +176,7 @@ class SirenJetFunction(torch.autograd.Function):
                     gx = gx + gy * J
                     if need_p:
                         gp = gp + engine.backward_params(ws, x, gy)[1]
-            return None, (gx if need_x else None), (gp if need_p else None), None, None
+            return None, (gx if need_x else None), (gp if need_p else None), None, None, None
         # create_graph=True: differentiable in (x, theta, gy, gJ); J here is this node's own output 1
         if need_x:
             gx = gy * J if gy is not None else None
@@ -178,7 +195,7 @@ class SirenJetFunction(torch.autograd.Function):
             if gJ is not None:
                 _, gpj = _torch_path.jacobian_vjp(engine.cfg, x, flat, gJ, create_graph=True)
                 gp = gpj if gp is None else gp + gpj
-        return None, gx, gp, None, None
+        return None, gx, gp, None, None, None
 
 
 class SirenHVP(torch.autograd.Function):
@@ -237,17 +254,22 @@ class SirenHessian(torch.autograd.Function):
         return min(SirenHessian.KEEP_MAX_BYTES, int(free * SirenHessian.KEEP_FREE_FRACTION))
 
     @staticmethod
-    def forward(ctx, engine, ws, x, flat, u=None):
+    def forward_sweep(engine, ws, x, u, want_yg=False):
+        """The node's forward kernel: (hm, kept | None) — or (hm, kept | None, y, g) with want_yg — keeping the jets
+        when they fit the budget (else the backward recomputes its forward jet)."""
         per_point = 4 * (engine.cfg.n_hidden + 1) * 6 * 256
-        keep = x.shape[0] * per_point <= SirenHessian._keep_budget(x)
-        hm, ctx.kept = None, None
-        if keep:
+        if x.shape[0] * per_point <= SirenHessian._keep_budget(x):
             try:
-                hm, ctx.kept = engine.hessian(ws, x, u, keep=True)
-            except torch.cuda.OutOfMemoryError:  # the backward then recomputes the forward jet
-                hm, ctx.kept = None, None
-        if hm is None:
-            hm = engine.hessian(ws, x, u)
+                return engine.hessian(ws, x, u, keep=True, want_yg=want_yg)
+            except torch.cuda.OutOfMemoryError:
+                pass
+        res = engine.hessian(ws, x, u, want_yg=want_yg)
+        return res if want_yg else (res, None)
+
+    @staticmethod
+    def forward(ctx, engine, ws, x, flat, u=None, pre=None):
+        # pre: (hm, kept) of this very (ws, x), run by the jet node's forward (JetState.hessian)
+        hm, ctx.kept = pre if pre is not None else SirenHessian.forward_sweep(engine, ws, x, u)
         ctx.engine, ctx.ws = engine, ws
         ctx.save_for_backward(x, flat, u)
         return hm
@@ -261,15 +283,15 @@ class SirenHessian(torch.autograd.Function):
         need_p = ctx.needs_input_grad[3] and _will_execute(ctx, 2)
         need_u = u is not None and ctx.needs_input_grad[4] and _will_execute(ctx, 3)
         if not (need_x or need_p or need_u):
-            return None, None, None, None, None
+            return None, None, None, None, None, None
         if not torch.is_grad_enabled():
             gx, gp, gu = eng.hessian_backward(ctx.ws, x, G.contiguous(), u, want_theta=need_p, want_u=need_u,
                                               kept=ctx.kept)
             ctx.kept = None
-            return None, None, (gx if need_x else None), gp, gu
+            return None, None, (gx if need_x else None), gp, gu, None
         ctx.kept = None  # the differentiable recompute below does not read the kept jets
         rx, rp, ru = _torch_path.hessian_vjp(eng.cfg, x, flat, G, create_graph=True, u=u)
-        return None, None, rx, rp, ru
+        return None, None, rx, rp, ru, None
 
 
 def _hessian_product(ctx, engine, ws, x, flat, v, u=None):
@@ -279,8 +301,13 @@ def _hessian_product(ctx, engine, ws, x, flat, v, u=None):
         return None
     hm = getattr(ctx, 'hessian_node', None)
     if hm is None:
-        hm = SirenHessian.apply(engine, ws, x, flat, u)
+        pre = getattr(ctx, 'pre_hessian', None) if u is None else None
+        hm = SirenHessian.apply(engine, ws, x, flat, u, pre)
         ctx.hessian_node = hm
+        ctx.pre_hessian = None
+        jet = getattr(ctx, 'jet', None)
+        if u is None and jet is not None:
+            jet.observe_hessian_request()
     # elementwise (n, d, d) products: a batched GEMM of n 2x2 matrices runs ~100x slower on the BLAS path
     return (hm * v.unsqueeze(-2)).sum(-1)
 

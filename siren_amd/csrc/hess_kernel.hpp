@@ -66,7 +66,8 @@ template <bool KEEP>
 __global__ __launch_bounds__(THREADS, 1) void hess_kernel(const float* __restrict__ ws, const float* __restrict__ x,
                                                           int64_t n, const float* __restrict__ u, int d, int o,
                                                           int lh, float w0, float w, float* __restrict__ hm,
-                                                          float* __restrict__ kept) {
+                                                          float* __restrict__ kept, float* __restrict__ yo,
+                                                          float* __restrict__ gxo) {
     __shared__ __attribute__((aligned(16))) float lds[NBUF * SLICE + SMALL_MAX];
     float* ring = lds;
     float* sm = lds + NBUF * SLICE;
@@ -145,10 +146,13 @@ __global__ __launch_bounds__(THREADS, 1) void hess_kernel(const float* __restric
     }
 
     // ---- Hm = Wout-weighted last jet: seed sum_j u_j Wout_j (u == NULL: sum_j Wout_j) ---------------------------
+    // (yo / gxo nullable: y_j = Wout_j . a_L + bout_j and the seed-weighted gradient sum_j u_j dPhi_j/dx from the
+    // same last jet — the value / first-order streams — so a caller that needs (y, dPhi/dx, Hm) runs ONE sweep)
     float uw[MAXO];
 #pragma unroll
     for (int j = 0; j < MAXO; ++j) uw[j] = (u != nullptr && j < o && valid) ? u[coord * o + j] : 0.f;
-    float p1 = 0.f, p2 = 0.f;
+    float p0 = 0.f, p1 = 0.f, p2 = 0.f;
+    float yv[MAXO] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int rb = 0; rb < NB; ++rb) {
         f32x4 sd;
@@ -161,10 +165,35 @@ __global__ __launch_bounds__(THREADS, 1) void hess_kernel(const float* __restric
         }
         p1 += sd[0] * act[1][rb][0] + sd[1] * act[1][rb][1] + sd[2] * act[1][rb][2] + sd[3] * act[1][rb][3];
         p2 += sd[0] * act[2][rb][0] + sd[1] * act[2][rb][1] + sd[2] * act[2][rb][2] + sd[3] * act[2][rb][3];
+        if (gxo != nullptr)
+            p0 += sd[0] * act[0][rb][0] + sd[1] * act[0][rb][1] + sd[2] * act[0][rb][2] + sd[3] * act[0][rb][3];
+        if (yo != nullptr) {
+#pragma unroll
+            for (int j = 0; j < MAXO; ++j) {  // WoT rows j >= o are zero padded
+                const f32x4 wj = *(const f32x4*)(sm + SM_WO + j * H + 16 * rb + 4 * g);
+                yv[j] += wj[0] * act[0][rb][0] + wj[1] * act[0][rb][1] + wj[2] * act[0][rb][2] + wj[3] * act[0][rb][3];
+            }
+        }
     }
-    p1 = sum_groups(p1);  // lo: (u . dy/dx_2, unused) | hi: H_11
+    p1 = sum_groups(p1);  // lo: u . dy/dx_2 | hi: H_11
     p2 = sum_groups(p2);  // lo: H_12 | hi: H_22
+    if (gxo != nullptr) p0 = sum_groups(p0);  // lo: (u . (y - bout), unused) | hi: u . dy/dx_1
+    if (yo != nullptr) {
+#pragma unroll
+        for (int j = 0; j < MAXO; ++j) yv[j] = sum_groups(yv[j]);  // lo: Wout_j . a_L
+    }
     if (valid && g == 0) {
+        if (gxo != nullptr) {
+            if (hi)
+                gxo[coord * d] = p0;
+            else if (d > 1)
+                gxo[coord * d + 1] = p1;
+        }
+        if (yo != nullptr && !hi) {
+#pragma unroll
+            for (int j = 0; j < MAXO; ++j)
+                if (j < o) yo[coord * o + j] = yv[j] + sm[SM_BOUT + j];
+        }
         if (d == 1) {
             if (hi) hm[coord] = p1;
         } else if (hi) {

@@ -66,9 +66,10 @@ void launch_jet_quad(dim3 grid, hipStream_t st, const float* ws, const float* x,
                      const float* u, float* gx, float* gu, int d, int o, int lh, float w0, float w, float* spill,
                      float* abuf, float* dbuf, int64_t n_pad);
 // tu_hess.hip: the Hessian node's forward, Hm (n, d, d) = sum_j u_j H_j (d <= 2) in one 6-stream forward jet sweep
-// (grid = hess_groups(n) / 4 workgroups); kept (nullable) receives the per-layer jets for launch_jet_quad
+// (grid = hess_groups(n) / 4 workgroups); kept (nullable) receives the per-layer jets for launch_qf_rev; y (n, o) /
+// gx (n, d) nullable: the value and the seed-weighted gradient from the same sweep
 void launch_hess(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* u, int d, int o,
-                 int lh, float w0, float w, float* hm, float* kept);
+                 int lh, float w0, float w, float* hm, float* kept, float* y, float* gx);
 // the kept Hessian-node backward on Q8 tile pairs (qf_kernel.hpp; grid = hess_groups(n) / 4, n_pad = hess_groups(n) * 8):
 // abuf / dbuf (L + 1) layers x 4 n_pad columns x 256 floats
 void launch_qf_rev(int64_t ngroups, hipStream_t st, const float* ws, const float* x, int64_t n, const float* G,

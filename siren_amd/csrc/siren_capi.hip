@@ -870,13 +870,18 @@ int32_t siren_hessian_ws_floats(const siren_cfg* cfg, int64_t n, int32_t keep, i
 
 int32_t siren_hessian(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* u, float* kept,
                       float* hm, void* stream) {
+    return siren_hessian_ex(cfg, ws, x, n, u, kept, hm, nullptr, nullptr, stream);
+}
+
+int32_t siren_hessian_ex(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* u, float* kept,
+                         float* hm, float* y, float* gx, void* stream) {
     if (int rc = check_quad(cfg)) return rc;
     if (n < 0) return fail(SIREN_EINVAL, "n < 0");
     if (n == 0) return SIREN_OK;
     if (ws == nullptr || x == nullptr || hm == nullptr) return fail(SIREN_EINVAL, "ws/x/hm is NULL");
     if (n > (int64_t)0x7fffffff * 8) return fail(SIREN_EINVAL, "n exceeds the grid");
     siren::launch_hess(dim3((unsigned)(siren::hess_groups(n) / siren::WAVES)), (hipStream_t)stream, ws, x, n, u,
-                       cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, hm, kept);
+                       cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, hm, kept, y, gx);
     return hip_status("siren_hessian");
 }
 

@@ -6,11 +6,13 @@
 namespace siren {
 
 void launch_hess(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* u, int d, int o,
-                 int lh, float w0, float w, float* hm, float* kept) {
+                 int lh, float w0, float w, float* hm, float* kept, float* y, float* gx) {
     if (kept != nullptr)
-        hipLaunchKernelGGL(hess_kernel<true>, grid, dim3(THREADS), 0, st, ws, x, n, u, d, o, lh, w0, w, hm, kept);
+        hipLaunchKernelGGL(hess_kernel<true>, grid, dim3(THREADS), 0, st, ws, x, n, u, d, o, lh, w0, w, hm, kept, y,
+                           gx);
     else
-        hipLaunchKernelGGL(hess_kernel<false>, grid, dim3(THREADS), 0, st, ws, x, n, u, d, o, lh, w0, w, hm, kept);
+        hipLaunchKernelGGL(hess_kernel<false>, grid, dim3(THREADS), 0, st, ws, x, n, u, d, o, lh, w0, w, hm, kept, y,
+                           gx);
 }
 
 void launch_qf_rev(int64_t ngroups, hipStream_t st, const float* ws, const float* x, int64_t n, const float* G,

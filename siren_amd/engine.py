@@ -251,10 +251,12 @@ class SirenEngine:
         return (self.supported and c.hidden == 256 and 1 <= c.n_hidden <= 5 and c.d_in <= 2
                 and bool(c.outermost_linear))
 
-    def hessian(self, ws, x, u=None, keep=False):
+    def hessian(self, ws, x, u=None, keep=False, want_yg=False):
         """Hm (n, d_in, d_in) = sum_j u_j H_j(x) (u (n, d_out), None = ones) in one forward-mode second-order jet
         sweep (siren_hessian). keep=True also returns the per-layer jets (n-proportional fp32 buffer) that
-        hessian_backward(..., kept=) reads instead of recomputing its forward: (hm, kept)."""
+        hessian_backward(..., kept=) reads instead of recomputing its forward: (hm, kept). want_yg=True returns
+        (hm, kept, y, g) with y = Phi(x) (n, d_out) and g = sum_j u_j dPhi_j/dx (n, d_in) from the same sweep
+        (siren_hessian_ex; kept None unless keep)."""
         self._require()
         if not self.hessian_backward_supported:
             raise _lib.SirenUnsupported('siren_hessian covers hidden 256, 1..5 hidden layers, in_features <= 2, '
@@ -271,6 +273,12 @@ class SirenEngine:
             _lib.check(self.lib.siren_hessian_ws_floats(ctypes.byref(self.cfg), n, 1, ctypes.byref(cnt)),
                        'siren_hessian_ws_floats')
             kept = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
+        if want_yg:
+            y = torch.empty(n, o, dtype=torch.float32, device=x.device)
+            g = torch.empty(n, d, dtype=torch.float32, device=x.device)
+            _lib.check(self.lib.siren_hessian_ex(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(u), _ptr(kept),
+                                                 _ptr(hm), _ptr(y), _ptr(g), _stream(x.device)), 'siren_hessian_ex')
+            return hm, kept, y, g
         _lib.check(self.lib.siren_hessian(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(u), _ptr(kept), _ptr(hm),
                                           _stream(x.device)), 'siren_hessian')
         return (hm, kept) if keep else hm

@@ -186,7 +186,7 @@ def _fused_apply(engine, jet, coords, weights_biases, precision='fp32'):
     if (jet is not None and jet.active and engine.cfg.d_out == 1 and engine.grad_supported
             and torch.is_grad_enabled() and x2d.requires_grad):
         y, _ = SirenJetFunction.apply(engine, x2d, flat, flat.requires_grad,
-                                      precision == 'bf16x6')  # J: the node's second output
+                                      precision == 'bf16x6', jet)  # J: the node's second output
     elif (precision == 'bf16x6' and engine.split_supported
           and not (torch.is_grad_enabled() and (x2d.requires_grad or flat.requires_grad))):
         # no graph is recorded (dense evaluation: create_mesh, summaries under no_grad): the split-bf16 forward

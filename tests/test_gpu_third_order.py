@@ -337,3 +337,80 @@ def test_reference_recipe_runs_one_hessian_backward(cuda, monkeypatch):
         loss = torch.mean(reference_laplace(out['model_out'], out['model_in']) ** 2)
         loss.backward()
         assert calls == {'hess': step + 1, 'hvp': 0}
+
+
+def test_reference_recipe_one_forward_sweep(cuda, g1, monkeypatch):
+    """From the third step on (a Hessian node was built from the jet node: JetState.hessian) the jet forward IS the
+    Hessian node's sweep (siren_hessian_ex: y, dPhi/dx, Hm, kept): no W1 forward, no second Hessian forward, one kept
+    backward — and the step still matches the reference's fp64 laplace_mse theta-grads (G1) and its Laplacian."""
+    from siren_amd.engine import SirenEngine
+    from siren_amd.modules import SingleBVPNet
+    _forbid_torch_path(monkeypatch)
+    calls = {'w1': 0, 'hess': 0, 'hess_yg': 0, 'bwd_kept': 0}
+    orig_fg, orig_fgs, orig_h, orig_b = (SirenEngine.forward_grad, SirenEngine.forward_grad_store,
+                                         SirenEngine.hessian, SirenEngine.hessian_backward)
+
+    def fg(self, *a, **k):
+        calls['w1'] += 1
+        return orig_fg(self, *a, **k)
+
+    def fgs(self, *a, **k):
+        calls['w1'] += 1
+        return orig_fgs(self, *a, **k)
+
+    def hess(self, *a, **k):
+        calls['hess_yg' if k.get('want_yg') else 'hess'] += 1
+        return orig_h(self, *a, **k)
+
+    def bwd(self, *a, **k):
+        calls['bwd_kept'] += k.get('kept') is not None
+        return orig_b(self, *a, **k)
+    monkeypatch.setattr(SirenEngine, 'forward_grad', fg)
+    monkeypatch.setattr(SirenEngine, 'forward_grad_store', fgs)
+    monkeypatch.setattr(SirenEngine, 'hessian', hess)
+    monkeypatch.setattr(SirenEngine, 'hessian_backward', bwd)
+    m = SingleBVPNet(verbose=False).to(cuda)
+    m.load_state_dict({k[2:]: torch.tensor(v) for k, v in g1.items() if k.startswith('w_')})
+    gt = to_dev(g1['gt_laplace'], cuda)
+    for step in range(3):
+        for k in calls:
+            calls[k] = 0
+        m.zero_grad()
+        out = m({'coords': to_dev(g1['coords'], cuda)})
+        lap = reference_laplace(out['model_out'], out['model_in'])
+        torch.mean((lap - gt) ** 2).backward()
+        if step == 2:
+            assert calls == {'w1': 0, 'hess': 0, 'hess_yg': 1, 'bwd_kept': 1}, calls
+            rl = g1['G1_laplace_f64']
+            assert np.max(np.abs(lap.detach().cpu().numpy() - rl)) <= tol_rel(rl)
+            for k, p in m.named_parameters():
+                ref = g1['G1_laplace_mse_grad_' + k]
+                assert np.max(np.abs(p.grad.cpu().numpy() - ref)) <= 1e-4 * np.max(np.abs(ref)) + 1e-12, k
+            y = out['model_out'].detach().cpu().numpy()
+            assert np.max(np.abs(y - g1['G1_model_out_f64'])) <= 1e-4
+
+
+@pytest.mark.parametrize('n,d,L,o,weighted', [(1, 2, 3, 1, False), (1000, 2, 3, 1, False), (333, 1, 2, 3, True),
+                                               (4097, 2, 5, 2, True), (70, 2, 4, 4, True)])
+def test_hessian_ex_value_and_gradient(cuda, n, d, L, o, weighted):
+    """siren_hessian_ex: y and the seed-weighted gradient from the Hessian sweep against the W1 kernel
+    (siren_forward_grad with gy = u) and fp64 autograd; Hm and the kept jets bitwise those of siren_hessian."""
+    from siren_amd.engine import SirenEngine
+    layers = random_layers(d, L, o, seed=n + 13 * L)
+    eng = SirenEngine(d, 256, L, o)
+    ws = eng.pack(to_dev(O.flatten(layers), cuda))
+    rng = np.random.default_rng(n)
+    x = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    u = rng.normal(size=(n, o)).astype(np.float32) if weighted else None
+    xd, ud = to_dev(x, cuda), (to_dev(u, cuda) if weighted else None)
+    hm, kept, y, g = eng.hessian(ws, xd, ud, keep=True, want_yg=True)
+    hm0, kept0 = eng.hessian(ws, xd, ud, keep=True)
+    assert torch.equal(hm, hm0) and torch.equal(kept, kept0)
+    xt = torch.tensor(x, dtype=torch.float64, requires_grad=True)
+    params = [torch.tensor(t, dtype=torch.float64) for W, b in layers for t in (W, b)]
+    yt = O.torch_forward(xt, params)
+    gt = torch.autograd.grad(yt, xt, torch.ones_like(yt) if u is None else torch.tensor(u, dtype=torch.float64))[0]
+    assert np.max(np.abs(y.cpu().numpy() - yt.detach().numpy())) <= 1e-4
+    assert np.max(np.abs(g.cpu().numpy() - gt.numpy())) <= tol_rel(gt.numpy())
+    y1, g1_ = eng.forward_grad(ws, xd, ud if weighted else None)
+    assert torch.allclose(y, y1, rtol=0, atol=2e-5) and torch.allclose(g, g1_, rtol=0, atol=2e-5 * max(1., float(g1_.abs().max())))

@@ -8,9 +8,9 @@ Paths (BASELINE.json configs; F = 2 sum fan_in fan_out FLOP per coordinate, SURV
   sdf          5x256 d3 o1, 2^19 coords: forward_grad_store + seeded W3 from the kept forward (sdf kernels, 8F)
   video        5x512 d3 o3, 2^20 coords: forward_store + backward_stored (hidden 512 W2 = 3F)
   poisson      5x256 d2 o1, 512^2 grid: forward_laplace_store + laplace_backward_stored (W4s = 3 (1 + 2d) F = 15F)
-  poisson_ref  5x256 d2 o1, 512^2 grid: the reference recipe's kernels: W1 (J), the shared Hessian node's forward
-               (one 6-stream jet, kept), ONE quadratic-form jet reverse (its backward); the same loss gradient as
-               poisson (15F counted)
+  poisson_ref  5x256 d2 o1, 512^2 grid: the reference recipe's kernels in steady state: the shared Hessian node's
+               forward (one 6-stream jet, kept, which also returns y and J: the module's jet forward from the third
+               step on), ONE quadratic-form jet reverse (its backward); the same loss gradient as poisson (15F)
   w3_theta     5x256 d2 o1, 2^19 coords: W3 H v + theta-grads without a kept forward (6F)
   hypernet     32 x 4096 coords, 5x256 d2 o1 per-element weights: grouped stored forward + grouped reverse-only W2
                (the hypernetwork training kernels, W2 = 3F)
@@ -143,8 +143,9 @@ def build_step(name, dev):
         G = torch.diag_embed(gl.expand(n, d))  # the summed cotangent of the shared Hessian node: glap * I
 
         def step():
-            eng.forward_grad(ws, x)
-            _, kept = eng.hessian(ws, x, keep=True)          # the shared Hessian node (forward): one jet sweep
+            # the jet node's forward IS the shared Hessian node's sweep once the module has seen the recipe
+            # (JetState.hessian): y, J, Hm and the kept jets in one launch (siren_hessian_ex)
+            _, kept, _, _ = eng.hessian(ws, x, keep=True, want_yg=True)
             return eng.hessian_backward(ws, x, G, kept=kept)  # its ONE backward (third order): reverse-only jet
         return step
     raise ValueError(name)
