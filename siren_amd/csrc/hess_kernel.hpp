@@ -169,9 +169,12 @@ __global__ __launch_bounds__(THREADS, 1) void hess_kernel(const float* __restric
             p0 += sd[0] * act[0][rb][0] + sd[1] * act[0][rb][1] + sd[2] * act[0][rb][2] + sd[3] * act[0][rb][3];
         if (yo != nullptr) {
 #pragma unroll
-            for (int j = 0; j < MAXO; ++j) {  // WoT rows j >= o are zero padded
-                const f32x4 wj = *(const f32x4*)(sm + SM_WO + j * H + 16 * rb + 4 * g);
-                yv[j] += wj[0] * act[0][rb][0] + wj[1] * act[0][rb][1] + wj[2] * act[0][rb][2] + wj[3] * act[0][rb][3];
+            for (int j = 0; j < MAXO; ++j) {
+                if (j < o) {  // wave-uniform
+                    const f32x4 wj = *(const f32x4*)(sm + SM_WO + j * H + 16 * rb + 4 * g);
+                    yv[j] += wj[0] * act[0][rb][0] + wj[1] * act[0][rb][1] + wj[2] * act[0][rb][2] +
+                             wj[3] * act[0][rb][3];
+                }
             }
         }
     }
@@ -180,7 +183,8 @@ __global__ __launch_bounds__(THREADS, 1) void hess_kernel(const float* __restric
     if (gxo != nullptr) p0 = sum_groups(p0);  // lo: (u . (y - bout), unused) | hi: u . dy/dx_1
     if (yo != nullptr) {
 #pragma unroll
-        for (int j = 0; j < MAXO; ++j) yv[j] = sum_groups(yv[j]);  // lo: Wout_j . a_L
+        for (int j = 0; j < MAXO; ++j)
+            if (j < o) yv[j] = sum_groups(yv[j]);  // lo: Wout_j . a_L
     }
     if (valid && g == 0) {
         if (gxo != nullptr) {
