@@ -220,7 +220,8 @@ int32_t siren_hessian_backward(const siren_cfg* cfg, const float* ws, const floa
  * column per input dimension) — in ONE forward-mode second-order jet sweep over the coordinate axes (value, 2
  * tangents, 3 second-order streams; 8 coordinates x 6 streams in three MFMA tiles, no reverse sweep). kept (nullable,
  * siren_hessian_ws_floats(cfg, n, 1, &count) floats; caller-owned, 0 floats with keep = 0) receives the per-layer
- * jets: siren_hessian_backward_kept with the same kept then skips the forward GEMMs of its quadratic-form jet. Same
+ * jets of hidden layers 1..L (layer 0 is rebuilt from x): siren_hessian_backward_kept with the same kept then skips
+ * the forward GEMMs of its quadratic-form jet. Same
  * coverage as siren_hessian_backward. */
 int32_t siren_hessian_ws_floats(const siren_cfg* cfg, int64_t n, int32_t keep, int64_t* count);
 int32_t siren_hessian(const siren_cfg* cfg, const float* ws, const float* x, int64_t n, const float* u, float* kept,

@@ -242,7 +242,7 @@ class SirenHessian(torch.autograd.Function):
     (siren_hessian) that keeps its per-layer jets (KEEP_MAX_BYTES) for the backward, which then runs the reverse
     GEMMs only."""
 
-    KEEP_MAX_BYTES = 16 << 30  # kept jets: 4 (n_hidden + 1) 6 256 bytes per point (6 KiB / layer)
+    KEEP_MAX_BYTES = 16 << 30  # kept jets: 4 n_hidden 6 256 bytes per point (6 KiB / layer)
     KEEP_FREE_FRACTION = 0.5   # ... and at most this share of the device's free memory at forward time
 
     @staticmethod
@@ -257,7 +257,7 @@ class SirenHessian(torch.autograd.Function):
     def forward_sweep(engine, ws, x, u, want_yg=False):
         """The node's forward kernel: (hm, kept | None) — or (hm, kept | None, y, g) with want_yg — keeping the jets
         when they fit the budget (else the backward recomputes its forward jet)."""
-        per_point = 4 * (engine.cfg.n_hidden + 1) * 6 * 256
+        per_point = 4 * engine.cfg.n_hidden * 6 * 256  # layers 1..L (layer 0 is rebuilt from x)
         if x.shape[0] * per_point <= SirenHessian._keep_budget(x):
             try:
                 return engine.hessian(ws, x, u, keep=True, want_yg=want_yg)

@@ -22,8 +22,9 @@
 // KEEP: the pre-activation jets of every layer (bias included) go to a lane-major scratch, kept by the node for its
 // backward: the quadratic-form jet (jet_kernel.hpp QG, KEPT) then reads its forward from it instead of recomputing
 // the forward GEMMs (its second-order stream along Q is the linear combination sum_ij Q_ij d2z/dx_i dx_j).
-// Layout (hess_kept_off): [layer l][8-coordinate group][block rb][tile t][lane] f32x4 — each wave's stores are
-// 1 KiB contiguous.
+// Layout (hess_kept_off): [layer l - 1][8-coordinate group][block rb][tile t][lane] f32x4 for layers l = 1 .. L —
+// each wave's stores are 1 KiB contiguous. Layer 0's jet (z = W0 x + b0, z_i = W0[:, i], z_ij = 0) is not kept: the
+// backward rebuilds it from x (qf_layer0), which saves a quarter of the kept traffic at L = 3 (round 4).
 #include "lds_ops.h"
 #include "ring.hpp"
 #include "siren_common.h"
@@ -32,11 +33,11 @@ namespace siren {
 
 // 8-coordinate groups of a Hessian sweep over n coordinates (workgroups of 32)
 __host__ __device__ constexpr int64_t hess_groups(int64_t n) { return (n + 31) / 32 * 4; }
-// float offset of (layer l, group grp, block rb, tile t, lane) in the kept scratch, and the stride between layers (a
-// group-major order, each workgroup's jets of all layers contiguous, measured the same: 5.32 vs 5.31 ms forward)
+// float offset of (layer l >= 1, group grp, block rb, tile t, lane) in the kept scratch, and the stride between layers
+// (a group-major order, each workgroup's jets of all layers contiguous, measured the same: 5.32 vs 5.31 ms forward)
 __host__ __device__ constexpr int64_t hess_kept_off(int64_t ngroups, int lh, int l, int64_t grp, int rb, int t,
                                                     int lane) {
-    return ((((int64_t)l * ngroups + grp) * NB + rb) * 3 + t) * 256 + lane * 4;
+    return ((((int64_t)(l - 1) * ngroups + grp) * NB + rb) * 3 + t) * 256 + lane * 4;
 }
 __host__ __device__ constexpr int64_t hess_kept_lstride(int64_t ngroups) { return ngroups * NB * 3 * 256; }
 
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(THREADS, 1) void hess_kernel(const float* __restric
     const bool valid = coord < n;
     const float x0 = valid ? x[coord * d] : 0.f;
     const float x1 = (valid && d > 1) ? x[coord * d + 1] : 0.f;
-    float* kp = KEEP ? kept + hess_kept_off(ngroups, lh, 0, grp, 0, 0, lane) : nullptr;
+    float* kp = KEEP ? kept + hess_kept_off(ngroups, lh, 1, grp, 0, 0, lane) : nullptr;  // layer 1
     const int64_t kl = hess_kept_lstride(ngroups);  // floats between layers of the kept scratch
     __syncthreads();
     int s = 0;
@@ -104,12 +105,7 @@ __global__ __launch_bounds__(THREADS, 1) void hess_kernel(const float* __restric
         const f32x4 wb = *(const f32x4*)(sm + SM_W0 + H + nb);  // zero padded row when d == 1
         const f32x4 zv = *(const f32x4*)(sm + SM_BIAS + nb) + x0 * wa + x1 * wb;
         const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-        const f32x4 t0 = hi ? wa : zv, t1 = hi ? zero : wb;
-        if constexpr (KEEP) {
-            *(f32x4*)(kp + rb * 768) = t0;
-            *(f32x4*)(kp + rb * 768 + 256) = t1;
-            *(f32x4*)(kp + rb * 768 + 512) = zero;
-        }
+        const f32x4 t0 = hi ? wa : zv, t1 = hi ? zero : wb;  // (not kept: qf_layer0 rebuilds it)
         hess_sin(t0, t1, zero, w0, hi, act[0][rb], act[1][rb], act[2][rb]);
     }
 
@@ -136,7 +132,7 @@ __global__ __launch_bounds__(THREADS, 1) void hess_kernel(const float* __restric
         for (int rb = 0; rb < NB; ++rb) {
             const f32x4 t0 = hi ? acc[0][rb] : acc[0][rb] + *(const f32x4*)(bl + 16 * rb);
             if constexpr (KEEP) {
-                float* kpl = kp + l * kl;
+                float* kpl = kp + (l - 1) * kl;
                 *(f32x4*)(kpl + rb * 768) = t0;
                 *(f32x4*)(kpl + rb * 768 + 256) = acc[1][rb];
                 *(f32x4*)(kpl + rb * 768 + 512) = acc[2][rb];

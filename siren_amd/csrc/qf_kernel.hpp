@@ -60,6 +60,21 @@ __device__ __forceinline__ QfKept qf_load(const float* p) {
 
 __device__ __forceinline__ void qf_store_block(float* p, const f32x4& v) { store_block(p, 0, v); }
 
+// layer 0's jet of block rb, rebuilt from the coordinate exactly as hess_kernel computes it (it is not kept):
+// lo lanes (z, z_2, z_12) = (W0 x + b0, W0[:, 1], 0), hi lanes (z_1, z_11, z_22) = (W0[:, 0], 0, 0)
+__device__ __forceinline__ QfKept qf_layer0(const float* sm, int rb, int g, bool hi, float x0, float x1) {
+    const int nb = 16 * rb + 4 * g;
+    const f32x4 wa = *(const f32x4*)(sm + SM_W0 + nb);
+    const f32x4 wb = *(const f32x4*)(sm + SM_W0 + H + nb);  // zero padded row when d == 1
+    const f32x4 zv = *(const f32x4*)(sm + SM_BIAS + nb) + x0 * wa + x1 * wb;
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    QfKept r;
+    r.k[0] = hi ? wa : zv;
+    r.k[1] = hi ? zero : wb;
+    r.k[2] = zero;
+    return r;
+}
+
 // per-coordinate coefficients of the quadratic form (lane constants): q11 = G_11, q12 = G_12 + G_21, q22 = G_22
 struct QfCoef {
     float q11, q12, q22;
@@ -128,7 +143,7 @@ __global__ __launch_bounds__(THREADS, 1) void qf_rev_kernel(const float* __restr
     const bool valid = coord < n;
     const int64_t lstride = 4 * n_pad * H;                  // floats per layer of abuf / dbuf
     const int64_t toff = 2 * grp * (H * 16) + 4 * g * 16 + c;  // tile 0 of the pair; tile 1 at + H * 16
-    const float* kp = kept + hess_kept_off(ngroups, lh, 0, grp, 0, 0, lane);
+    const float* kp = kept + hess_kept_off(ngroups, lh, 1, grp, 0, 0, lane);  // layer 1 (layer 0 is rebuilt)
     const int64_t kl = hess_kept_lstride(ngroups);  // floats between layers of the kept scratch
     QfCoef q;
     {
@@ -159,12 +174,19 @@ __global__ __launch_bounds__(THREADS, 1) void qf_rev_kernel(const float* __restr
     auto epilogue = [&](int lm, auto seed) {
         constexpr bool SEED = decltype(seed)::value;
         const float wl = lm == 0 ? w0 : w, wl2 = wl * wl;
-        const float* kr = kp + lm * kl;
+        const bool rebuild = lm == 0;  // wave-uniform: layer 0's jet comes from x, not from the kept scratch
+        const float* kr = kp + (rebuild ? 0 : lm - 1) * kl;
         float* ap = abuf + (int64_t)lm * lstride + toff;
         float* dp = dbuf + (int64_t)lm * lstride + toff;
         QfKept kq[QF_PREFETCH];
+        float x0 = 0.f, x1 = 0.f;  // (loaded here, not held across the kernel: the register budget is full)
+        if (!rebuild) {
 #pragma unroll
-        for (int i = 0; i < QF_PREFETCH; ++i) kq[i] = qf_load(kr + i * 768);
+            for (int i = 0; i < QF_PREFETCH; ++i) kq[i] = qf_load(kr + i * 768);
+        } else {
+            x0 = valid ? x[coord * d] : 0.f;
+            x1 = (valid && d > 1) ? x[coord * d + 1] : 0.f;
+        }
         float uw[MAXO], gup[MAXO];
 #pragma unroll
         for (int j = 0; j < MAXO; ++j) {
@@ -173,9 +195,9 @@ __global__ __launch_bounds__(THREADS, 1) void qf_rev_kernel(const float* __restr
         }
 #pragma unroll
         for (int rb = 0; rb < NB; ++rb) {
-            const QfKept kc = kq[rb % QF_PREFETCH];
+            const QfKept kc = rebuild ? qf_layer0(sm, rb, g, hi, x0, x1) : kq[rb % QF_PREFETCH];
             asm volatile("" ::: "memory");  // keep the prefetch distance: no hoisting of the layer's 48 loads
-            if (rb + QF_PREFETCH < NB) kq[rb % QF_PREFETCH] = qf_load(kr + (rb + QF_PREFETCH) * 768);
+            if (!rebuild && rb + QF_PREFETCH < NB) kq[rb % QF_PREFETCH] = qf_load(kr + (rb + QF_PREFETCH) * 768);
             f32x4 ua, ub;
             if constexpr (SEED) {
                 // the cotangent of the a_L jet lives on the Q stream only: u_3 = sum_j u_j Wout_j (hi lanes, tile 1)

@@ -864,7 +864,7 @@ int32_t siren_hessian_backward_ws_floats(const siren_cfg* cfg, int64_t n, int64_
 int32_t siren_hessian_ws_floats(const siren_cfg* cfg, int64_t n, int32_t keep, int64_t* count) {
     if (int rc = check_quad(cfg)) return rc;
     if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
-    *count = keep ? siren::hess_groups(n) * 8 * (int64_t)(cfg->n_hidden + 1) * 6 * siren::H : 0;
+    *count = keep ? siren::hess_groups(n) * 8 * (int64_t)cfg->n_hidden * 6 * siren::H : 0;  // layers 1..L
     return SIREN_OK;
 }
 
