@@ -538,9 +538,10 @@ def path_rooflines(rates):
     from the committed per-path profile (profiles/pmc_<path>.json, tools/profile_round.sh: rocprofv3 kernel time,
     FETCH_SIZE / WRITE_SIZE HBM bytes per step and the kernels' I/O-contract bytes)."""
     out = {}
-    for path, mc in rates.items():
+    for key, mc in rates.items():
         if mc is None:
             continue
+        path = key.split('@')[0]  # 'image_w2@n2p20': the same path at another N (same kernels, same profile)
         try:
             rec = json.load(open(os.path.join(ROOT, 'profiles', 'pmc_%s.json' % path)))
         except (OSError, ValueError):
@@ -550,7 +551,7 @@ def path_rooflines(rates):
         c = rec['config']
         F = 2 * (c['d_in'] * c['hidden'] + c['hidden_layers'] * c['hidden'] ** 2 + c['hidden'] * c['d_out'])
         ach = PATH_UNITS[path] * F * mc * 1e6 / 1e12
-        out[path] = {'bound': 'mfma', 'unit': 'TFLOP/s', 'peak': PEAK_FP32_MFMA_TFLOPS,
+        out[key] = {'bound': 'mfma', 'unit': 'TFLOP/s', 'peak': PEAK_FP32_MFMA_TFLOPS,
                      'flop_per_coord': PATH_UNITS[path] * F, 'achieved_step': round(ach, 2),
                      'frac_step': round(ach / PEAK_FP32_MFMA_TFLOPS, 4),
                      'frac_kernels_rocprof': rec.get('mfma_frac_of_kernel_time'),
@@ -662,6 +663,7 @@ def main():
         cr, dpr = extra['configs'], dp or {}
         extra['roofline_by_path'] = path_rooflines({
             'image_w2': extra['w2_image_mse_train_mcoords_s'],
+            'image_w2@n2p20': extra['w2_image_mse_train_n2p20_mcoords_s'],  # config 2's own N
             'sdf': dpr.get('sdf_5x256_d3', {}).get('mcoords_s') if n_ranks == 1 else None,
             'video': dpr.get('video_5x512_d3o3', {}).get('mcoords_s') if n_ranks == 1 else None,
             'video1024': dpr.get('video_5x1024_d3o3', {}).get('mcoords_s') if n_ranks == 1 else None,

@@ -43,49 +43,62 @@ __global__ void pack_kernel(const float* __restrict__ p, float* __restrict__ ws,
     const int lsf = 4 + __builtin_ctz((unsigned)h);  // log2(slice floats)
     const unsigned sfm = (1u << lsf) - 1u;
     const unsigned hm = (unsigned)h - 1u, lh2 = (unsigned)__builtin_ctz((unsigned)h);
-    for (int64_t gidx = begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; gidx < total;
-         gidx += (int64_t)gridDim.x * blockDim.x) {
+    // one thread per 4 consecutive workspace floats (one 16 B store; region boundaries of the small block are multiples
+    // of 4): a slice quad is 4 consecutive floats of one W row (forward) or one float of 4 rows (transposed), so the
+    // index math runs once per quad (the per-float version was instruction-bound: 49 us for 32 x 1.6 MB)
+    const int64_t qend = total >> 2;
+    for (int64_t qi = (begin >> 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; qi < qend;
+         qi += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t gidx = qi << 2;
         const bool scaled = base > 0 && gidx >= base;
         const unsigned idx = (unsigned)(scaled ? gidx - base : gidx);
-        float v = 0.f, sc = 1.f;
+        f32x4 v4 = {0.f, 0.f, 0.f, 0.f};
+        float sc = 1.f;
         if (idx < (unsigned)spad) {
-            const int e = (int)idx;
-            if (e < sl.wo) {
-                const int k = e >> lh2, n = e & hm;
-                v = k < d ? p[off.w0 + (int64_t)n * d + k] : 0.f;
-                sc = s0;
-            } else if (e < sl.seed) {
-                const int j = (e - sl.wo) >> lh2, n = (e - sl.wo) & hm;
-                v = j < o ? p[off.wout + (int64_t)j * h + n] : 0.f;
-            } else if (e < sl.bout) {
-                const int n = e - sl.seed;
-                float acc = 0.f;
-                for (int j = 0; j < o; ++j) acc += p[off.wout + (int64_t)j * h + n];
-                v = acc;
-            } else if (e < sl.bias) {
-                const int j = e - sl.bout;
-                v = j < o ? p[off.bout + j] : 0.f;
-            } else if (e < sl.floats(lh)) {
-                const int l = (e - sl.bias) >> lh2, n = (e - sl.bias) & hm;
-                v = p[off.b(l) + n];
-                sc = l == 0 ? s0 : s;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int e = (int)idx + q;
+                float v = 0.f;
+                if (e < sl.wo) {
+                    const int k = e >> lh2, n = e & hm;
+                    v = k < d ? p[off.w0 + (int64_t)n * d + k] : 0.f;
+                    sc = s0;
+                } else if (e < sl.seed) {
+                    const int j = (e - sl.wo) >> lh2, n = (e - sl.wo) & hm;
+                    v = j < o ? p[off.wout + (int64_t)j * h + n] : 0.f;
+                } else if (e < sl.bout) {
+                    const int n = e - sl.seed;
+                    float acc = 0.f;
+                    for (int j = 0; j < o; ++j) acc += p[off.wout + (int64_t)j * h + n];
+                    v = acc;
+                } else if (e < sl.bias) {
+                    const int j = e - sl.bout;
+                    v = j < o ? p[off.bout + j] : 0.f;
+                } else if (e < sl.floats(lh)) {
+                    const int l = (e - sl.bias) >> lh2, n = (e - sl.bias) & hm;
+                    v = p[off.b(l) + n];
+                    sc = l == 0 ? s0 : s;
+                }
+                v4[q] = v;
             }
         } else {
             const unsigned e = idx - (unsigned)spad;
             const unsigned slice = e >> lsf;
             const unsigned w = e & sfm;
-            const int r = w & 3, i = (w >> 2) & 15, g = (w >> 6) & 3, blk = w >> 8;
+            const int i = (w >> 2) & 15, g = (w >> 6) & 3, blk = w >> 8;
             if (slice < (unsigned)(lh * nb)) {
                 const int l = (int)(slice / nb) + 1, kb = (int)(slice % nb);
-                v = p[off.w(l) + (int64_t)(16 * blk + i) * h + 16 * kb + 4 * g + r];
+                const float* src = p + off.w(l) + (int64_t)(16 * blk + i) * h + 16 * kb + 4 * g;
+                v4 = f32x4{src[0], src[1], src[2], src[3]};
             } else {
                 const int s2 = (int)slice - lh * nb;
                 const int l = lh - s2 / nb, kb = s2 % nb;
-                v = p[off.w(l) + (int64_t)(16 * kb + 4 * g + r) * h + 16 * blk + i];
+                const float* src = p + off.w(l) + (int64_t)(16 * kb + 4 * g) * h + 16 * blk + i;
+                v4 = f32x4{src[0], src[h], src[2 * h], src[3 * h]};
             }
             sc = s;
         }
-        ws[gidx] = scaled ? v * sc : v;
+        *(f32x4*)(ws + gidx) = scaled ? v4 * sc : v4;
     }
 }
 

@@ -8,7 +8,7 @@ namespace siren {
 void launch_pack(const float* p, float* ws, int d, int o, int lh, int h, int64_t spad, int64_t total, int64_t base,
                  float s0, float s, hipStream_t st, int batch, int64_t p_bstride, int64_t begin) {
     const int threads = 256;
-    const int64_t blocks = std::min<int64_t>((total - begin + threads - 1) / threads, 8192);
+    const int64_t blocks = std::min<int64_t>(((total - begin) / 4 + threads - 1) / threads, 8192);  // one quad / thread
     hipLaunchKernelGGL(pack_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1), (unsigned)batch), dim3(threads), 0,
                        st, p, ws, d, o, lh, spad, total, h, base, s0, s, p_bstride, begin);
 }
