@@ -58,6 +58,7 @@ class JetState:
         self.mode = mode
         self.active = mode is True
         self.hessian = False
+        self.laplace = False  # likewise for the fused diff_operators.laplace of the value node (W4 jet sweep)
 
     def observe_x_gradient_request(self):
         if self.mode == 'auto':
@@ -67,13 +68,27 @@ class JetState:
         if self.mode in ('auto', True):
             self.hessian = True
 
+    def observe_laplace_request(self):
+        if self.mode in ('auto', True):
+            self.laplace = True
+
 
 class SirenFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, engine, jet, x, flat, store=False):
         ws = engine.pack(flat)
-        ctx.tws = None
-        if store and engine.stored_for(x.shape[0]) and STORED_FORWARD:
+        ctx.tws, ctx.pre_laplace = None, None
+        if jet is not None and jet.laplace and engine.laplace_supported:
+            # this module's output went to diff_operators.laplace last time (laplace_mse): the value comes from the
+            # W4 jet sweep that laplace() needs anyway, and its Laplacian (+ kept jet stores) wait on this node for
+            # fused_laplace — one forward sweep instead of a stored W1 forward AND the jet
+            if store and STORED_FORWARD:
+                lap, ltws, y = engine.forward_laplace_store(ws, x, want_y=True)
+            else:
+                y, _, lap = engine.forward_laplace(ws, x)
+                ltws = None
+            ctx.pre_laplace = (lap, ltws)
+        elif store and engine.stored_for(x.shape[0]) and STORED_FORWARD:
             # training forward: keep a_l / cos(w z_l) so the weight-gradient backward is reverse-only
             y, ctx.tws = engine.forward_store(ws, x)
         else:
@@ -481,9 +496,11 @@ class SirenLaplace(torch.autograd.Function):
     differentiable backward (create_graph over it, a fourth derivative) recomputes with device torch ops."""
 
     @staticmethod
-    def forward(ctx, engine, ws, x, flat, store=False):
+    def forward(ctx, engine, ws, x, flat, store=False, pre=None):
         ctx.tws = None
-        if store and STORED_FORWARD:  # training: keep the jet stores, the backward is reverse-only
+        if pre is not None:  # (lap, kept stores | None) run by the value node's forward (JetState.laplace)
+            lap, ctx.tws = pre
+        elif store and STORED_FORWARD:  # training: keep the jet stores, the backward is reverse-only
             lap, ctx.tws = engine.forward_laplace_store(ws, x)
         else:
             _, _, lap = engine.forward_laplace(ws, x)
@@ -498,16 +515,16 @@ class SirenLaplace(torch.autograd.Function):
         need_x = ctx.needs_input_grad[2] and _will_execute(ctx, 1)
         need_p = ctx.needs_input_grad[3] and _will_execute(ctx, 2)
         if not (need_x or need_p):
-            return None, None, None, None, None
+            return None, None, None, None, None, None
         if not torch.is_grad_enabled():
             if ctx.tws is not None:
                 gx, gp = ctx.engine.laplace_backward_stored(ctx.ws, x, glap, ctx.tws)
             else:
                 gx, gp = ctx.engine.laplace_backward(ctx.ws, x, glap)
-            return None, None, (gx if need_x else None), (gp if need_p else None), None
+            return None, None, (gx if need_x else None), (gp if need_p else None), None, None
         gx, gp = _torch_path.laplace_vjp(ctx.engine.cfg, x, flat, glap.contiguous(),
                                          create_graph=torch.is_grad_enabled())
-        return None, None, (gx if need_x else None), (gp if need_p else None), None
+        return None, None, (gx if need_x else None), (gp if need_p else None), None, None
 
 
 _VIEW_NODES = ('ViewBackward0', 'ReshapeAliasBackward0', 'UnsafeViewBackward0')
@@ -547,5 +564,14 @@ def fused_laplace(y, x):
     if node is None or not node.engine.laplace_supported:
         return None
     xs, flat = node.saved_tensors[:2]
-    lap = SirenLaplace.apply(node.engine, node.ws, xs, flat, torch.is_grad_enabled() and flat.requires_grad)
+    store = torch.is_grad_enabled() and flat.requires_grad
+    pre = getattr(node, 'pre_laplace', None)
+    if pre is not None and store and pre[1] is None:
+        pre = None  # computed without the jet stores (no parameter graph then); this call wants them
+    lap = SirenLaplace.apply(node.engine, node.ws, xs, flat, store, pre)
+    if hasattr(node, 'pre_laplace'):
+        node.pre_laplace = None
+    jet = getattr(node, 'jet', None)
+    if jet is not None:
+        jet.observe_laplace_request()
     return lap.view(*y.shape[:-1], 1)

@@ -356,9 +356,9 @@ class SirenEngine:
                    'siren_laplace_backward')
         return gx, gp
 
-    def forward_laplace_store(self, ws, x):
+    def forward_laplace_store(self, ws, x, want_y=False):
         """Split W4 (laplace_mse training forward): the Laplacian (n, 1) + the jet stores, kept in a workspace for
-        laplace_backward_stored. Returns (lap, tws)."""
+        laplace_backward_stored. Returns (lap, tws), or (lap, tws, y) with want_y (y = Phi(x) from the same sweep)."""
         self._require()
         x = self._check_x(x)
         n = x.shape[0]
@@ -367,10 +367,11 @@ class SirenEngine:
                    'siren_laplace_backward_ws_floats')
         tws = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
         lap = torch.empty(n, 1, dtype=torch.float32, device=x.device)
-        _lib.check(self.lib.siren_forward_laplace_store(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, None, None,
+        y = torch.empty(n, self.cfg.d_out, dtype=torch.float32, device=x.device) if want_y else None
+        _lib.check(self.lib.siren_forward_laplace_store(ctypes.byref(self.cfg), _ptr(ws), _ptr(x), n, _ptr(y), None,
                                                         _ptr(lap), _ptr(tws), _stream(x.device)),
                    'siren_forward_laplace_store')
-        return lap, tws
+        return (lap, tws, y) if want_y else (lap, tws)
 
     def laplace_backward_stored(self, ws, x, glap, tws):
         """Split W4s: (gx, gparams) from forward_laplace_store's workspace (reverse-only jet sweep)."""

@@ -203,3 +203,41 @@ def test_split_laplace_forward_backward_matches(cuda, n, d, L):
     gx_s, gp_s = eng.laplace_backward_stored(ws, x, glap, tws)
     gx_r, gp_r = eng.laplace_backward(ws, x, glap)
     assert torch.equal(gx_s, gx_r) and torch.equal(gp_s, gp_r)
+
+
+def test_laplace_mse_one_forward_sweep(cuda, g1, monkeypatch):
+    """From the second step on (the module's output went to diff_operators.laplace: JetState.laplace) the module's
+    forward IS the W4 jet sweep (y from the same launch, its Laplacian and kept stores handed to fused_laplace): no
+    stored W1 forward, one jet forward, one reverse-only W4s backward — and the step still matches the reference's
+    fp64 laplace_mse theta-grads (G1), its Laplacian and its model output."""
+    from siren_amd import loss_functions as LF
+    from siren_amd.engine import SirenEngine
+    from siren_amd.modules import SingleBVPNet
+    calls = {'fwd_store': 0, 'lap_store': 0, 'lap_bwd_stored': 0}
+    orig = {k: getattr(SirenEngine, k) for k in ('forward_store', 'forward_laplace_store', 'laplace_backward_stored')}
+
+    def wrap(name, key):
+        def f(self, *a, **k):
+            calls[key] += 1
+            return orig[name](self, *a, **k)
+        return f
+    monkeypatch.setattr(SirenEngine, 'forward_store', wrap('forward_store', 'fwd_store'))
+    monkeypatch.setattr(SirenEngine, 'forward_laplace_store', wrap('forward_laplace_store', 'lap_store'))
+    monkeypatch.setattr(SirenEngine, 'laplace_backward_stored', wrap('laplace_backward_stored', 'lap_bwd_stored'))
+    m = SingleBVPNet(verbose=False).to(cuda)
+    m.load_state_dict({k[2:]: torch.tensor(v) for k, v in g1.items() if k.startswith('w_')})
+    gt = {'laplace': to_dev(g1['gt_laplace'], cuda)}
+    for step in range(3):
+        for k in calls:
+            calls[k] = 0
+        m.zero_grad()
+        out = m({'coords': to_dev(g1['coords'], cuda)})
+        losses = LF.laplace_mse(out, gt)
+        losses['laplace_loss'].backward()
+        if step >= 1:
+            assert calls == {'fwd_store': 0, 'lap_store': 1, 'lap_bwd_stored': 1}, (step, calls)
+            for k, p in m.named_parameters():
+                ref = g1['G1_laplace_mse_grad_' + k]
+                assert np.max(np.abs(p.grad.cpu().numpy() - ref)) <= 1e-4 * np.max(np.abs(ref)) + 1e-12, k
+            y = out['model_out'].detach().cpu().numpy()
+            assert np.max(np.abs(y - g1['G1_model_out_f64'])) <= 1e-4
