@@ -128,7 +128,8 @@ __global__ __launch_bounds__(THREADS, 1) void qf_rev_kernel(const float* __restr
     __shared__ __attribute__((aligned(16))) float lds[NBUF * SLICE + SMALL_MAX];
     float* ring = lds;
     float* sm = lds + NBUF * SLICE;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR): never a spilled VGPR
     const int g = lane >> 4, c = lane & 15;
     const bool hi = c >= 8;
     const int nslices = 2 * lh * NB;

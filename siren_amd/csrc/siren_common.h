@@ -297,6 +297,15 @@ __device__ __forceinline__ f32x4 fma4(float s, const f32x4& v, const f32x4& z) {
                  __builtin_fmaf(s, v[3], z[3])};
 }
 
+// A scalar operand as an opaque value. A context-struct field splat into an f32x4 product is otherwise widened by
+// instcombine into a 16-byte load across the neighbouring fields; SROA then cannot split the struct, it stays in
+// scratch, and its fields are reloaded from scratch (with a vmcnt wait) inside the MFMA loops (round 4: the W1
+// seed epilogue, every w3i epilogue). Census: no private alloca in any kernel (`= alloca` in the device IR).
+__device__ __forceinline__ float opaque(float v) {
+    asm("" : "+v"(v));
+    return v;
+}
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }

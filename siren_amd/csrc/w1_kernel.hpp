@@ -277,7 +277,7 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
         for (int j = 0; j < MAXO; ++j)
             if (j < cx.o && !cx.seed_ones) ga += st.gyv[j] * ep.v[1 + j];
         if (cx.seed_ones) ga = ep.v[5];
-        st.act[b] = (ga * cs) * cx.wsd;
+        st.act[b] = (ga * cs) * opaque(cx.wsd);
         if (cx.dstore) store_block(cx.dbuf + LH * cx.lstride, b, st.act[b]);
     } else if constexpr (KIND == EPI_SEED) {
         const f32x4 z = st.acc[(G + 1) & 1][b] + ep.v[0];
@@ -300,7 +300,7 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
             }
         }
         if (cx.seed_ones) ga = ep.v[5];
-        st.act[b] = (ga * cs) * cx.wsd;
+        st.act[b] = (ga * cs) * opaque(cx.wsd);
         if constexpr (STORE) store_block(cx.dbuf + LH * cx.lstride, b, st.act[b]);
     } else {
         constexpr int L = 2 * LH - G;  // delta_L = u_L . cos(w z_L) . w,  1 <= L < LH

@@ -301,9 +301,9 @@ __device__ __forceinline__ void w3i_epilogue(W3iState<LH>& st, const W3iCtx& cx,
         }
         const f32x4 z = zx + ep.v[4];
         f32x4 sn, cs;
-        w3_sincos4(cx.w0 * z, sn, cs);
+        w3_sincos4(opaque(cx.w0) * z, sn, cs);
         st.ap[b] = sn;
-        st.at[b] = (cx.w0 * cs) * zd;
+        st.at[b] = (opaque(cx.w0) * cs) * zd;
         spill(0, 1, zd);
         if constexpr (!KEPT) spill(0, 0, z);  // the reverse recomputes sin / cos of w0 z (bitwise the same)
         if constexpr (THETA) {
@@ -313,13 +313,13 @@ __device__ __forceinline__ void w3i_epilogue(W3iState<LH>& st, const W3iCtx& cx,
     } else if constexpr (KIND == W3E_FWD) {
         const f32x4 zd = acct[b];
         if constexpr (KEPT) {
-            st.at[b] = (cx.w * st.pc[slot]) * zd;
+            st.at[b] = (opaque(cx.w) * st.pc[slot]) * zd;
         } else {
             const f32x4 z = accp[b] + ep.v[0];
             f32x4 sn, cs;
-            w3_sincos4(cx.w * z, sn, cs);
+            w3_sincos4(opaque(cx.w) * z, sn, cs);
             st.ap[b] = sn;
-            st.at[b] = (cx.w * cs) * zd;
+            st.at[b] = (opaque(cx.w) * cs) * zd;
             spill(G, 0, z);
             if constexpr (THETA) tile(sn);
         }
@@ -334,14 +334,14 @@ __device__ __forceinline__ void w3i_epilogue(W3iState<LH>& st, const W3iCtx& cx,
             sn = st.ps[slot];
         } else {
             const f32x4 z = accp[b] + ep.v[0];
-            w3_sincos4(cx.w * z, sn, cs);
+            w3_sincos4(opaque(cx.w) * z, sn, cs);
         }
-        const f32x4 atl = (cx.w * cs) * zd;
+        const f32x4 atl = (opaque(cx.w) * cs) * zd;
         if constexpr (THETA) {
             if constexpr (!KEPT) tile(sn);
             tile(atl);
         }
-        f32x4 adb = cx.useed * ep.v[5];
+        f32x4 adb = opaque(cx.useed) * ep.v[5];
         f32x4 abseed = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < MAXO; ++j) {
@@ -353,8 +353,8 @@ __device__ __forceinline__ void w3i_epilogue(W3iState<LH>& st, const W3iCtx& cx,
             abseed = abseed + st.gyv[j] * wj;
             adb = adb + st.uv[j] * wj;
         }
-        st.at[b] = (cx.w * cs) * adb;
-        st.ap[b] = (cx.w * cs) * abseed - (cx.w * cx.w) * sn * zd * adb;
+        st.at[b] = (opaque(cx.w) * cs) * adb;
+        st.ap[b] = (opaque(cx.w) * cs) * abseed - (opaque(cx.w) * opaque(cx.w)) * sn * zd * adb;
         if constexpr (THETA) {
             tile(st.ap[b]);
             tile(st.at[b]);
@@ -366,11 +366,11 @@ __device__ __forceinline__ void w3i_epilogue(W3iState<LH>& st, const W3iCtx& cx,
             cs = st.pc[slot];
             sn = st.ps[slot];
         } else {
-            w3_sincos4(cx.w * st.pc[slot], sn, cs);
+            w3_sincos4(opaque(cx.w) * st.pc[slot], sn, cs);
         }
-        const f32x4 wc = cx.w * cs;
+        const f32x4 wc = opaque(cx.w) * cs;
         st.at[b] = wc * acct[b];
-        st.ap[b] = wc * accp[b] - (cx.w * cx.w) * sn * st.pz[slot] * acct[b];
+        st.ap[b] = wc * accp[b] - (opaque(cx.w) * opaque(cx.w)) * sn * st.pz[slot] * acct[b];
         if constexpr (THETA) {
             tile(st.ap[b]);
             tile(st.at[b]);

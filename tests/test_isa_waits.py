@@ -43,7 +43,8 @@ def _compile_and_check(tu):
         i = s.find('\n' + nm + ':')
         j = s.find('.Lfunc_end', i)
         body = s[i:j].split('\n')
-        probs = C.check(body, nm) + C.check_vmem(body, nm) + C.check_store_data(body, nm) + C.check_flat(body, nm)
+        probs = (C.check(body, nm) + C.check_vmem(body, nm) + C.check_store_data(body, nm) + C.check_flat(body, nm) +
+                 C.check_private(body, nm))
         if probs:
             bad.append('%s %s: %d (first: %s)' % (tu, nm, len(probs), probs[0][1]))
     return bad

@@ -349,6 +349,18 @@ def check_flat(body, name):
     return problems
 
 
+def check_private(body, name):
+    """Explicit private-memory (scratch) accesses — a context struct or array the compiler could not keep in registers
+    (SROA blocked, e.g. by a scalar field's splat widened into a 16-byte load), whose fields are then reloaded from
+    scratch with a vmcnt wait in the hot loop. Register spills ("Folded Spill / Reload") are not reported here."""
+    problems = []
+    for no, line in enumerate(body):
+        t = line.strip()
+        if t.startswith('scratch_') and 'Folded' not in t:
+            problems.append((no, t.split(';')[0].strip(), None))
+    return problems
+
+
 def main():
     path = sys.argv[1]
     want = sys.argv[2] if len(sys.argv) > 2 else ''
@@ -361,7 +373,8 @@ def main():
         i = s.find('\n' + nm + ':')
         j = s.find('.Lfunc_end', i)
         body = s[i:j].split('\n')
-        probs = check(body, nm) + check_vmem(body, nm) + check_store_data(body, nm) + check_flat(body, nm)
+        probs = (check(body, nm) + check_vmem(body, nm) + check_store_data(body, nm) + check_flat(body, nm) +
+                 check_private(body, nm))
         print('%-70s %d reads of in-flight load registers' % (nm[:70], len(probs)))
         for no, t, ln in probs[:8]:
             print('    line %d: %s   (load at line %d: %s)' % (no, t, ln, body[ln].strip()))
