@@ -59,6 +59,18 @@ class JetState:
         self.active = mode is True
         self.hessian = False
         self.laplace = False  # likewise for the fused diff_operators.laplace of the value node (W4 jet sweep)
+        self._unused = None   # [bool]: the last speculative sweep's results were not (yet) consumed
+
+    def speculate(self):
+        """Called by a forward about to run a speculative sweep: if the previous one was never consumed (the loss
+        stopped asking for the Hessian / Laplacian), switch the modes off — a later request turns them on again.
+        Returns the flag cell for this forward's node (set to False when its results are consumed)."""
+        if self._unused is not None and self._unused[0]:
+            self.hessian = self.laplace = False
+            self._unused = None
+            return None
+        self._unused = [True]
+        return self._unused
 
     def observe_x_gradient_request(self):
         if self.mode == 'auto':
@@ -78,7 +90,10 @@ class SirenFunction(torch.autograd.Function):
     def forward(ctx, engine, jet, x, flat, store=False):
         ws = engine.pack(flat)
         ctx.tws, ctx.pre_laplace = None, None
-        if jet is not None and jet.laplace and engine.laplace_supported:
+        # (jet is None unless a graph is being recorded — modules._fused_apply — so a no_grad evaluation after
+        # laplace training, e.g. summaries or create_mesh, keeps the plain forward)
+        ctx.spec = jet.speculate() if (jet is not None and jet.laplace and engine.laplace_supported) else None
+        if ctx.spec is not None:
             # this module's output went to diff_operators.laplace last time (laplace_mse): the value comes from the
             # W4 jet sweep that laplace() needs anyway, and its Laplacian (+ kept jet stores) wait on this node for
             # fused_laplace — one forward sweep instead of a stored W1 forward AND the jet
@@ -142,7 +157,9 @@ class SirenJetFunction(torch.autograd.Function):
         ctx.tws = None
         ctx.jet, ctx.pre_hessian = jet, None
         pre = None
-        if jet is not None and jet.hessian and not split and engine.hessian_backward_supported:
+        ctx.spec = (jet.speculate() if (jet is not None and jet.hessian and not split and
+                                        engine.hessian_backward_supported) else None)
+        if ctx.spec is not None:
             pre = SirenHessian.forward_sweep(engine, ws, x, None, want_yg=True)
         if pre is not None:
             # the Hessian node of this module's gradient will be requested again (it was last step): run its sweep
@@ -320,6 +337,8 @@ def _hessian_product(ctx, engine, ws, x, flat, v, u=None):
         hm = SirenHessian.apply(engine, ws, x, flat, u, pre)
         ctx.hessian_node = hm
         ctx.pre_hessian = None
+        if pre is not None and getattr(ctx, 'spec', None) is not None:
+            ctx.spec[0] = False  # the speculative sweep was used
         jet = getattr(ctx, 'jet', None)
         if u is None and jet is not None:
             jet.observe_hessian_request()
@@ -571,6 +590,8 @@ def fused_laplace(y, x):
     lap = SirenLaplace.apply(node.engine, node.ws, xs, flat, store, pre)
     if hasattr(node, 'pre_laplace'):
         node.pre_laplace = None
+    if pre is not None and getattr(node, 'spec', None) is not None:
+        node.spec[0] = False  # the speculative sweep was used
     jet = getattr(node, 'jet', None)
     if jet is not None:
         jet.observe_laplace_request()

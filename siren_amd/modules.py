@@ -193,7 +193,9 @@ def _fused_apply(engine, jet, coords, weights_biases, precision='fp32'):
         y = engine.forward_split(engine.pack_split(flat.detach()), x2d.detach().contiguous())
     else:
         # a graph that will want parameter gradients: the forward keeps a_l / cos for a reverse-only backward
-        y = SirenFunction.apply(engine, jet, x2d, flat, torch.is_grad_enabled() and flat.requires_grad)
+        # (the jet state only matters when a graph is recorded: a derivative can be requested of y only then)
+        y = SirenFunction.apply(engine, jet if torch.is_grad_enabled() else None, x2d, flat,
+                                torch.is_grad_enabled() and flat.requires_grad)
     return y.view(*lead, y.shape[-1])
 
 

@@ -241,3 +241,17 @@ def test_laplace_mse_one_forward_sweep(cuda, g1, monkeypatch):
                 assert np.max(np.abs(p.grad.cpu().numpy() - ref)) <= 1e-4 * np.max(np.abs(ref)) + 1e-12, k
             y = out['model_out'].detach().cpu().numpy()
             assert np.max(np.abs(y - g1['G1_model_out_f64'])) <= 1e-4
+    # a no_grad evaluation after laplace training keeps the plain forward (no jet sweep)
+    jets = {'n': 0}
+    orig_fl = SirenEngine.forward_laplace
+
+    def fl(self, *a, **k):
+        jets['n'] += 1
+        return orig_fl(self, *a, **k)
+    monkeypatch.setattr(SirenEngine, 'forward_laplace', fl)
+    for k in calls:
+        calls[k] = 0
+    with torch.no_grad():
+        y = m({'coords': to_dev(g1['coords'], cuda)})['model_out'].cpu().numpy()
+    assert jets['n'] == 0 and calls['lap_store'] == 0
+    assert np.max(np.abs(y - g1['G1_model_out_f64'])) <= 1e-4

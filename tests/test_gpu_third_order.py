@@ -388,6 +388,18 @@ def test_reference_recipe_one_forward_sweep(cuda, g1, monkeypatch):
                 assert np.max(np.abs(p.grad.cpu().numpy() - ref)) <= 1e-4 * np.max(np.abs(ref)) + 1e-12, k
             y = out['model_out'].detach().cpu().numpy()
             assert np.max(np.abs(y - g1['G1_model_out_f64'])) <= 1e-4
+    # the loss stops asking for the Hessian (a first-order gradient loss): one wasted speculative sweep, then the
+    # jet forward is the W1 kernel again
+    from siren_amd import diff_operators as D
+    for step in range(3):
+        for k in calls:
+            calls[k] = 0
+        out = m({'coords': to_dev(g1['coords'], cuda)})
+        g = D.gradient(out['model_out'], out['model_in'])
+        m.zero_grad()
+        (g ** 2).mean().backward()
+        if step >= 1:
+            assert calls['hess_yg'] == 0 and calls['w1'] == 1, (step, calls)
 
 
 @pytest.mark.parametrize('n,d,L,o,weighted', [(1, 2, 3, 1, False), (1000, 2, 3, 1, False), (333, 1, 2, 3, True),
