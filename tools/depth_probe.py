@@ -1,6 +1,7 @@
-"""W0 / W1 kernel efficiency vs depth (hidden layers 1..3, hidden 256, d 2, o 1): separates per-layer costs from
-code-size effects (the fully unrolled W1 body grows ~40 KB per hidden layer).
-usage: python tools/depth_probe.py [--n N]"""
+"""W0 / W1 / W2 / W3 efficiency vs depth (hidden layers 1..5, hidden 256, d 2, o 1): separates per-layer costs
+from code-size effects (the fully unrolled W1 body grows ~40 KB per hidden layer) and measures the 4..5-layer
+stored split against the register-resident 1..3-layer kernels.
+usage: python tools/depth_probe.py [--n N] [--layers 1,2,3,4,5]"""
 import argparse
 import os
 import sys
@@ -14,19 +15,24 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--n', type=int, default=1 << 20)
     ap.add_argument('--reps', type=int, default=10)
+    ap.add_argument('--layers', default='1,2,3,4,5')
     a = ap.parse_args()
     import __graft_entry__
     __graft_entry__.build()
     from siren_amd.engine import SirenEngine
     dev = torch.device('cuda:0')
     x = torch.rand(a.n, 2, device=dev) * 2 - 1
-    for L in (1, 2, 3):
+    gy = torch.randn(a.n, 1, device=dev)
+    v = torch.randn(a.n, 2, device=dev)
+    for L in [int(t) for t in a.layers.split(',')]:
         eng = SirenEngine(2, 256, L, 1)
         torch.manual_seed(0)
         flat = (torch.rand(eng.param_count, device=dev) - 0.5) * 0.01
         ws = eng.pack(flat)
         F = 2 * (2 * 256 + L * 256 * 256 + 256)
-        for name, fn, fl in (('W0', lambda: eng.forward(ws, x), F), ('W1', lambda: eng.forward_grad(ws, x), 2 * F)):
+        for name, fn, fl in (('W0', lambda: eng.forward(ws, x), F), ('W1', lambda: eng.forward_grad(ws, x), 2 * F),
+                             ('W2', lambda: eng.backward_params(ws, x, gy), 3 * F),
+                             ('W3th', lambda: eng.second_order(ws, x, v, want_theta=True), 6 * F)):
             fn()
             torch.cuda.synchronize()
             ts = []
