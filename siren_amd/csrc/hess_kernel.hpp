@@ -41,6 +41,16 @@ __host__ __device__ constexpr int64_t hess_kept_off(int64_t ngroups, int lh, int
 }
 __host__ __device__ constexpr int64_t hess_kept_lstride(int64_t ngroups) { return ngroups * NB * 3 * 256; }
 
+// this lane's index, recomputed at each use (exec must be full there): an asm without inputs is neither hoisted nor
+// merged, so the lane-derived LDS / global addresses of the epilogues (bias and Wout rows, kept pointer, coordinate)
+// are rebuilt in two VALU ops instead of living across the layer loop — at 512 registers they were the spills, each
+// reload a vmcnt(0) that also drained the weight ring's in-flight slices
+__device__ __forceinline__ int lane_here() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 __device__ __forceinline__ float row_ror8(float v) {
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xf, 0xf, false));
 }
@@ -88,8 +98,6 @@ __global__ __launch_bounds__(THREADS, 1) void hess_kernel(const float* __restric
     const bool valid = coord < n;
     const float x0 = valid ? x[coord * d] : 0.f;
     const float x1 = (valid && d > 1) ? x[coord * d + 1] : 0.f;
-    float* kp = KEEP ? kept + hess_kept_off(ngroups, lh, 1, grp, 0, 0, lane) : nullptr;  // layer 1
-    const int64_t kl = hess_kept_lstride(ngroups);  // floats between layers of the kept scratch
     __syncthreads();
     int s = 0;
     ring_issue(stream, ring, 0, nslices, wave, lane);
@@ -128,12 +136,13 @@ __global__ __launch_bounds__(THREADS, 1) void hess_kernel(const float* __restric
                 ++s;
             }
         }
-        const float* bl = sm + SM_BIAS + l * H + 4 * g;
+        const int le = lane_here();
+        const float* bl = sm + SM_BIAS + l * H + 4 * (le >> 4);
 #pragma unroll
         for (int rb = 0; rb < NB; ++rb) {
             const f32x4 t0 = hi ? acc[0][rb] : acc[0][rb] + *(const f32x4*)(bl + 16 * rb);
             if constexpr (KEEP) {
-                float* kpl = kp + (l - 1) * kl;
+                float* kpl = kept + hess_kept_off(ngroups, lh, l, grp, 0, 0, le);
                 *(f32x4*)(kpl + rb * 768) = t0;
                 *(f32x4*)(kpl + rb * 768 + 256) = acc[1][rb];
                 *(f32x4*)(kpl + rb * 768 + 512) = acc[2][rb];
@@ -145,20 +154,24 @@ __global__ __launch_bounds__(THREADS, 1) void hess_kernel(const float* __restric
     // ---- Hm = Wout-weighted last jet: seed sum_j u_j Wout_j (u == NULL: sum_j Wout_j) ---------------------------
     // (yo / gxo nullable: y_j = Wout_j . a_L + bout_j and the seed-weighted gradient sum_j u_j dPhi_j/dx from the
     // same last jet — the value / first-order streams — so a caller that needs (y, dPhi/dx, Hm) runs ONE sweep)
+    const int lf = lane_here();
+    const int gf = lf >> 4;
+    const int64_t cf = grp * 8 + (lf & 7);
+    const bool vf = cf < n;
     float uw[MAXO];
 #pragma unroll
-    for (int j = 0; j < MAXO; ++j) uw[j] = (u != nullptr && j < o && valid) ? u[coord * o + j] : 0.f;
+    for (int j = 0; j < MAXO; ++j) uw[j] = (u != nullptr && j < o && vf) ? u[cf * o + j] : 0.f;
     float p0 = 0.f, p1 = 0.f, p2 = 0.f;
     float yv[MAXO] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int rb = 0; rb < NB; ++rb) {
         f32x4 sd;
         if (u != nullptr) {  // WoT rows j >= o are zero padded
-            const float* wo = sm + SM_WO + 16 * rb + 4 * g;
+            const float* wo = sm + SM_WO + 16 * rb + 4 * gf;
             sd = uw[0] * *(const f32x4*)wo + uw[1] * *(const f32x4*)(wo + H) + uw[2] * *(const f32x4*)(wo + 2 * H) +
                  uw[3] * *(const f32x4*)(wo + 3 * H);
         } else {
-            sd = *(const f32x4*)(sm + SM_SEED + 16 * rb + 4 * g);
+            sd = *(const f32x4*)(sm + SM_SEED + 16 * rb + 4 * gf);
         }
         p1 += sd[0] * act[1][rb][0] + sd[1] * act[1][rb][1] + sd[2] * act[1][rb][2] + sd[3] * act[1][rb][3];
         p2 += sd[0] * act[2][rb][0] + sd[1] * act[2][rb][1] + sd[2] * act[2][rb][2] + sd[3] * act[2][rb][3];
@@ -168,7 +181,7 @@ __global__ __launch_bounds__(THREADS, 1) void hess_kernel(const float* __restric
 #pragma unroll
             for (int j = 0; j < MAXO; ++j) {
                 if (j < o) {  // wave-uniform
-                    const f32x4 wj = *(const f32x4*)(sm + SM_WO + j * H + 16 * rb + 4 * g);
+                    const f32x4 wj = *(const f32x4*)(sm + SM_WO + j * H + 16 * rb + 4 * gf);
                     yv[j] += wj[0] * act[0][rb][0] + wj[1] * act[0][rb][1] + wj[2] * act[0][rb][2] +
                              wj[3] * act[0][rb][3];
                 }
@@ -183,26 +196,26 @@ __global__ __launch_bounds__(THREADS, 1) void hess_kernel(const float* __restric
         for (int j = 0; j < MAXO; ++j)
             if (j < o) yv[j] = sum_groups(yv[j]);  // lo: Wout_j . a_L
     }
-    if (valid && g == 0) {
+    if (vf && gf == 0) {
         if (gxo != nullptr) {
             if (hi)
-                gxo[coord * d] = p0;
+                gxo[cf * d] = p0;
             else if (d > 1)
-                gxo[coord * d + 1] = p1;
+                gxo[cf * d + 1] = p1;
         }
         if (yo != nullptr && !hi) {
 #pragma unroll
             for (int j = 0; j < MAXO; ++j)
-                if (j < o) yo[coord * o + j] = yv[j] + sm[SM_BOUT + j];
+                if (j < o) yo[cf * o + j] = yv[j] + sm[SM_BOUT + j];
         }
         if (d == 1) {
-            if (hi) hm[coord] = p1;
+            if (hi) hm[cf] = p1;
         } else if (hi) {
-            hm[coord * 4] = p1;
-            hm[coord * 4 + 3] = p2;
+            hm[cf * 4] = p1;
+            hm[cf * 4 + 3] = p2;
         } else {
-            hm[coord * 4 + 1] = p2;
-            hm[coord * 4 + 2] = p2;
+            hm[cf * 4 + 1] = p2;
+            hm[cf * 4 + 2] = p2;
         }
     }
 }
