@@ -88,6 +88,29 @@ def test_zero_coords_is_a_noop(lib):
     assert lib.siren_forward(ctypes.byref(cfg), None, None, -1, None, None) == _lib.SIREN_EINVAL
 
 
+def test_size_queries_reject_null_cfg(lib):
+    """Every cfg-taking size query in include/siren_amd.h validates cfg before reading it: a NULL cfg is
+    SIREN_EINVAL, never a crash (siren_second_order_batched_ws_floats used to dereference it first)."""
+    from siren_amd import _lib
+    hdr = open(os.path.join(ROOT, 'include', 'siren_amd.h')).read()
+    names = re.findall(r'^int32_t (siren_\w*_floats)\(const siren_cfg\* cfg', hdr, re.M)
+    assert 'siren_second_order_batched_ws_floats' in names and len(names) >= 15
+    for name in names:
+        assert name in _lib._SIGS, name
+        c = _lib._I64(-7)
+        args = []
+        for t in _lib._SIGS[name]:
+            if t is _lib._CFG:
+                args.append(None)
+            elif t is ctypes.POINTER(_lib._I64):
+                args.append(ctypes.byref(c))
+            else:
+                args.append(t(16) if t is _lib._I64 else t(1))
+        assert getattr(lib, name)(*args) == _lib.SIREN_EINVAL, name
+        assert c.value == -7, name   # the count is left untouched on failure
+        assert lib.siren_last_error(), name
+
+
 def test_state_dict_keys_and_seed0_init_match_reference(g1, manifest):
     from siren_amd.modules import SingleBVPNet
     torch.manual_seed(0)
