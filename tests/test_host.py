@@ -88,19 +88,20 @@ def test_zero_coords_is_a_noop(lib):
     assert lib.siren_forward(ctypes.byref(cfg), None, None, -1, None, None) == _lib.SIREN_EINVAL
 
 
-def test_size_queries_reject_null_cfg(lib):
-    """Every cfg-taking size query in include/siren_amd.h validates cfg before reading it: a NULL cfg is
-    SIREN_EINVAL, never a crash (siren_second_order_batched_ws_floats used to dereference it first)."""
+def test_entry_points_reject_null_cfg(lib):
+    """Every cfg-taking entry point in include/siren_amd.h validates cfg before reading it or touching the device:
+    a NULL cfg is SIREN_EINVAL, never a crash (siren_second_order_batched_ws_floats used to dereference it first).
+    No GPU is needed: the call must return before any HIP call."""
     from siren_amd import _lib
     hdr = open(os.path.join(ROOT, 'include', 'siren_amd.h')).read()
-    names = re.findall(r'^int32_t (siren_\w*_floats)\(const siren_cfg\* cfg', hdr, re.M)
-    assert 'siren_second_order_batched_ws_floats' in names and len(names) >= 15
+    names = re.findall(r'^int32_t (siren_\w+)\(const siren_cfg\* cfg', hdr, re.M)
+    assert 'siren_second_order_batched_ws_floats' in names and len(names) >= 30
     for name in names:
-        assert name in _lib._SIGS, name
+        assert name in _lib._SIGS and _lib._SIGS[name][0] is _lib._CFG, name
         c = _lib._I64(-7)
         args = []
         for t in _lib._SIGS[name]:
-            if t is _lib._CFG:
+            if t is _lib._CFG or t is _lib._P:
                 args.append(None)
             elif t is ctypes.POINTER(_lib._I64):
                 args.append(ctypes.byref(c))
