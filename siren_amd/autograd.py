@@ -54,35 +54,60 @@ class JetState:
     laplace_mse recipe); from then on the jet forward is the Hessian node's own sweep (siren_hessian_ex: y, dPhi/dx,
     the Hessian and its kept jets at once) and the node reuses it instead of running a second forward."""
 
+    # The speculative modes are tracked per call site, keyed by the flattened coordinate shape (n, d): a module called
+    # twice per step on batches of different sizes (e.g. a training and a validation batch) whose Hessian / Laplacian
+    # is requested of one call only keeps speculating for that call and not for the other (one shared cell made the
+    # unconsumed call switch the mode off and the consuming call's request switch it on again every step, so each
+    # step paid one wasted sweep). Calls of the SAME shape share a key (the cell then tracks the most recent one).
+    MAX_KEYS = 16  # distinct call shapes tracked per module (the oldest is dropped beyond that)
+
     def __init__(self, mode='auto'):
         self.mode = mode
         self.active = mode is True
-        self.hessian = False
-        self.laplace = False  # likewise for the fused diff_operators.laplace of the value node (W4 jet sweep)
-        self._unused = None   # [bool]: the last speculative sweep's results were not (yet) consumed
+        self._hessian = {}  # key -> a Hessian node was built from this call's jet node
+        self._laplace = {}  # key -> likewise for the fused diff_operators.laplace of the value node (W4 jet sweep)
+        self._unused = {}   # key -> [bool]: the last speculative sweep's results were not (yet) consumed
 
-    def speculate(self):
-        """Called by a forward about to run a speculative sweep: if the previous one was never consumed (the loss
-        stopped asking for the Hessian / Laplacian), switch the modes off — a later request turns them on again.
-        Returns the flag cell for this forward's node (set to False when its results are consumed)."""
-        if self._unused is not None and self._unused[0]:
-            self.hessian = self.laplace = False
-            self._unused = None
+    @staticmethod
+    def key(x):
+        return tuple(x.shape)
+
+    def hessian(self, key):
+        return self._hessian.get(key, False)
+
+    def laplace(self, key):
+        return self._laplace.get(key, False)
+
+    def speculate(self, key):
+        """Called by a forward about to run a speculative sweep for call key: if the previous one of this key was never
+        consumed (the loss stopped asking for the Hessian / Laplacian), switch the key's modes off — a later request
+        turns them on again. Returns the flag cell for this forward's node (set to False when its results are
+        consumed)."""
+        cell = self._unused.pop(key, None)
+        if cell is not None and cell[0]:
+            self._hessian.pop(key, None)
+            self._laplace.pop(key, None)
             return None
-        self._unused = [True]
-        return self._unused
+        cell = [True]
+        self._unused[key] = cell
+        return cell
+
+    def _remember(self, table, key):
+        table[key] = True
+        while len(table) > self.MAX_KEYS:
+            table.pop(next(iter(table)))
 
     def observe_x_gradient_request(self):
         if self.mode == 'auto':
             self.active = True
 
-    def observe_hessian_request(self):
+    def observe_hessian_request(self, key):
         if self.mode in ('auto', True):
-            self.hessian = True
+            self._remember(self._hessian, key)
 
-    def observe_laplace_request(self):
+    def observe_laplace_request(self, key):
         if self.mode in ('auto', True):
-            self.laplace = True
+            self._remember(self._laplace, key)
 
 
 class SirenFunction(torch.autograd.Function):
@@ -92,7 +117,9 @@ class SirenFunction(torch.autograd.Function):
         ctx.tws, ctx.pre_laplace = None, None
         # (jet is None unless a graph is being recorded — modules._fused_apply — so a no_grad evaluation after
         # laplace training, e.g. summaries or create_mesh, keeps the plain forward)
-        ctx.spec = jet.speculate() if (jet is not None and jet.laplace and engine.laplace_supported) else None
+        key = JetState.key(x)
+        ctx.spec = (jet.speculate(key) if (jet is not None and jet.laplace(key) and engine.laplace_supported)
+                    else None)
         if ctx.spec is not None:
             # this module's output went to diff_operators.laplace last time (laplace_mse): the value comes from the
             # W4 jet sweep that laplace() needs anyway, and its Laplacian (+ kept jet stores) wait on this node for
@@ -157,8 +184,9 @@ class SirenJetFunction(torch.autograd.Function):
         ctx.tws = None
         ctx.jet, ctx.pre_hessian = jet, None
         pre = None
-        ctx.spec = (jet.speculate() if (jet is not None and jet.hessian and not split and
-                                        engine.hessian_backward_supported) else None)
+        key = JetState.key(x)
+        ctx.spec = (jet.speculate(key) if (jet is not None and jet.hessian(key) and not split and
+                                           engine.hessian_backward_supported) else None)
         if ctx.spec is not None:
             pre = SirenHessian.forward_sweep(engine, ws, x, None, want_yg=True)
         if pre is not None:
@@ -341,7 +369,7 @@ def _hessian_product(ctx, engine, ws, x, flat, v, u=None):
             ctx.spec[0] = False  # the speculative sweep was used
         jet = getattr(ctx, 'jet', None)
         if u is None and jet is not None:
-            jet.observe_hessian_request()
+            jet.observe_hessian_request(JetState.key(x))
     # elementwise (n, d, d) products: a batched GEMM of n 2x2 matrices runs ~100x slower on the BLAS path
     return (hm * v.unsqueeze(-2)).sum(-1)
 
@@ -590,9 +618,11 @@ def fused_laplace(y, x):
     lap = SirenLaplace.apply(node.engine, node.ws, xs, flat, store, pre)
     if hasattr(node, 'pre_laplace'):
         node.pre_laplace = None
-    if pre is not None and getattr(node, 'spec', None) is not None:
-        node.spec[0] = False  # the speculative sweep was used
+    if getattr(node, 'spec', None) is not None:
+        # a Laplacian was requested of this node: the speculation was right even when its sweep ran without the jet
+        # stores this call needs (recomputed above) — the next forward must not read it as unconsumed
+        node.spec[0] = False
     jet = getattr(node, 'jet', None)
     if jet is not None:
-        jet.observe_laplace_request()
+        jet.observe_laplace_request(JetState.key(xs))
     return lap.view(*y.shape[:-1], 1)

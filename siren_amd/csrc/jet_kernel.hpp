@@ -42,9 +42,6 @@
 #include "siren_common.h"
 #include "siren_params.h"
 
-#ifndef SIREN_PROBE
-#define SIREN_PROBE 0
-#endif
 
 
 namespace siren {
@@ -212,12 +209,6 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
 #pragma unroll
             for (int rb = 0; rb < NB; ++rb) {
                 const f32x4 z = acc[rb] + val * *(const f32x4*)(bl + 16 * rb);
-#if SIREN_PROBE >= 1
-                if (true) {
-                    zs.next_store(z);
-                    act[rb] = z;
-                } else
-#endif
                 if constexpr (QG) {
                     f32x4 kz;
                     act[rb] = jet_sin_q(z, w, val, kb, kg, qc[0], qc[1], js == 3, kz);
@@ -227,9 +218,7 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
                     act[rb] = jet_sin<MIX>(z, w, val, kb, kg);
                 }
             }
-#if SIREN_PROBE < 2
             jstore_tile(abuf + (int64_t)l * lstride + toff, act);
-#endif
             if (PHASE == JET_FWD && l == lh) {
                 // outputs per stream (the W4 forward's): y_j (value), sum_j dy_j/dx_k (tangent k), sum_j Lap y_j
                 float tot = 0.f;
@@ -304,17 +293,11 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
             {
 #pragma unroll
                 for (int rb = 0; rb < NB; ++rb) {
-#if SIREN_PROBE >= 1  // timing probe (tools/probe_build.sh): no epilogue arithmetic
-                    act[rb] = acc[rb] + zl.next_load();
-#else
                     act[rb] = QG ? jet_sin_adjoint_q(acc[rb], zl.next_load(), wl, val, m12, qc[0], qc[1])
                                  : jet_sin_adjoint<MIX>(acc[rb], zl.next_load(), wl, val, m12, s1);
-#endif
                 }
             }
-#if SIREN_PROBE < 2
             jstore_tile(dbuf + (int64_t)lm * lstride + toff, act);
-#endif
         }
     }
 

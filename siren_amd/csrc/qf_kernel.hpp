@@ -28,17 +28,7 @@
 
 namespace siren {
 
-#ifndef QF_PROBE
-#define QF_PROBE 0  // timing probes (tools/qf_probe.sh; numerically meaningless): 1 no epilogue arithmetic, 2 also no
-                    // kept loads, 3 also no tile stores
-#endif
-#ifndef QF_PREFETCH_N
-#define QF_PREFETCH_N 3
-#endif
-constexpr int QF_PREFETCH = QF_PREFETCH_N;
-#ifndef QF_STAGGER
-#define QF_STAGGER 0  // first-round start delay per CU quarter, in s_sleep(127) units (~3.4 us each)
-#endif  // kept blocks loaded ahead of the epilogue element that consumes them
+constexpr int QF_PREFETCH = 3;  // kept blocks loaded ahead of the epilogue element that consumes them
 
 // this lane's three kept streams of block rb (tiles 0..2 of hess_kept_off), one 16 B global load each
 struct QfKept {
@@ -47,11 +37,6 @@ struct QfKept {
 __device__ __forceinline__ QfKept qf_load(const float* p) {
     typedef const __attribute__((address_space(1))) f32x4 gf32x4;
     QfKept r;
-#if QF_PROBE >= 2 || defined(QF_NOLOAD)
-    r.k[0] = r.k[1] = r.k[2] = f32x4{0.5f, 0.25f, 0.125f, 1.f};
-    asm volatile("" : "+v"(r.k[0]), "+v"(r.k[1]), "+v"(r.k[2]));
-    return r;
-#endif
     r.k[0] = *(gf32x4*)p;
     r.k[1] = *(gf32x4*)(p + 256);
     r.k[2] = *(gf32x4*)(p + 512);
@@ -86,13 +71,6 @@ struct QfCoef {
 // -> a-jet (aa, ab) and z-jet cotangent (za, zb) of this lane's two streams
 __device__ __forceinline__ void qf_elem(float k0, float k1, float k2, float ua, float ub, float wl, float wl2,
                                         const QfCoef& q, bool hi, float& aa, float& ab, float& za, float& zb) {
-#if QF_PROBE >= 1
-    aa = k0 + ua;
-    ab = k1 + ub;
-    za = k2 * ua;
-    zb = k0 * ub;
-    return;
-#endif
     const float p0 = row_ror8(k0), p1 = row_ror8(k1);
     const float zp = __builtin_fmaf(q.e1, k1, q.e2 * k2);
     const float z3 = zp + row_ror8(zp);
@@ -158,12 +136,6 @@ __global__ __launch_bounds__(THREADS, 1) void qf_rev_kernel(const float* __restr
         q.cb = hi ? q.q12 : 2.f * q.q22;
     }
     __syncthreads();
-    if (QF_STAGGER > 0 && blockIdx.x < 256) {
-        // de-phase the CUs: one workgroup per CU runs the tiles back to back, so without an offset every CU reaches its
-        // epilogues (the kept loads and tile stores) at the same time and the HBM bursts queue behind each other
-        const int k = (blockIdx.x >> 3) & 3;
-        for (int i = 0; i < k * QF_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-    }
     // the ring starts at the first reverse slice (the stream's transposed layers)
     int s = lh * NB;
     ring_issue(stream, ring, s, nslices, wave, lane);
@@ -222,12 +194,10 @@ __global__ __launch_bounds__(THREADS, 1) void qf_rev_kernel(const float* __restr
                 act[0][rb][r] = za;
                 act[1][rb][r] = zb;
             }
-#if QF_PROBE < 3 && !defined(QF_NOSTORE)
             if constexpr (!SEED) qf_store_block(ap, aa);  // a_L's value / d/dx_1 streams feed no gradient
             qf_store_block(ap + H * 16, ab);
             qf_store_block(dp, act[0][rb]);
             qf_store_block(dp + H * 16, act[1][rb]);
-#endif
             ap += 256;
             dp += 256;
             asm volatile("" : "+v"(ap), "+v"(dp));
@@ -250,19 +220,8 @@ __global__ __launch_bounds__(THREADS, 1) void qf_rev_kernel(const float* __restr
         }
     };
 
-#ifdef QF_PROF
-    // probe (numerically meaningless gx): s_memtime after each phase, wave 0 of the first 256 workgroups, into gx as
-    // u64 [block][event]: 0 start, 1 seed epilogue, then per reverse GEMM (end of GEMM, end of epilogue)
-    unsigned long long qst[2 + 2 * 8];
-    int qe = 0;
-    qst[qe++] = __builtin_amdgcn_s_memtime();
-#define QF_STAMP() qst[qe++] = __builtin_amdgcn_s_memtime()
-#else
-#define QF_STAMP()
-#endif
     // seed at layer L from the kept z_L jet (no forward sweep), then the L reverse GEMMs
     epilogue(lh, std::true_type{});
-    QF_STAMP();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // slice s landed (and the seed's stores): publish it
     __builtin_amdgcn_s_barrier();
 #pragma unroll 1
@@ -283,17 +242,8 @@ __global__ __launch_bounds__(THREADS, 1) void qf_rev_kernel(const float* __restr
                 ++s;
             }
         }
-        QF_STAMP();
         epilogue(2 * lh - p - 1, std::false_type{});
-        QF_STAMP();
     }
-#ifdef QF_PROF
-    if (wave == 0 && lane == 0 && blockIdx.x < 256) {
-        unsigned long long* out = (unsigned long long*)gx + blockIdx.x * 16;
-        for (int e = 0; e < qe && e < 16; ++e) out[e] = qst[e];
-    }
-    return;
-#endif
 
     // ---- gx = W0^T zb_0,value (tile 0, lo lanes) ---------------------------------------------------------------
 #pragma unroll

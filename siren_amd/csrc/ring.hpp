@@ -9,9 +9,6 @@ namespace siren {
 // ------------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void ring_issue(const float* __restrict__ stream, float* ring, int s, int nslices,
                                            int wave, int lane) {
-#if defined(SIREN_PROBE) && SIREN_PROBE >= 3  // timing probe (tools/probe_build.sh 3): no weight-slice traffic
-    if (s >= 2) return;
-#endif
     if (s < nslices) {
         const int wu = __builtin_amdgcn_readfirstlane(wave);
         const char* src = (const char*)(stream + (int64_t)s * SLICE + wu * 1024);

@@ -232,7 +232,8 @@ int32_t siren_workspace_floats(const siren_cfg* cfg, int64_t* count) {
 int32_t siren_pack(const siren_cfg* cfg, const float* params, float* ws, void* stream) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (params == nullptr || ws == nullptr) return fail(SIREN_EINVAL, "params/ws is NULL");
-    if (layered(cfg)) {  // the parameters as they are + W_l^T; the rest of ws is the layered path's chunk scratch
+    if (layered(cfg)) {  // ws = [parameters as they are][W_l^T] and nothing else (immutable since ABI 5: the chunk
+                          // scratch is every layered entry point's caller-owned tws, layered_ws_floats)
         siren::layered_pack(siren::LayeredPlan(cfg->d_in, cfg->hidden, cfg->n_hidden, cfg->d_out, -1), params, ws,
                             (hipStream_t)stream);
         return hip_status("siren_pack");

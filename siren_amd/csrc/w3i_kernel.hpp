@@ -29,11 +29,6 @@
 //     pair, counted lgkmcnt waits: w1_kernel's slice machinery (ring_issue4, lds_read4, lgkm_wait).
 #pragma once
 #include "w1_kernel.hpp"
-// W3I_EXP: timing probes for tools/variant_build.sh (results numerically meaningless when set): 1 no reloads, 2 no tile
-// stores, 4 no spill stores, 16 no per-slice scheduling barrier, 32 mid-slice waits that do not count the epilogue ops
-#ifndef W3I_EXP
-#define W3I_EXP 0
-#endif
 // The epilogue block runs as one VALU cluster after operand pair W3I_EPI_PAIR (>= 4: after the mid-slice wait its
 // reloads land at; A/B pairs 4 / 5 / 6 / 7 / slice end interleaved by hipcc: pair 5 -1.4 % on w3_theta, pair 7 the
 // same there and -1.4 % more on the sdf step, profiles/r03x_epilogue_placement.log; cf. w1_kernel.hpp w1_epi_pair)
@@ -76,19 +71,17 @@ constexpr bool w3_reloads() {
 // barrier): the next mid-slice wait leaves them outstanding instead of waiting for them (s_waitcnt counts stores too)
 template <int KIND, bool THETA, bool KEPT>
 constexpr int w3_nstores() {
-    constexpr int T = (W3I_EXP & 2) ? 0 : 1, SP = (W3I_EXP & 4) ? 0 : 1;
-    return KIND == W3E_FIRST ? SP * (KEPT ? 1 : 2) + (THETA ? T * (KEPT ? 1 : 2) : 0)
-         : KIND == W3E_FWD   ? (KEPT ? SP + (THETA ? T : 0) : 2 * SP + (THETA ? 2 * T : 0))
-         : KIND == W3E_SEED  ? (THETA ? T * (KEPT ? 3 : 4) : 0)
-                             : (THETA ? 2 * T : 0);
+    return KIND == W3E_FIRST ? (KEPT ? 1 : 2) + (THETA ? (KEPT ? 1 : 2) : 0)
+         : KIND == W3E_FWD   ? (KEPT ? 1 + (THETA ? 1 : 0) : 2 + (THETA ? 2 : 0))
+         : KIND == W3E_SEED  ? (THETA ? (KEPT ? 3 : 4) : 0)
+                             : (THETA ? 2 : 0);
 }
 
 // vector-memory loads of an epilogue's reloads (w3_reload_issue): REV reloads (z, zdot) — or (cos, zdot, a) from the
 // stored forward when KEPT, a being 4 dword loads from the tile layout —, a KEPT FWD cos, a KEPT SEED (cos, a)
 template <int KIND, bool KEPT>
 constexpr int w3_nreloads() {
-    return (W3I_EXP & 1) ? 0
-         : KIND == W3E_REV ? (KEPT ? 6 : 2)
+    return KIND == W3E_REV ? (KEPT ? 6 : 2)
          : (KEPT && KIND == W3E_FWD) ? 1 : ((KEPT && KIND == W3E_SEED) ? 5 : 0);
 }
 template <int E, int LH, bool THETA, bool KEPT>
@@ -140,7 +133,6 @@ __device__ __forceinline__ const char* w3_at(const char* base, int64_t off) {
 // store reads them late; gfx940+ store-data hazard). hipcc inserts those for its own stores, not for inline asm — without
 // it the coordinates of lanes 12..15 of every 16-lane row came back wrong once the allocator reused a stored register.
 __device__ __forceinline__ void w3_store16(const char* base, unsigned voff, const f32x4& v) {
-    if (W3I_EXP & 4) return;
     asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" ::"v"(voff), "v"(v), "s"(base));
 }
 // A block of the wgrad tile layout (element (neuron 16 rb + 4 g + r, coordinate c) at rb 256 + neuron 16 + c, what
@@ -196,7 +188,7 @@ template <int E, int LH, bool THETA, bool KEPT>
 __device__ __forceinline__ void w3_reload_issue(W3iState<LH>& st, const W3iCtx& cx) {
     constexpr int G = E / NB, B = E % NB;
     constexpr int KIND = w3_epi_kind<G, LH>();
-    if constexpr (G < 2 * LH && w3_reloads<KIND, KEPT>() && !(W3I_EXP & 1)) {
+    if constexpr (G < 2 * LH && w3_reloads<KIND, KEPT>()) {
         constexpr int M = KIND == W3E_REV ? 2 * LH - G : G;  // the layer whose forward values are reloaded
         if constexpr (KEPT)
             w3_load16(st.pc[E % 3], w3_at(cx.kc, (int64_t)(M * NB + B) * 1024), cx.vl);
@@ -229,7 +221,7 @@ template <int E, int LH, bool THETA, bool KEPT>
 __device__ __forceinline__ void w3_tile_flush(W3iState<LH>& st, const W3iCtx& cx) {
     constexpr int G = E / NB, B = E % NB;
     constexpr int KIND = w3_epi_kind<G, LH>();
-    if constexpr (THETA && G < 2 * LH && !(W3I_EXP & 2)) {
+    if constexpr (THETA && G < 2 * LH) {
         constexpr int NT = w3_ntiles<KIND, KEPT>();
 #pragma unroll
         for (int i = 0; i < NT; ++i) asm volatile("" : "+v"(st.tq[i]));  // landed
@@ -287,7 +279,7 @@ __device__ __forceinline__ void w3i_epilogue(W3iState<LH>& st, const W3iCtx& cx,
     auto spill = [&](int l, int q, const f32x4& val) { w3_store16(w3_at(cx.wsp, w3_spill_off(l, q, b)), cx.vl, val); };
     int nt = 0;  // tile blocks staged so far (w3_tile_flush stores them in this order)
     auto tile = [&](const f32x4& val) {
-        if (!(W3I_EXP & 2)) w3_stage(st.tq[nt], val, cx.tw, cx.tr);
+        w3_stage(st.tq[nt], val, cx.tw, cx.tr);
         ++nt;
     };
     if constexpr (KIND == W3E_FIRST) {
@@ -403,9 +395,8 @@ __device__ __forceinline__ void w3i_slice(W3iState<LH>& st, const W3iCtx& cx) {
             // slice S+1 (issued at the mid-slice of S-2, after epilogue S+1's reloads) must have landed; younger and
             // allowed outstanding: epilogue S-1's stores, epilogue S+2's reloads and slice S+2's ring loads (both
             // issued at the mid-slice of S-1), epilogue S's stores
-            constexpr int ALLOW = (W3I_EXP & 32) ? (S + 2 < NS ? 4 : 0)
-                                                 : w3_nvmem_st<S - 1, LH, THETA, KEPT>() + w3_nvmem_rl<S + 2, LH, KEPT>() +
-                                                       (S + 2 < NS ? 4 : 0) + w3_nvmem_st<S, LH, THETA, KEPT>();
+            constexpr int ALLOW = w3_nvmem_st<S - 1, LH, THETA, KEPT>() + w3_nvmem_rl<S + 2, LH, KEPT>() +
+                                  (S + 2 < NS ? 4 : 0) + w3_nvmem_st<S, LH, THETA, KEPT>();
             static_assert(ALLOW < 64, "vmcnt is 6 bits");
             asm volatile("s_waitcnt vmcnt(%0)" ::"i"(ALLOW) : "memory");
             w3_reload_landed<S + 1, LH, KEPT>(st);
@@ -465,7 +456,7 @@ __device__ __forceinline__ void w3i_slice(W3iState<LH>& st, const W3iCtx& cx) {
 
     // one scheduling region per slice: the epilogue interleaves with this slice's MFMAs, but hipcc may not hoist later
     // blocks' epilogue arithmetic (whose inputs are all ready when the GEMM starts) into it
-    if (!(W3I_EXP & 16)) __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 template <int G, int LH, bool THETA, bool KEPT>

@@ -445,8 +445,8 @@ class SirenEngine:
         u / gy (B, n, d_out) nullable. Returns (gx (B, n, d_in), gparams (B, P) | None[, ydot (B, n, d_out)])."""
         self._require()
         if not self.second_order_supported:
-            raise _lib.SirenUnsupported('siren_second_order covers d_out <= 4, linear output, hidden 256 with 1..3 '
-                                        'hidden layers or hidden 512')
+            raise _lib.SirenUnsupported('siren_second_order covers d_out <= 4, linear output, hidden 256 with 1..5 '
+                                        'hidden layers (nonzero omegas beyond 3) or hidden 512')
         x = self._check_xb(x)
         B, n, d, o = x.shape[0], x.shape[1], self.cfg.d_in, self.cfg.d_out
         v = self._check_batched_like('v', v, (B, n, d), x.device)
@@ -616,8 +616,8 @@ class SirenEngine:
         ydot = J v (n, d_out) = dF/du when want_ydot."""
         self._require()
         if not self.second_order_supported:
-            raise _lib.SirenUnsupported('siren_second_order covers d_out <= 4, linear output, hidden 256 with 1..3 '
-                                        'hidden layers or hidden 512')
+            raise _lib.SirenUnsupported('siren_second_order covers d_out <= 4, linear output, hidden 256 with 1..5 '
+                                        'hidden layers (nonzero omegas beyond 3) or hidden 512')
         x = self._check_x(x)
         n, o = x.shape[0], self.cfg.d_out
         v = v.contiguous()

@@ -61,6 +61,33 @@ def cuda():
     return torch.device('cuda:0')
 
 
+def torch_path_functions():
+    """Every public function of siren_amd._torch_path (the device-torch recompute), enumerated from the module so a
+    new fallback is covered without editing the guard."""
+    import inspect
+    from siren_amd import _torch_path
+    return sorted(name for name, f in vars(_torch_path).items()
+                  if not name.startswith('_') and inspect.isfunction(f) and f.__module__ == _torch_path.__name__)
+
+
+def forbid_torch_path(monkeypatch, allow=()):
+    """Make every device-torch recompute raise: a test that passes under it ran its derivatives on the HIP kernels."""
+    from siren_amd import _torch_path
+    for name in torch_path_functions():
+        if name in allow:
+            continue
+
+        def boom(*a, _n=name, **k):
+            raise AssertionError('device-torch recompute %s must not run' % _n)
+        monkeypatch.setattr(_torch_path, name, boom)
+
+
+@pytest.fixture
+def no_torch_path(monkeypatch):
+    """Fixture form of forbid_torch_path (every _torch_path function forbidden for the whole test)."""
+    forbid_torch_path(monkeypatch)
+
+
 def weights_of(fx):
     """Fixture weights as a flat fp32 vector in state_dict order, plus the (W, b) list."""
     from oracle import siren_oracle as O

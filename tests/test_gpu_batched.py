@@ -10,6 +10,7 @@ import pytest
 import torch
 
 from oracle import siren_oracle as O
+from conftest import forbid_torch_path
 
 pytestmark = pytest.mark.gpu
 
@@ -140,15 +141,6 @@ def _poison_pack(monkeypatch):
     monkeypatch.setattr(E.SirenEngine, 'pack_batched', pack_batched)
 
 
-def _forbid_torch_path(monkeypatch):
-    from siren_amd import _torch_path
-
-    def boom(*a, **k):
-        raise AssertionError('device-torch recompute used on a kernel-covered path')
-    for name in ('vjp_params', 'jacobian_vjp', 'vjp_vjp', 'hvp_vjp', 'laplace_vjp', 'forward', 'laplacian'):
-        monkeypatch.setattr(_torch_path, name, boom)
-
-
 @pytest.mark.parametrize('lname', ['gradients_mse', 'laplace_mse'])
 def test_hypo_second_and_third_order_vs_reference(cuda, g7, g11, monkeypatch, lname):
     """gradients_mse (second order) and laplace_mse through the reference's divergence(gradient()) (third order) on a
@@ -158,7 +150,7 @@ def test_hypo_second_and_third_order_vs_reference(cuda, g7, g11, monkeypatch, ln
     from siren_amd.modules import SingleBVPNet
     from siren_amd import loss_functions as LF
     _poison_pack(monkeypatch)
-    _forbid_torch_path(monkeypatch)
+    forbid_torch_path(monkeypatch)
     m = SingleBVPNet(in_features=2, out_features=1, verbose=False).to(cuda)
     params = OrderedDict((k[2:], torch.tensor(v, device=cuda, requires_grad=True))
                          for k, v in g7.items() if k.startswith('p_'))

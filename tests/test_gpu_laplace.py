@@ -7,7 +7,7 @@ import pytest
 import torch
 
 from oracle import siren_oracle as O
-from conftest import weights_of
+from conftest import forbid_torch_path, weights_of
 
 pytestmark = pytest.mark.gpu
 
@@ -164,14 +164,10 @@ def test_w4s_deterministic_and_linear(cuda):
 
 def test_laplace_mse_step_runs_on_hip_kernels(cuda, g1, monkeypatch):
     """laplace_mse training through the drop-in API: forward = W4, backward = W4s; no device-torch recompute."""
-    from siren_amd import _torch_path
     from siren_amd import loss_functions as LF
     from siren_amd.modules import SingleBVPNet
 
-    def boom(*a, **k):
-        raise AssertionError('torch recompute path used')
-    for name in ('laplace_vjp', 'hvp_vjp', 'jacobian_vjp', 'vjp_params'):
-        monkeypatch.setattr(_torch_path, name, boom)
+    forbid_torch_path(monkeypatch)
     m = SingleBVPNet(verbose=False).to(cuda)
     m.load_state_dict({k[2:]: torch.tensor(v) for k, v in g1.items() if k.startswith('w_')})
     out = m({'coords': to_dev(g1['coords'], cuda)})

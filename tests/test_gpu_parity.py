@@ -13,7 +13,7 @@ import pytest
 import torch
 
 from oracle import siren_oracle as O
-from conftest import weights_of
+from conftest import forbid_torch_path, weights_of
 
 pytestmark = pytest.mark.gpu
 
@@ -288,13 +288,13 @@ def test_training_theta_grads_vs_reference(cuda, g1, loss):
 def test_sdf_losses_vs_reference(cuda, g3, manifest, jet, monkeypatch):
     """sdf training (value + gradient terms). With jet=True the value and gradient cotangents meet in ONE
     SirenJetFunction backward: the seeded W3 kernel, no first-order W2 pass and no torch recompute."""
-    from siren_amd import loss_functions as Lf, _torch_path
+    from siren_amd import loss_functions as Lf
     from siren_amd.engine import SirenEngine
+    forbid_torch_path(monkeypatch)
     if jet is True:
         def boom(*a, **k):
-            raise AssertionError('separate first-order pass / torch fallback used on the seeded W3 path')
+            raise AssertionError('separate first-order pass used on the seeded W3 path')
         monkeypatch.setattr(SirenEngine, 'backward_params', boom)
-        monkeypatch.setattr(_torch_path, 'jacobian_vjp', boom)
     m = load_model(g3, cuda, in_features=3, jet=jet)
     out = m({'coords': to_dev(g3['coords'], cuda)})
     terms = Lf.sdf(out, {'sdf': to_dev(g3['gt_sdf'], cuda), 'normals': to_dev(g3['gt_normals'], cuda)})
@@ -429,11 +429,8 @@ def test_w3_trained_regime(cuda, g2, g1):
 @pytest.mark.parametrize('jet', [True, False])
 def test_second_order_losses_use_hip_kernel(cuda, g1, jet, monkeypatch):
     """gradients_mse training runs the W3 kernel, not the device torch recompute."""
-    from siren_amd import _torch_path, loss_functions as Lf
-    def boom(*a, **k):
-        raise AssertionError('torch fallback used on a first/second-order path')
-    monkeypatch.setattr(_torch_path, 'jacobian_vjp', boom)
-    monkeypatch.setattr(_torch_path, 'vjp_vjp', boom)
+    from siren_amd import loss_functions as Lf
+    forbid_torch_path(monkeypatch)
     m = load_model(g1, cuda, jet=jet)
     out = m({'coords': to_dev(g1['coords'], cuda)})
     losses = Lf.gradients_mse(out, {'gradients': to_dev(g1['gt_gradients'], cuda)})

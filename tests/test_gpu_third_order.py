@@ -13,6 +13,7 @@ import pytest
 import torch
 
 from oracle import siren_oracle as O
+from conftest import forbid_torch_path
 
 pytestmark = pytest.mark.gpu
 
@@ -101,15 +102,6 @@ def test_hvp_backward_n0_and_determinism(cuda):
     assert np.max(np.abs(a[0][idx].cpu().numpy() - rgx)) <= 1e-4 * max(1e-6, np.max(np.abs(rgx)))
 
 
-def _forbid_torch_path(monkeypatch):
-    from siren_amd import _torch_path
-
-    def boom(*a, **k):
-        raise AssertionError('device-torch recompute used')
-    for name in ('vjp_params', 'jacobian_vjp', 'vjp_vjp', 'hvp_vjp', 'laplace_vjp', 'laplacian', 'forward'):
-        monkeypatch.setattr(_torch_path, name, boom)
-
-
 def reference_laplace(y, x):
     """The reference's op sequence (diff_operators.py:27-43): gradient with create_graph, then one create_graph
     autograd.grad per input dimension — NOT siren_amd.diff_operators.laplace's fused interception."""
@@ -128,7 +120,7 @@ def test_reference_recipe_laplace_mse_trains_on_kernels(cuda, g1, name, request,
     from siren_amd.modules import SingleBVPNet
     fx = request.getfixturevalue(name)
     tag = name.upper()
-    _forbid_torch_path(monkeypatch)
+    forbid_torch_path(monkeypatch)
     m = SingleBVPNet(verbose=False).to(cuda)
     m.load_state_dict({k[2:]: torch.tensor(v) for k, v in fx.items() if k.startswith('w_')})
     gt = to_dev(g1['gt_laplace'], cuda)
@@ -207,7 +199,7 @@ def test_reference_recipe_laplace_mse_hidden512_on_kernels(cuda, monkeypatch):
     forbidden: W1 / W3 (two-stream jet) / third-order (mixed jet) kernels at hidden 512, theta-grads vs fp64
     autograd of the same loss (oracle restatement, modules.py + diff_operators.py op sequence)."""
     from siren_amd.modules import SingleBVPNet
-    _forbid_torch_path(monkeypatch)
+    forbid_torch_path(monkeypatch)
     torch.manual_seed(0)
     m = SingleBVPNet(hidden_features=512, verbose=False).to(cuda)
     coords = (torch.rand(1, 700, 2, generator=torch.Generator().manual_seed(5)) * 2 - 1)
@@ -345,7 +337,7 @@ def test_reference_recipe_one_forward_sweep(cuda, g1, monkeypatch):
     backward — and the step still matches the reference's fp64 laplace_mse theta-grads (G1) and its Laplacian."""
     from siren_amd.engine import SirenEngine
     from siren_amd.modules import SingleBVPNet
-    _forbid_torch_path(monkeypatch)
+    forbid_torch_path(monkeypatch)
     calls = {'w1': 0, 'hess': 0, 'hess_yg': 0, 'bwd_kept': 0}
     orig_fg, orig_fgs, orig_h, orig_b = (SirenEngine.forward_grad, SirenEngine.forward_grad_store,
                                          SirenEngine.hessian, SirenEngine.hessian_backward)
@@ -400,6 +392,56 @@ def test_reference_recipe_one_forward_sweep(cuda, g1, monkeypatch):
         (g ** 2).mean().backward()
         if step >= 1:
             assert calls['hess_yg'] == 0 and calls['w1'] == 1, (step, calls)
+
+
+def test_speculation_is_tracked_per_call(cuda, g1, monkeypatch):
+    """A module called twice per step (here a training batch whose Laplacian is taken through the reference recipe,
+    and a smaller batch with a first-order loss) keeps the Hessian-node speculation for the consuming call only
+    (JetState keys its cells by the call's coordinate shape): from the third step on, the training call runs one
+    Hessian sweep (y, dPhi/dx, Hm at once), the other call one W1 launch, and no sweep is wasted; the training call's
+    theta-grads still match the reference's fp64 laplace_mse gradients (G1)."""
+    from siren_amd import diff_operators as D
+    from siren_amd.engine import SirenEngine
+    from siren_amd.modules import SingleBVPNet
+    forbid_torch_path(monkeypatch)
+    calls = {'w1': 0, 'hess_yg': 0}
+    orig_fg, orig_fgs, orig_h = SirenEngine.forward_grad, SirenEngine.forward_grad_store, SirenEngine.hessian
+
+    def fg(self, *a, **k):
+        calls['w1'] += 1
+        return orig_fg(self, *a, **k)
+
+    def fgs(self, *a, **k):
+        calls['w1'] += 1
+        return orig_fgs(self, *a, **k)
+
+    def hess(self, *a, **k):
+        calls['hess_yg'] += bool(k.get('want_yg'))
+        return orig_h(self, *a, **k)
+    monkeypatch.setattr(SirenEngine, 'forward_grad', fg)
+    monkeypatch.setattr(SirenEngine, 'forward_grad_store', fgs)
+    monkeypatch.setattr(SirenEngine, 'hessian', hess)
+    m = SingleBVPNet(verbose=False).to(cuda)
+    m.load_state_dict({k[2:]: torch.tensor(v) for k, v in g1.items() if k.startswith('w_')})
+    gt = to_dev(g1['gt_laplace'], cuda)
+    other = (torch.rand(1, 300, 2, generator=torch.Generator().manual_seed(5)) * 2 - 1).to(cuda)
+    for step in range(4):
+        for k in calls:
+            calls[k] = 0
+        m.zero_grad()
+        out = m({'coords': to_dev(g1['coords'], cuda)})
+        lap = reference_laplace(out['model_out'], out['model_in'])
+        loss = torch.mean((lap - gt) ** 2)
+        loss.backward()
+        grads = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+        m.zero_grad()
+        o2 = m({'coords': other})
+        (D.gradient(o2['model_out'], o2['model_in']) ** 2).mean().backward()
+        if step >= 2:
+            assert calls == {'w1': 1, 'hess_yg': 1}, (step, calls)
+            for k, gk in grads.items():
+                ref = g1['G1_laplace_mse_grad_' + k]
+                assert np.max(np.abs(gk.cpu().numpy() - ref)) <= 1e-4 * np.max(np.abs(ref)) + 1e-12, k
 
 
 @pytest.mark.parametrize('n,d,L,o,weighted', [(1, 2, 3, 1, False), (1000, 2, 3, 1, False), (333, 1, 2, 3, True),

@@ -11,7 +11,7 @@ import pytest
 import torch
 
 from oracle import siren_oracle as O
-from conftest import pml_case, pml_ref_grads
+from conftest import forbid_torch_path, pml_case, pml_ref_grads
 
 pytestmark = pytest.mark.gpu
 
@@ -90,21 +90,10 @@ def _model(case, cuda, d, o, jet='auto'):
     return m
 
 
-def _no_second_order_fallback(monkeypatch):
-    from siren_amd import _torch_path
-
-    def boom(*a, **k):
-        raise AssertionError('device-torch recompute used on a second- or third-order path')
-    # hvp_vjp: the PML losses' training backward through the second jacobian() (a third derivative) runs on the
-    # mixed-jet kernel (siren_hvp_backward)
-    for name in ('vjp_vjp', 'jacobian_vjp', 'hvp_vjp', 'vjp_params', 'laplace_vjp'):
-        monkeypatch.setattr(_torch_path, name, boom)
-
-
 def test_jacobian_hessian_vector_output_vs_reference(cuda, g6, monkeypatch):
     """d_out = 2 (a complex Helmholtz field): jacobian through W1 vjp nodes, hessian through the W3 kernel."""
     from siren_amd import diff_operators as D
-    _no_second_order_fallback(monkeypatch)
+    forbid_torch_path(monkeypatch)
     case = pml_case(g6, 'H')
     m = _model(case, cuda, 2, 2)
     out = m({'coords': to_dev(case[0], cuda)})
@@ -123,7 +112,7 @@ def test_pml_training_theta_grads_vs_reference(cuda, g6, manifest, monkeypatch, 
     """helmholtz_pml / wave_pml training step: loss terms and theta-grads vs the reference's fp64 golden; the
     second-order sweeps run on W3 and the third-order ones on the mixed jet (every torch recompute is forbidden)."""
     from siren_amd import loss_functions as LF
-    _no_second_order_fallback(monkeypatch)
+    forbid_torch_path(monkeypatch)
     case = pml_case(g6, tag)
     coords, gt = case[0], case[1]
     m = _model(case, cuda, d, o, jet=jet)

@@ -7,7 +7,7 @@ import pytest
 import torch
 
 from oracle import siren_oracle as O
-from conftest import weights_of
+from conftest import forbid_torch_path, weights_of
 
 pytestmark = pytest.mark.gpu
 
@@ -212,15 +212,6 @@ def test_wide_second_order_vs_fp64(cuda, n, d, L, o, weighted, seeded):
     assert np.max(np.abs(ydot.cpu().numpy() - rjv)) <= tol_rel(rjv)
 
 
-def _no_torch_second_order(monkeypatch):
-    from siren_amd import _torch_path
-
-    def boom(*a, **k):
-        raise AssertionError('device-torch recompute used on a second-order path')
-    for name in ('vjp_vjp', 'jacobian_vjp', 'vjp_params'):
-        monkeypatch.setattr(_torch_path, name, boom)
-
-
 @pytest.mark.parametrize('case', ['A', 'B'])
 def test_g9_second_order_losses_at_hidden512_vs_reference(cuda, g9, manifest, case, monkeypatch):
     """gradients_mse (d2) and sdf (d3) training at hidden_features=512 through the drop-in API against the
@@ -228,7 +219,7 @@ def test_g9_second_order_losses_at_hidden512_vs_reference(cuda, g9, manifest, ca
     second runs with jet mode switched on)."""
     from siren_amd.modules import SingleBVPNet
     from siren_amd import loss_functions as LF
-    _no_torch_second_order(monkeypatch)
+    forbid_torch_path(monkeypatch)
     d = 2 if case == 'A' else 3
     m = SingleBVPNet(in_features=d, hidden_features=512, verbose=False).to(cuda)
     m.load_state_dict({k[len(case) + 3:]: torch.tensor(v) for k, v in g9.items() if k.startswith(case + '_w_')})
