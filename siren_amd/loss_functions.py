@@ -1,4 +1,4 @@
-"""The loss consumers of the hot path (loss_functions.py:8-12, 80-109, 214-238), restated for the harness.
+"""The loss consumers of the hot path (loss_functions.py:8-56, 80-109, 214-238), restated for the harness.
 
 The reference's own loss_functions module runs unchanged against siren_amd models; these restatements exist so
 the tests, smoke() and bench.py can run on the GPU box, where the reference is absent.
@@ -14,6 +14,39 @@ def image_mse(mask, model_output, gt):
     return {'img_loss': (err if mask is None else mask * err).mean()}
 
 
+def image_l1(mask, model_output, gt):
+    err = torch.abs(model_output['model_out'] - gt['img'])
+    return {'img_loss': (err if mask is None else mask * err).mean()}
+
+
+def _rand_coords_like(model_in):
+    """Uniform coordinates in [-1, 1) for the inpainting priors: (B, N // 2, d), drawn like the reference's
+    2 * (torch.rand(...).cuda() - 0.5) (loss_functions.py:23-25, 40-42) — from the global CPU generator, then moved
+    to the model's device — so a seeded run draws the reference's exact points (the arithmetic is exact in fp32)."""
+    b, n, d = model_in.shape
+    return (2 * (torch.rand((b, n // 2, d)) - 0.5)).to(device=model_in.device)
+
+
+def image_mse_TV_prior(mask, k1, model, model_output, gt):
+    """image_mse + k1 * mean |d model / dx| at N/2 random points (loss_functions.py:22-36): the prior is a second
+    model call per step, and its gradient node's backward (the second-order W3 sweep) trains through it."""
+    rand_output = model({'coords': _rand_coords_like(model_output['model_in'])})
+    err = (model_output['model_out'] - gt['img']) ** 2
+    prior = torch.abs(diff_operators.gradient(rand_output['model_out'], rand_output['model_in'])).mean()
+    return {'img_loss': (err if mask is None else mask * err).mean(), 'prior_loss': k1 * prior}
+
+
+def image_mse_FH_prior(mask, k1, model, model_output, gt):
+    """image_mse + k1 * mean |Hessian|_F at N/2 random points (loss_functions.py:39-56): diff_operators.hessian of the
+    second model call, so the prior trains through a third derivative (the shared Hessian node's backward)."""
+    rand_output = model({'coords': _rand_coords_like(model_output['model_in'])})
+    hes, _ = diff_operators.hessian(rand_output['model_out'], rand_output['model_in'])
+    hes = hes.view(*hes.shape[0:2], -1)
+    hnorm = hes.norm(dim=-1, keepdim=True)
+    err = (model_output['model_out'] - gt['img']) ** 2
+    return {'img_loss': (err if mask is None else mask * err).mean(), 'prior_loss': k1 * torch.abs(hnorm).mean()}
+
+
 def function_mse(model_output, gt):
     return {'func_loss': ((model_output['model_out'] - gt['func']) ** 2).mean()}
 
@@ -21,6 +54,15 @@ def function_mse(model_output, gt):
 def gradients_mse(model_output, gt):
     g = diff_operators.gradient(model_output['model_out'], model_output['model_in'])
     return {'gradients_loss': torch.mean((g - gt['gradients']).pow(2).sum(-1))}
+
+
+def gradients_color_mse(model_output, gt):
+    """Weighted per-channel gradient loss of an RGB network (loss_functions.py:92-101): one diff_operators.gradient
+    per output channel (each a vjp node with a one-hot output weighting), concatenated to (B, N, 6)."""
+    y, x = model_output['model_out'], model_output['model_in']
+    g = torch.cat([diff_operators.gradient(y[..., c], x) for c in range(3)], dim=-1)
+    weights = torch.tensor([1e1, 1e1, 1., 1., 1e1, 1e1], dtype=g.dtype, device=g.device)
+    return {'gradients_loss': torch.mean((weights * (g[0:2] - gt['gradients']).pow(2)).sum(-1))}
 
 
 def laplace_mse(model_output, gt):
