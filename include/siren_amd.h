@@ -57,6 +57,9 @@ enum {
 /* cfg.reserved flag (benchmarking only): the round-2 second-order kernel whose epilogues run between the GEMMs
  * (w3_kernel) instead of the interleaved one (w3i_kernel). Same results. */
 #define SIREN_FLAG_W3_SERIAL 4
+/* cfg.reserved flag (benchmarking only): the round-4 kept Hessian-node backward whose epilogues run between the
+ * reverse GEMMs (qf_rev_kernel) instead of the interleaved one (qfi_rev_kernel). Same results. */
+#define SIREN_FLAG_QF_SERIAL 8
 
 /* Network description. Mirrors SingleBVPNet(out_features, type='sine', in_features, mode='mlp',
  * hidden_features, num_hidden_layers) (modules.py:122-123) and the notebook Siren(in_features,

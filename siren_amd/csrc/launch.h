@@ -75,6 +75,11 @@ void launch_hess(dim3 grid, hipStream_t st, const float* ws, const float* x, int
 void launch_qf_rev(int64_t ngroups, hipStream_t st, const float* ws, const float* x, int64_t n, const float* G,
                    const float* u, const float* kept, float* gx, float* gu, int d, int o, int lh, float w0, float w,
                    float* abuf, float* dbuf, int64_t n_pad);
+// tu_qfi.hip: the same backward with its epilogues interleaved into the reverse GEMMs (qfi_kernel.hpp), lh 1..5; same
+// arguments, grid and tile layout (results bitwise those of launch_qf_rev)
+void launch_qfi_rev(int64_t ngroups, hipStream_t st, const float* ws, const float* x, int64_t n, const float* G,
+                    const float* u, const float* kept, float* gx, float* gu, int d, int o, int lh, float w0, float w,
+                    float* abuf, float* dbuf, int64_t n_pad);
 // its edge layers (EDGE_Q8): rows zb_0 (dbuf layer 0) and the a_L jet (abuf layer L) over n_pad / 8 tile pairs
 void launch_small_q8(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x, const float* u,
                      int64_t n, int64_t n_pad, int64_t tps, float* eslab, int64_t E, int d, int o, int lh);

@@ -913,8 +913,12 @@ int32_t siren_hessian_backward_kept(const siren_cfg* cfg, const float* ws, const
         float* qa = tws;
         float* qd = qa + qp.buf_floats;
         float* qpart = qd + qp.buf_floats;
-        siren::launch_qf_rev(siren::hess_groups(n), st, ws, x, n, G, u, kept, gx, gu, cfg->d_in, cfg->d_out,
-                             cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, qa, qd, qp.n_pad);
+        if ((cfg->reserved & SIREN_FLAG_QF_SERIAL) != 0)
+            siren::launch_qf_rev(siren::hess_groups(n), st, ws, x, n, G, u, kept, gx, gu, cfg->d_in, cfg->d_out,
+                                 cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, qa, qd, qp.n_pad);
+        else
+            siren::launch_qfi_rev(siren::hess_groups(n), st, ws, x, n, G, u, kept, gx, gu, cfg->d_in, cfg->d_out,
+                                  cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, qa, qd, qp.n_pad);
         if (int rc = hip_status("siren_hessian_backward (kept quadratic-form jet)")) return rc;
         if (gparams == nullptr) return SIREN_OK;
         siren::launch_wgrad(dim3((unsigned)qp.splits, (unsigned)cfg->n_hidden), st, qa, qd, qp.cols, qp.tps, qpart, P,

@@ -286,6 +286,32 @@ def test_hessian_backward_vs_fp64(cuda, n, d, L, o, weighted):
         assert np.max(np.abs(hm[:, :, i] - ref)) <= 1e-4 * max(1., np.max(np.abs(ref)))
 
 
+@pytest.mark.parametrize('n,d,L,o,weighted', [(1, 2, 3, 1, False), (4097, 2, 3, 1, False), (333, 1, 2, 3, True),
+                                               (1000, 2, 1, 2, True), (70, 2, 4, 4, True), (2500, 2, 5, 1, True),
+                                               (65536, 2, 3, 1, False)])
+def test_hessian_backward_interleaved_vs_serial(cuda, n, d, L, o, weighted):
+    """The interleaved kept backward (qfi_rev_kernel, default) against the serial one (qf_rev_kernel,
+    SIREN_FLAG_QF_SERIAL): the same per-element arithmetic (qf_elem) on a different schedule, so gx and gu agree
+    bitwise and the theta-grads to rounding (non-symmetric G, 1..5 hidden layers, ragged n)."""
+    from siren_amd.engine import SirenEngine
+    layers = random_layers(d, L, o, seed=7 * n + L)
+    eng, ser = SirenEngine(d, 256, L, o), SirenEngine(d, 256, L, o, flags=8)
+    ws = eng.pack(to_dev(O.flatten(layers), cuda))
+    rng = np.random.default_rng(n + 1)
+    x = to_dev(rng.uniform(-1, 1, (n, d)).astype(np.float32), cuda)
+    G = to_dev((rng.normal(size=(n, d, d)) / max(n, 1)).astype(np.float32), cuda)
+    u = to_dev(rng.normal(size=(n, o)).astype(np.float32), cuda) if weighted else None
+    _, kept = eng.hessian(ws, x, u, keep=True)
+    a = eng.hessian_backward(ws, x, G, u, want_theta=True, want_u=True, kept=kept)
+    b = ser.hessian_backward(ws, x, G, u, want_theta=True, want_u=True, kept=kept)
+    assert torch.equal(a[0], b[0]), float((a[0] - b[0]).abs().max())  # gx
+    assert torch.equal(a[2], b[2]), float((a[2] - b[2]).abs().max())  # gu
+    assert torch.isfinite(a[1]).all()
+    assert float((a[1] - b[1]).abs().max()) <= 1e-6 * float(b[1].abs().max())
+    c = eng.hessian_backward(ws, x, G, u, want_theta=True, want_u=True, kept=kept)
+    assert all(torch.equal(p, q) for p, q in zip(a, c))  # deterministic
+
+
 def test_hessian_node_forward_matches_w3_axes(cuda):
     """siren_hessian (forward-mode 6-stream jet) against the W3 reverse-over-forward sweep along each axis (the
     node's previous forward): two independent second-order methods agree to fp32 rounding."""
