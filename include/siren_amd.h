@@ -60,6 +60,9 @@ enum {
 /* cfg.reserved flag (benchmarking only): the round-4 kept Hessian-node backward whose epilogues run between the
  * reverse GEMMs (qf_rev_kernel) instead of the interleaved one (qfi_rev_kernel). Same results. */
 #define SIREN_FLAG_QF_SERIAL 8
+/* cfg.reserved flag (benchmarking only): the hidden-512 stored-forward split on the round-2 kernel whose epilogues
+ * run between the GEMMs (wide_kernel) instead of the interleaved one (widei_kernel). Same results. */
+#define SIREN_FLAG_WIDE_SERIAL 16
 
 /* Network description. Mirrors SingleBVPNet(out_features, type='sine', in_features, mode='mlp',
  * hidden_features, num_hidden_layers) (modules.py:122-123) and the notebook Siren(in_features,

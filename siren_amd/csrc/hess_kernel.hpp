@@ -51,6 +51,13 @@ __device__ __forceinline__ int lane_here() {
     return l;
 }
 
+// layer 0's pre-activation z = b0 + x_0 W0[:, 0] + x_1 W0[:, 1] as one explicit fma chain: the Hessian node's forward
+// and every backward that rebuilds layer 0 from x (qf_common.hpp) must round it identically (hipcc's contraction of
+// the plain expression differs by context)
+__device__ __forceinline__ f32x4 layer0_z(const f32x4& b, const f32x4& wa, const f32x4& wb, float x0, float x1) {
+    return fma4(x1, wb, fma4(x0, wa, b));
+}
+
 __device__ __forceinline__ float row_ror8(float v) {
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xf, 0xf, false));
 }
@@ -112,7 +119,7 @@ __global__ __launch_bounds__(THREADS, 1) void hess_kernel(const float* __restric
         const int nb = 16 * rb + 4 * g;
         const f32x4 wa = *(const f32x4*)(sm + SM_W0 + nb);
         const f32x4 wb = *(const f32x4*)(sm + SM_W0 + H + nb);  // zero padded row when d == 1
-        const f32x4 zv = *(const f32x4*)(sm + SM_BIAS + nb) + x0 * wa + x1 * wb;
+        const f32x4 zv = layer0_z(*(const f32x4*)(sm + SM_BIAS + nb), wa, wb, x0, x1);
         const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
         const f32x4 t0 = hi ? wa : zv, t1 = hi ? zero : wb;  // (not kept: qf_layer0 rebuilds it)
         hess_sin(t0, t1, zero, w0, hi, act[0][rb], act[1][rb], act[2][rb]);

@@ -88,6 +88,9 @@ void launch_small_mix(dim3 grid, hipStream_t st, const float* abuf, const float*
                       int d, int o, int lh, int h);
 // tu_wide.hip: hidden width 512 (mode as siren_common.h MODE_*); spill = cos scratch for MODE_W1 / MODE_STORE
 void launch_wide(int mode, dim3 grid, hipStream_t st, const FusedArgs& a, float* spill);
+// tu_widei.hip: the stored-forward split at hidden 512 with interleaved epilogues (widei_kernel.hpp), MODE_FWDS /
+// MODE_REV, 1..5 hidden layers; arguments as launch_wide. Returns false (nothing launched) outside that range.
+bool launch_widei(int mode, dim3 grid, hipStream_t st, const FusedArgs& a, float* spill);
 // tu_wide_jet.hip: second order at hidden 512 (two-stream jet: 8 coordinates x (value, tangent) per wave, 32 per
 // workgroup); abuf / dbuf / spill: (L + 1) layers x 2 n_pad columns x 512 floats each
 void launch_wide_jet2(dim3 grid, hipStream_t st, const float* ws, const float* x, const float* v, const float* gy,

@@ -47,7 +47,7 @@ __device__ __forceinline__ QfKept qf_layer0(const float* sm, int rb, int g, bool
     const int nb = 16 * rb + 4 * g;
     const f32x4 wa = *(const f32x4*)(sm + SM_W0 + nb);
     const f32x4 wb = *(const f32x4*)(sm + SM_W0 + H + nb);  // zero padded row when d == 1
-    const f32x4 zv = *(const f32x4*)(sm + SM_BIAS + nb) + x0 * wa + x1 * wb;
+    const f32x4 zv = layer0_z(*(const f32x4*)(sm + SM_BIAS + nb), wa, wb, x0, x1);
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
     QfKept r;
     r.k[0] = hi ? wa : zv;
@@ -85,6 +85,27 @@ __device__ __forceinline__ void qf_elem(float k0, float k1, float k2, float ua, 
     const float t3 = w2s * (lin * u3);                            // w^2 s (2 Q z)_i u_3
     zb = hi ? wc * ub : __builtin_fmaf(wc, ub, -t3);              // zb_3 | zb_2
     const float K = __builtin_fmaf(w2s, z3, (wl2 * wc) * qz);     // w^2 s z_3 + w^3 c z^T Q z
+    const float t0 = __builtin_fmaf(w2s, __builtin_fmaf(pa, z1, ub * z2), u3 * K);
+    za = __builtin_fmaf(wc, ua, -(hi ? t3 : t0));                 // zb_1 | zb_0
+}
+
+// qf_elem for layer 0, whose jet every lane can form itself (qf_layer0's values, no partner exchange): z = W0 x + b0,
+// z_i = W0[:, i], z_ij = 0 — so z_3 = 0 and K = w^3 c z^T Q z. Same arithmetic as qf_elem on those values (every
+// product with the zero streams dropped), hence bitwise the same results.
+__device__ __forceinline__ void qf_elem0(float z, float z1, float z2, float ua, float ub, float wl, float wl2,
+                                         const QfCoef& q, bool hi, float& aa, float& ab, float& za, float& zb) {
+    const float pa = row_ror8(ua), pb = row_ror8(ub);
+    float sn, cs;
+    sincos_fast(wl * z, sn, cs);
+    const float wc = wl * cs, w2s = wl2 * sn;
+    const float qz = __builtin_fmaf(z1, __builtin_fmaf(q.q11, z1, q.q12 * z2), (q.q22 * z2) * z2);  // z^T Q z
+    const float lin = __builtin_fmaf(q.ca, z1, q.cb * z2);                                       // (2 Q z)_own
+    const float u3 = hi ? ub : pb;
+    aa = hi ? wc * z1 : sn;                                       // a_1 | a_0
+    ab = hi ? __builtin_fmaf(wc, 0.f, -w2s * qz) : wc * z2;       // a_3 | a_2   (z_3 = 0)
+    const float t3 = w2s * (lin * u3);
+    zb = hi ? wc * ub : __builtin_fmaf(wc, ub, -t3);              // zb_3 | zb_2
+    const float K = __builtin_fmaf(w2s, 0.f, (wl2 * wc) * qz);
     const float t0 = __builtin_fmaf(w2s, __builtin_fmaf(pa, z1, ub * z2), u3 * K);
     za = __builtin_fmaf(wc, ua, -(hi ? t3 : t0));                 // zb_1 | zb_0
 }

@@ -16,7 +16,7 @@
 //   * Epilogue E = G NB + b reads the kept z-jet of layer L - G, block b (3 x 16 B per lane, saddr-form loads issued at
 //     the mid-slice barrier three slices ahead, retired by that slice's counted vmcnt) and stages its four tile blocks
 //     (a-jet pair, zb pair; the seed's a-jet value stream feeds no gradient and is skipped) through a per-wave LDS
-//     transpose into one coalesced 1 KiB store each, issued at the start of the slice that consumes the block.
+//     transpose into one coalesced 1 KiB store each, issued early in the slice that consumes the block.
 //   * Every mid-slice s_waitcnt vmcnt(N) counts the vector-memory ops issued after the ring slice it publishes (a load's
 //     data waits for every older load AND store: they retire in issue order), compile-time per slice.
 //   * After the last GEMM, the layer-0 epilogue (the jet rebuilt from x, qf_layer0) runs serially: a_0 / zb_0 tiles and
@@ -28,7 +28,14 @@
 #ifndef QFI_EPI_PAIR
 #define QFI_EPI_PAIR 7  // operand pair after which the epilogue cluster runs (>= 4: after the mid-slice reload wait)
 #endif
+// operand pair after whose wait the previous epilogue's tile blocks are stored (< QFI_EPI_PAIR, which restages them;
+// >= 4: behind the mid-slice ring refill). Measured (profiles/r05c_qfi_probes.log, r05d): pair 0 5.14 ms, behind the
+// refill 5.50 ms
+#ifndef QFI_STORE_PAIR
+#define QFI_STORE_PAIR 0
+#endif
 static_assert(QFI_EPI_PAIR >= 4 && QFI_EPI_PAIR < siren::NB / 2, "the kept reloads land at the mid-slice wait");
+static_assert(QFI_STORE_PAIR >= 0 && QFI_STORE_PAIR < QFI_EPI_PAIR, "the epilogue restages the tile blocks");
 
 namespace siren {
 
@@ -164,8 +171,8 @@ __device__ __forceinline__ void qfi_epilogue(QfiState<LH>& st, const QfiCtx& cx,
 }
 
 // One slice S = G NB + KB of reverse GEMM G: 8 operand pairs x 16 MFMAs (two column tiles per A operand), the mid-slice
-// ring barrier after pair 3 (epilogue S+3's kept reloads issued ahead of the ring refill), the tile blocks of epilogue S
-// stored at its start, and epilogue block KB+1 as one VALU cluster after pair QFI_EPI_PAIR.
+// ring barrier after pair 3 (epilogue S+3's kept reloads issued ahead of the ring refill), epilogue S's tile blocks
+// stored after pair QFI_STORE_PAIR's wait, and epilogue block KB+1 as one VALU cluster after pair QFI_EPI_PAIR.
 template <int G, int KB, int LH>
 __device__ __forceinline__ void qfi_slice(QfiState<LH>& st, const QfiCtx& cx) {
     constexpr int NS = LH * NB;
@@ -183,10 +190,13 @@ __device__ __forceinline__ void qfi_slice(QfiState<LH>& st, const QfiCtx& cx) {
         constexpr int p = decltype(P)::value;
         if constexpr (p == 4 && S + 1 < NS) {
             // publish slice S+1 (issued at the mid-slice of S-2, after epilogue S+1's reloads) and free the slot of
-            // slice S-1 for slice S+3. Younger and allowed outstanding: epilogue S-1's tile stores (start of slice
-            // S-1), epilogue S+2's reloads and slice S+2's ring loads (mid-slice of S-1), epilogue S's tile stores
-            constexpr int ALLOW = qfi_nst<S - 1, LH>() + qfi_nrl<S + 2, LH>() + (S + 2 < NS ? 4 : 0) +
-                                  qfi_nst<S, LH>();
+            // slice S-1 for slice S+3. Younger and allowed outstanding: the tile stores of the last two epilogues
+            // issued after that ring slice (S-1 and S with the stores before the mid-slice wait, S-2 and S-1 after
+            // it), epilogue S+2's reloads and slice S+2's ring loads (mid-slice of S-1)
+            constexpr bool EARLY = QFI_STORE_PAIR < 4;
+            constexpr int ALLOW = (EARLY ? qfi_nst<S - 1, LH>() + qfi_nst<S, LH>()
+                                         : qfi_nst<S - 2, LH>() + qfi_nst<S - 1, LH>()) +
+                                  qfi_nrl<S + 2, LH>() + (S + 2 < NS ? 4 : 0);
             static_assert(ALLOW < 64, "vmcnt is 6 bits");
             asm volatile("s_waitcnt vmcnt(%0)" ::"i"(ALLOW) : "memory");
             qfi_reload_landed<S + 1, LH>(st);
@@ -217,8 +227,9 @@ __device__ __forceinline__ void qfi_slice(QfiState<LH>& st, const QfiCtx& cx) {
 #pragma unroll
             for (int j = 0; j < MAXO; ++j) asm volatile("" : "+v"(sp.wo[j]));
         }
-        // the tile blocks epilogue S staged (end of the previous slice / before the GEMM): retired by the same wait
-        if constexpr (p == 0) qfi_tile_flush<S, LH>(st, cx);
+        // the tile blocks epilogue S staged (end of the previous slice / before the GEMM): their LDS transpose was
+        // retired by pair 0's wait; stored after this pair's wait
+        if constexpr (p == QFI_STORE_PAIR) qfi_tile_flush<S, LH>(st, cx);
         if constexpr (p == QFI_EPI_PAIR && EPI) {
             __builtin_amdgcn_sched_barrier(0);
             qfi_epilogue<G, LH>(st, cx, KB + 1, (S + 1) % 3, sp);
@@ -357,31 +368,45 @@ __global__ __launch_bounds__(THREADS, 1) void qfi_rev_kernel(const float* __rest
         const float x1 = (valid && d > 1) ? x[coord * d + 1] : 0.f;
         const float wl = w0, wl2 = w0 * w0;
         float qk[2] = {0.f, 0.f};
+        // the last GEMM's epilogue S = NS - 1 staged nothing; block rb's tile blocks are staged after its arithmetic and
+        // stored after block rb + 1's (one LDS wait per block instead of one per tile block)
+        auto flush0 = [&](int rb) {
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(st.tq[0]), "+v"(st.tq[1]), "+v"(st.tq[2]), "+v"(st.tq[3]));
+            const int64_t off = rb * 1024;
+            w3_store16(w3_at(cx.ta, off), cx.vl, st.tq[0]);
+            w3_store16(w3_at(cx.ta, off + 16384), cx.vl, st.tq[1]);
+            w3_store16(w3_at(cx.td, off), cx.vl, st.tq[2]);
+            w3_store16(w3_at(cx.td, off + 16384), cx.vl, st.tq[3]);
+        };
 #pragma unroll
         for (int rb = 0; rb < NB; ++rb) {
-            const QfKept kc = qf_layer0(sm, rb, cx.g, cx.hi, x0, x1);
+            const int nb = 16 * rb + 4 * cx.g;
+            const f32x4 wa = *(const f32x4*)(sm + SM_W0 + nb);
+            const f32x4 wb = *(const f32x4*)(sm + SM_W0 + H + nb);  // zero padded row when d == 1
+            const f32x4 zv = layer0_z(*(const f32x4*)(sm + SM_BIAS + nb), wa, wb, x0, x1);
             const f32x4 ua = st.acc[GL][0][rb], ub = st.acc[GL][1][rb];
             f32x4 aa, ab, za, zb;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float ea, eb, ga, gb;
-                qf_elem(kc.k[0][r], kc.k[1][r], kc.k[2][r], ua[r], ub[r], wl, wl2, cx.q, cx.hi, ea, eb, ga, gb);
+                qf_elem0(zv[r], wa[r], wb[r], ua[r], ub[r], wl, wl2, cx.q, cx.hi, ea, eb, ga, gb);
                 aa[r] = ea;
                 ab[r] = eb;
                 za[r] = ga;
                 zb[r] = gb;
             }
-            const int64_t off = rb * 1024;
-            w3_stage_store(w3_at(cx.ta, off), aa, cx.tw, cx.tr, cx.vl);
-            w3_stage_store(w3_at(cx.ta, off + 16384), ab, cx.tw, cx.tr, cx.vl);
-            w3_stage_store(w3_at(cx.td, off), za, cx.tw, cx.tr, cx.vl);
-            w3_stage_store(w3_at(cx.td, off + 16384), zb, cx.tw, cx.tr, cx.vl);
+            if (rb > 0) flush0(rb - 1);
+            w3_stage(st.tq[0], aa, cx.tw, cx.tr);
+            w3_stage(st.tq[1], ab, cx.tw, cx.tr);
+            w3_stage(st.tq[2], za, cx.tw, cx.tr);
+            w3_stage(st.tq[3], zb, cx.tw, cx.tr);
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
                 const f32x4 wk = *(const f32x4*)(sm + SM_W0 + k * H + 16 * rb + 4 * cx.g);  // zero row when d == 1
                 qk[k] += wk[0] * za[0] + wk[1] * za[1] + wk[2] * za[2] + wk[3] * za[3];
             }
         }
+        flush0(NB - 1);
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             if (k < d) {

@@ -560,7 +560,9 @@ int32_t siren_forward_store(const siren_cfg* cfg, const float* ws, const float* 
     if (wide(cfg)) {
         siren::FusedArgs fa{ws, x, n, nullptr, y, nullptr, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first,
                             cfg->omega_hidden, 0, abuf, nullptr, plan.n_pad};
-        siren::launch_wide(siren::MODE_FWDS, grid, (hipStream_t)stream, fa, cbuf);
+        if ((cfg->reserved & SIREN_FLAG_WIDE_SERIAL) != 0 ||
+            !siren::launch_widei(siren::MODE_FWDS, grid, (hipStream_t)stream, fa, cbuf))
+            siren::launch_wide(siren::MODE_FWDS, grid, (hipStream_t)stream, fa, cbuf);
         return hip_status("siren_forward_store");
     }
     siren::FusedArgs fa{w1_ws(cfg, ws), x, n, nullptr, y, nullptr, cfg->d_in, cfg->d_out, cfg->n_hidden,
@@ -601,7 +603,9 @@ int32_t siren_backward_stored(const siren_cfg* cfg, const float* ws, const float
     if (wide(cfg)) {
         siren::FusedArgs fa{ws, x, n, gy, nullptr, gx, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first,
                             cfg->omega_hidden, 0, nullptr, dbuf, plan.n_pad};
-        siren::launch_wide(siren::MODE_REV, dim3((unsigned)(plan.n_pad / siren::TILE)), st, fa, cbuf);
+        const dim3 rgrid((unsigned)(plan.n_pad / siren::TILE));
+        if ((cfg->reserved & SIREN_FLAG_WIDE_SERIAL) != 0 || !siren::launch_widei(siren::MODE_REV, rgrid, st, fa, cbuf))
+            siren::launch_wide(siren::MODE_REV, rgrid, st, fa, cbuf);
     } else {
         siren::FusedArgs fa{w1_ws(cfg, ws), x, n, gy, nullptr, gx, cfg->d_in, cfg->d_out, cfg->n_hidden,
                             cfg->omega_first, cfg->omega_hidden, 0, cbuf, dbuf, plan.n_pad};

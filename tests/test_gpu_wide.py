@@ -139,6 +139,28 @@ def test_module_image_fit_step_wide(cuda, g4):
         assert np.max(np.abs(p.grad.cpu().numpy() - ref)) <= 1e-4 * max(1e-6, np.max(np.abs(ref))) + 1e-9, name
 
 
+@pytest.mark.parametrize('n,d,L,o', [(1, 3, 3, 3), (4097, 3, 3, 3), (700, 2, 1, 1), (333, 4, 5, 2), (130, 1, 2, 4),
+                                     (2000, 3, 4, 3), (65536, 3, 3, 3)])
+def test_wide_interleaved_split_bitwise_vs_serial(cuda, n, d, L, o):
+    """The interleaved hidden-512 stored split (widei_kernel, default) against the serial one (wide_kernel,
+    SIREN_FLAG_WIDE_SERIAL): the same arithmetic on another schedule, so y, the stored a_l tiles / cos scratch, gx and
+    the theta-grads are bitwise equal."""
+    from siren_amd.engine import SirenEngine
+    layers = random_layers(d, L, o, seed=11 * n + L)
+    eng, ser = wide_engine(d, L, o), SirenEngine(d, H, L, o, flags=16)
+    ws = eng.pack(to_dev(O.flatten(layers), cuda))
+    rng = np.random.default_rng(n + 3)
+    x = to_dev(rng.uniform(-1, 1, (n, d)), cuda)
+    gy = to_dev(rng.normal(size=(n, o)), cuda)
+    y_a, tws_a = eng.forward_store(ws, x)
+    y_b, tws_b = ser.forward_store(ws, x)
+    assert torch.equal(y_a, y_b)
+    gx_a, gp_a = eng.backward_stored(ws, x, gy, tws_a)
+    gx_b, gp_b = ser.backward_stored(ws, x, gy, tws_b)
+    assert torch.equal(gx_a, gx_b) and torch.equal(gp_a, gp_b)
+    assert torch.isfinite(gp_a).all()
+
+
 @pytest.mark.parametrize('n,d,L,o', [(1, 3, 3, 3), (4097, 3, 3, 3), (700, 2, 1, 1), (333, 4, 5, 2)])
 def test_wide_stored_forward_split_matches_recompute(cuda, n, d, L, o):
     """Hidden 512 stored-forward split (wide_kernel MODE_FWDS / MODE_REV) == the recompute pipeline; vs fp64."""
