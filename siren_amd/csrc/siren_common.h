@@ -297,6 +297,12 @@ __device__ __forceinline__ f32x4 fma4(float s, const f32x4& v, const f32x4& z) {
                  __builtin_fmaf(s, v[3], z[3])};
 }
 
+// q + w . v over the four elements as one explicit fma chain (the same rounding in every kernel that reduces a block
+// this way: hipcc's contraction of the plain sum differs by context)
+__device__ __forceinline__ float dot4_acc(const f32x4& w, const f32x4& v, float q) {
+    return __builtin_fmaf(w[3], v[3], __builtin_fmaf(w[2], v[2], __builtin_fmaf(w[1], v[1], __builtin_fmaf(w[0], v[0], q))));
+}
+
 // A scalar operand as an opaque value. A context-struct field splat into an f32x4 product is otherwise widened by
 // instcombine into a 16-byte load across the neighbouring fields; SROA then cannot split the struct, it stays in
 // scratch, and its fields are reloaded from scratch (with a vmcnt wait) inside the MFMA loops (round 4: the W1

@@ -257,7 +257,7 @@ __global__ __launch_bounds__(THREADS, 1) void wide_kernel(
 #pragma unroll
             for (int rb = 0; rb < WNB; ++rb) {
                 const f32x4 wk = *(const f32x4*)(sm + L.w0 + k * WH + 16 * rb + 4 * g);
-                q += wk[0] * act[rb][0] + wk[1] * act[rb][1] + wk[2] * act[rb][2] + wk[3] * act[rb][3];
+                q = dot4_acc(wk, act[rb], q);
             }
             q = sum_groups(q);
             if (valid && g == 0) gx[coord * d + k] = q;

@@ -18,10 +18,11 @@
 //     and gx = W0^T delta_0).
 //   * Each epilogue block's tile block (a_l or delta_l, the wgrad layout) is transposed through a per-wave LDS scratch
 //     into ONE coalesced 1 KiB store, issued at the start of the slice that consumes the block; the lane-major cos
-//     block goes out directly (FWDS) or is reloaded one and a half slices ahead (REV). The mid-slice s_waitcnt vmcnt(N)
-//     counts exactly the vector-memory ops issued after the ring slice it publishes.
-//   * 3-slot ring of 32 KiB slices (ring_mid protocol: the barrier after operand pair 7 of 16 publishes slice s + 1 and
-//     frees slot s - 1 for slice s + 2), the next slice's first operand pair read during the last pair.
+//     block goes out directly (FWDS) or is reloaded NBUF - 1 mid-slices ahead of its epilogue (REV). The mid-slice
+//     s_waitcnt vmcnt(N) counts exactly the vector-memory ops issued after the ring slice it publishes.
+//   * Ring of 32 KiB slices, 4 slots at 1..3 hidden layers (3 beyond, where the small block leaves no room): the barrier
+//     after operand pair 7 of 16 publishes slice s + 1 and frees slot s - 1 for slice s + NBUF - 1; the next slice's
+//     first operand pair is read during the last pair.
 // Same arithmetic as wide_kernel (sincos_fast on the unscaled pack), so the results are bitwise those of wide_kernel
 // (tests/test_gpu_wide.py).
 #include "w3i_kernel.hpp"
@@ -35,15 +36,29 @@ static_assert(WIDEI_EPI_PAIR >= 8 && WIDEI_EPI_PAIR < siren::WNB / 2, "REV's cos
 namespace siren {
 
 constexpr int wsmall_floats_ct(int lh) { return 9 * WH + 4 + (lh + 1) * WH; }
+// ring slots: 4 x 32 KiB while the small block fits beside them in the 160 KiB of LDS (1..3 hidden layers: the slice for
+// S + 3 is issued at the mid-slice of S, two slices of lead), else 3 (one slice of lead)
+constexpr int widei_nbuf(int lh) { return lh <= 3 ? 4 : 3; }
 
-// vector-memory ops of epilogue E (0 past the interleaved ones): the tile block store (flushed at the start of slice
-// E), FWDS's direct cos store (issued by the epilogue itself), REV's cos reload
 template <int E, int LH>
 constexpr bool widei_has(int) { return E >= 0 && E < LH * WNB; }
-template <int E, int LH, int MODE>
-constexpr int widei_nflush() { return widei_has<E, LH>(0) ? 1 : 0; }
-template <int E, int LH, int MODE>
-constexpr int widei_ndirect() { return (MODE == MODE_FWDS && widei_has<E, LH>(0)) ? 1 : 0; }
+
+// the vector-memory ops issued after ring slice S + 1 (issued at the mid-slice of S + 2 - NBUF, right after epilogue
+// S + 1's reload) up to the mid-slice wait of slice S: the reloads and ring slices of the mid-slices in between, and the
+// stores of the epilogues run after it (FWDS: the direct cos store and the tile flush; REV: the tile flush)
+template <int S, int LH, int MODE>
+constexpr int widei_allow() {
+    constexpr int ahead = widei_nbuf(LH) - 1, NS = LH * WNB;
+    int n = 0;
+    for (int m = S + 2 - ahead; m < S; ++m) {
+        const int e = m + ahead;  // reload and ring slice issued at the mid-slice of m
+        n += (MODE == MODE_REV && e >= 0 && e < NS) ? 1 : 0;
+        n += e < NS ? 8 : 0;
+    }
+    for (int e = S + 2 - ahead; e <= S; ++e)
+        n += (e >= 0 && e < NS) ? ((MODE == MODE_FWDS ? 1 : 0) + 1) : 0;
+    return n;
+}
 
 template <int LH, int MODE>
 struct WideiState {
@@ -94,6 +109,16 @@ __device__ __forceinline__ void widei_param_load(WideiParams<G, MODE>& ep, const
 #pragma unroll
     for (int i = 0; i < widei_nparams<G, MODE>(); ++i)
         ep.v[i] = *(const f32x4*)((const char*)cx.sm + widei_param_off<G, MODE>(i, b) + 16 * cx.g);
+}
+
+// this wave's 8 KiB of the 32 KiB slice s (8 saddr-form 1 KiB global_load_lds pieces) into ring slot s % NBUF
+template <int NBUF>
+__device__ __forceinline__ void widei_ring_issue(const float* __restrict__ stream, float* ring, int s, int wave,
+                                                 int lane) {
+    const char* src = (const char*)(stream + (int64_t)s * WSLICE + wave * 2048);
+    const unsigned dst = lds_addr(ring + (s % NBUF) * WSLICE + wave * 2048);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) glds_x4(src + q * 1024, 16u * lane, dst + q * 1024);
 }
 
 // the layer whose cos epilogue E reads (REV: SEED layer L, then L - G) or writes (FWDS: layer G)
@@ -170,9 +195,10 @@ __device__ __forceinline__ void widei_epilogue(WideiState<LH, MODE>& st, const W
 template <int G, int KB, int LH, int MODE>
 __device__ __forceinline__ void widei_slice(WideiState<LH, MODE>& st, const WideiCtx& cx) {
     constexpr int NS = LH * WNB;
+    constexpr int NBUF = widei_nbuf(LH);
     constexpr int S = G * WNB + KB;
-    constexpr int SLOT = (S % WNBUF) * WSLICE * 4;
-    constexpr int NSLOT = ((S + 1) % WNBUF) * WSLICE * 4;
+    constexpr int SLOT = (S % NBUF) * WSLICE * 4;
+    constexpr int NSLOT = ((S + 1) % NBUF) * WSLICE * 4;
     constexpr bool EPI = KB + 1 < WNB;
     f32x4(&acc)[WNB] = st.acc[G & 1];
     const f32x4 bop = st.b[KB & 1];
@@ -183,18 +209,18 @@ __device__ __forceinline__ void widei_slice(WideiState<LH, MODE>& st, const Wide
     static_for<0, WNB / 2>([&](auto P) {
         constexpr int p = decltype(P)::value;
         if constexpr (p == 8 && S + 1 < NS) {
-            // publish slice S+1 (issued at the mid-slice of S-1, after epilogue S+1's reload) and free the slot of
-            // slice S-1 for slice S+2. Younger and allowed outstanding: epilogue S's direct cos store (slice S-1) and
-            // its tile store (start of this slice)
-            constexpr int ALLOW = widei_ndirect<S, LH, MODE>() + widei_nflush<S, LH, MODE>();
+            // publish slice S+1 (issued behind epilogue S+1's reload) and free the slot of slice S-1 for slice
+            // S+NBUF-1; the vector-memory ops issued after slice S+1 stay outstanding (widei_allow)
+            constexpr int ALLOW = widei_allow<S, LH, MODE>();
+            static_assert(ALLOW < 64, "vmcnt is 6 bits");
             asm volatile("s_waitcnt vmcnt(%0)" ::"i"(ALLOW) : "memory");
             widei_reload_landed<S + 1, LH, MODE>(st);
-            widei_reload_issue<S + 2, LH, MODE>(st, cx);
+            widei_reload_issue<S + NBUF - 1, LH, MODE>(st, cx);
             __builtin_amdgcn_s_barrier();
-            if constexpr (S + 2 < NS) {
+            if constexpr (S + NBUF - 1 < NS) {
                 const float* spp = cx.stream;
                 asm volatile("" : "+s"(spp));  // keep slice addresses from being hoisted into SGPRs
-                wring_issue(spp, cx.ring, S + 2, NS, cx.wave, cx.lane);
+                widei_ring_issue<NBUF>(spp, cx.ring, S + NBUF - 1, cx.wave, cx.lane);
             }
         }
         f32x4 n0, n1;
@@ -271,11 +297,12 @@ __global__ __launch_bounds__(THREADS, 1) void widei_kernel(const float* __restri
     constexpr bool REV = MODE == MODE_REV;
     constexpr int NS = LH * WNB;
     constexpr int SMALL4 = (wsmall_floats_ct(LH) + 3) / 4 * 4;
-    __shared__ __attribute__((aligned(16))) float lds[WNBUF * WSLICE + SMALL4 + WAVES * STB_SCRATCH];
+    constexpr int NBUF = widei_nbuf(LH);
+    __shared__ __attribute__((aligned(16))) float lds[NBUF * WSLICE + SMALL4 + WAVES * STB_SCRATCH];
     WideiCtx cx;
     WideiState<LH, MODE> st;
     cx.ring = lds;
-    float* sm = lds + WNBUF * WSLICE;
+    float* sm = lds + NBUF * WSLICE;
     cx.sm = sm;
     cx.lane = threadIdx.x & 63;
     cx.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -287,9 +314,9 @@ __global__ __launch_bounds__(THREADS, 1) void widei_kernel(const float* __restri
     cx.stream = ws + L.pad(LH) + (REV ? (int64_t)LH * WNB * WSLICE : 0);
     const unsigned lds_base = lds_addr(lds);
     cx.ring_vaddr = lds_base + cx.lane * 16;
-    cx.sm_vaddr = lds_base + WNBUF * WSLICE * 4 + 16 * cx.g;
+    cx.sm_vaddr = lds_base + NBUF * WSLICE * 4 + 16 * cx.g;
     {
-        const unsigned scr = lds_base + 4u * (WNBUF * WSLICE + SMALL4 + cx.wave * STB_SCRATCH);
+        const unsigned scr = lds_base + 4u * (NBUF * WSLICE + SMALL4 + cx.wave * STB_SCRATCH);
         cx.tw = scr + 4u * (4 * cx.g * STB_ROW + c);
         cx.tr = scr + 4u * ((cx.lane >> 2) * STB_ROW + 4 * (cx.lane & 3));
     }
@@ -312,13 +339,14 @@ __global__ __launch_bounds__(THREADS, 1) void widei_kernel(const float* __restri
         for (int e = threadIdx.x; e < nf4; e += THREADS) ((f32x4*)sm)[e] = ((const f32x4*)ws)[e];
     }
     __syncthreads();
-    // prologue in the order the mid-slice counts assume: epilogues 0 and 1's reloads (REV), ring slices 0 and 1; then
-    // slice 0 and the reloads landed
-    widei_reload_issue<0, LH, MODE>(st, cx);
-    widei_reload_issue<1, LH, MODE>(st, cx);
-    wring_issue(cx.stream, cx.ring, 0, NS, cx.wave, cx.lane);
-    wring_issue(cx.stream, cx.ring, 1, NS, cx.wave, cx.lane);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    // prologue: the NBUF - 1 mid-slices before slice 0, in the order the mid-slice counts assume (epilogue e's reload,
+    // then ring slice e, for e = 0 .. NBUF - 2); then slice 0 and epilogue 0's reload landed
+    static_for<0, NBUF - 1>([&](auto E) {
+        widei_reload_issue<decltype(E)::value, LH, MODE>(st, cx);
+        widei_ring_issue<NBUF>(cx.stream, cx.ring, decltype(E)::value, cx.wave, cx.lane);
+    });
+    constexpr int PRO = (NBUF - 2) * (8 + (REV ? 1 : 0));  // ops issued after ring slice 0
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PRO) : "memory");
     __builtin_amdgcn_s_barrier();
     widei_reload_landed<0, LH, MODE>(st);
     st.pa0 = lds_read4<0>(cx.ring_vaddr);
@@ -378,7 +406,7 @@ __global__ __launch_bounds__(THREADS, 1) void widei_kernel(const float* __restri
             for (int k = 0; k < MAXD; ++k) {
                 if (k < d) {
                     const f32x4 wk = *(const f32x4*)(sm + L.w0 + k * WH + 16 * rb + 4 * cx.g);
-                    q[k] += wk[0] * dl[0] + wk[1] * dl[1] + wk[2] * dl[2] + wk[3] * dl[3];
+                    q[k] = dot4_acc(wk, dl, q[k]);
                 }
             }
         }
