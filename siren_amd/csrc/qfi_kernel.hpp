@@ -368,16 +368,9 @@ __global__ __launch_bounds__(THREADS, 1) void qfi_rev_kernel(const float* __rest
         const float x1 = (valid && d > 1) ? x[coord * d + 1] : 0.f;
         const float wl = w0, wl2 = w0 * w0;
         float qk[2] = {0.f, 0.f};
-        // the last GEMM's epilogue S = NS - 1 staged nothing; block rb's tile blocks are staged after its arithmetic and
-        // stored after block rb + 1's (one LDS wait per block instead of one per tile block)
-        auto flush0 = [&](int rb) {
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(st.tq[0]), "+v"(st.tq[1]), "+v"(st.tq[2]), "+v"(st.tq[3]));
-            const int64_t off = rb * 1024;
-            w3_store16(w3_at(cx.ta, off), cx.vl, st.tq[0]);
-            w3_store16(w3_at(cx.ta, off + 16384), cx.vl, st.tq[1]);
-            w3_store16(w3_at(cx.td, off), cx.vl, st.tq[2]);
-            w3_store16(w3_at(cx.td, off + 16384), cx.vl, st.tq[3]);
-        };
+        // tile blocks as four dword stores each (store_block): no LDS transpose, so no LDS wait between the blocks
+        float* pa0 = (float*)cx.ta + 4 * cx.g * 16 + c;
+        float* pd0 = (float*)cx.td + 4 * cx.g * 16 + c;
 #pragma unroll
         for (int rb = 0; rb < NB; ++rb) {
             const int nb = 16 * rb + 4 * cx.g;
@@ -395,18 +388,16 @@ __global__ __launch_bounds__(THREADS, 1) void qfi_rev_kernel(const float* __rest
                 za[r] = ga;
                 zb[r] = gb;
             }
-            if (rb > 0) flush0(rb - 1);
-            w3_stage(st.tq[0], aa, cx.tw, cx.tr);
-            w3_stage(st.tq[1], ab, cx.tw, cx.tr);
-            w3_stage(st.tq[2], za, cx.tw, cx.tr);
-            w3_stage(st.tq[3], zb, cx.tw, cx.tr);
+            store_block(pa0, rb, aa);
+            store_block(pa0 + H * 16, rb, ab);
+            store_block(pd0, rb, za);
+            store_block(pd0 + H * 16, rb, zb);
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
                 const f32x4 wk = *(const f32x4*)(sm + SM_W0 + k * H + 16 * rb + 4 * cx.g);  // zero row when d == 1
                 qk[k] += wk[0] * za[0] + wk[1] * za[1] + wk[2] * za[2] + wk[3] * za[3];
             }
         }
-        flush0(NB - 1);
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             if (k < d) {

@@ -355,11 +355,9 @@ __global__ __launch_bounds__(THREADS, 1) void widei_kernel(const float* __restri
     widei_run<0, LH, MODE>(st, cx);
 
     constexpr int GL = (LH - 1) & 1;
-    // the final epilogue (serial): block rb's tile block is staged after its arithmetic and stored after block rb + 1's
-    auto flush = [&](int rb) {
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(st.tq));
-        w3_store16(w3_at(cx.tb, (int64_t)(REV ? 0 : LH) * cx.lb + rb * 1024), cx.vl, st.tq);
-    };
+    // the final epilogue (serial): its tile blocks go out as four dword stores each (store_block), with no LDS
+    // transpose and so no LDS wait between the blocks' arithmetic (measured: the staged form kept the tail serial)
+    float* tp = (float*)cx.tb + (int64_t)(REV ? 0 : LH) * (cx.lb / 4) + 4 * cx.g * 16 + c;
     if constexpr (!REV) {
         // last hidden layer: a_L and cos(w z_L) (the reverse pass's seed) out, y = a_L Wout^T + bout
         const float* bl = sm + L.bias + LH * WH + 4 * cx.g;
@@ -374,8 +372,7 @@ __global__ __launch_bounds__(THREADS, 1) void widei_kernel(const float* __restri
                 sn[r] = a;
                 cs[r] = cc;
             }
-            if (rb > 0) flush(rb - 1);
-            w3_stage(st.tq, sn, cx.tw, cx.tr);
+            store_block(tp, rb, sn);
             w3_store16(w3_at(cx.cs, (int64_t)LH * cx.lb + rb * 1024), cx.vl, cs);
 #pragma unroll
             for (int j = 0; j < MAXO; ++j) {
@@ -385,7 +382,6 @@ __global__ __launch_bounds__(THREADS, 1) void widei_kernel(const float* __restri
                 }
             }
         }
-        flush(WNB - 1);
 #pragma unroll
         for (int j = 0; j < MAXO; ++j) {
             if (j < o) {
@@ -400,8 +396,7 @@ __global__ __launch_bounds__(THREADS, 1) void widei_kernel(const float* __restri
         for (int rb = 0; rb < WNB; ++rb) {
             const f32x4 c0 = *(const f32x4*)(cx.cs + rb * 1024 + 16 * cx.lane);
             const f32x4 dl = (st.acc[GL][rb] * c0) * w0;
-            if (rb > 0) flush(rb - 1);
-            w3_stage(st.tq, dl, cx.tw, cx.tr);
+            store_block(tp, rb, dl);
 #pragma unroll
             for (int k = 0; k < MAXD; ++k) {
                 if (k < d) {
@@ -410,7 +405,6 @@ __global__ __launch_bounds__(THREADS, 1) void widei_kernel(const float* __restri
                 }
             }
         }
-        flush(WNB - 1);
 #pragma unroll
         for (int k = 0; k < MAXD; ++k) {
             if (k < d) {
