@@ -13,7 +13,8 @@
 //   dWout[j]   = sum glap a_L,second                                               (lap = sum_j Wout_j a_L,second)
 //   gx         = W0^T zb_0,value
 //
-// jet_store_kernel: forward jet (stores a-jets to abuf and z-jets to a lane-major scratch), seed
+// jet_store_kernel: forward jet (stores a-jets to abuf and, per stream lane, the reverse's combinations of the z jet —
+// siren_common.h jet_sin_d; MIX / QG: the z jet itself — to a lane-major scratch), seed
 // u_L,second = (sum_j Wout_j) glap, then the reverse sweep storing zb-jets to dbuf; one layer body for all 2L
 // GEMM passes (runtime loop), 3-slot ring of 16 KiB slices (ring.hpp). Tiles are 16 columns = 4 coordinates.
 // Split (laplace_mse training, SirenLaplace with a stored forward): PHASE JET_FWD runs the forward passes only —
@@ -123,6 +124,9 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
     }
     const float kb0 = js == 0 ? 0.f : w0, kg0 = js == 3 ? w0 * w0 : 0.f;
     const float kb = js == 0 ? 0.f : w, kg = js == 3 ? w * w : 0.f;
+    // !MIX: the scratch holds the reverse's combinations of the z jet (jet_sin_d), per layer scale w0 / w
+    const float dA0 = js == 0 ? w0 : 0.f, dB0 = js == 0 ? 0.f : w0 * w0, dC0 = js == 3 ? w0 * w0 * w0 : 0.f;
+    const float dA = js == 0 ? w : 0.f, dB = js == 0 ? 0.f : w * w, dC = js == 3 ? w * w * w : 0.f;
     const float m12 = (js == 1 || js == 2) ? 1.f : 0.f;
     const float gl = (PHASE != JET_FWD && valid && js == 3) ? (MIX ? 1.f : glap[coord]) : 0.f;
     const bool s1 = js == 1;
@@ -154,7 +158,7 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
 #pragma unroll
         for (int rb = 0; rb < NB; ++rb) {
             const f32x4 u = gl * *(const f32x4*)(sm + SM_SEED + 16 * rb + 4 * g);
-            act[rb] = jet_sin_adjoint<MIX>(u, zl.next_load(), w, val, m12, s1);
+            act[rb] = jet_sin_adjoint_d(u, zl.next_load(), val, m12);
         }
         jstore_tile(dbuf + (int64_t)lh * lstride + toff, act);
     } else {
@@ -171,9 +175,13 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
                 f32x4 kz;
                 act[rb] = jet_sin_q(z, w0, val, kb0, kg0, qc[0], qc[1], js == 3, kz);
                 zs.next_store(kz);
-            } else {
+            } else if constexpr (MIX) {
                 zs.next_store(z);
                 act[rb] = jet_sin<MIX>(z, w0, val, kb0, kg0);
+            } else {
+                f32x4 dz;
+                act[rb] = jet_sin_d(z, w0, val, kb0, kg0, dA0, dB0, dC0, dz);
+                zs.next_store(dz);
             }
         }
         jstore_tile(abuf + toff, act);
@@ -213,9 +221,13 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
                     f32x4 kz;
                     act[rb] = jet_sin_q(z, w, val, kb, kg, qc[0], qc[1], js == 3, kz);
                     zs.next_store(kz);
-                } else {
+                } else if constexpr (MIX) {
                     zs.next_store(z);
                     act[rb] = jet_sin<MIX>(z, w, val, kb, kg);
+                } else {
+                    f32x4 dz;
+                    act[rb] = jet_sin_d(z, w, val, kb, kg, dA, dB, dC, dz);
+                    zs.next_store(dz);
                 }
             }
             jstore_tile(abuf + (int64_t)l * lstride + toff, act);
@@ -279,8 +291,9 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
                     } else {
                         sd = *(const f32x4*)(sm + SM_SEED + 16 * rb + 4 * g);
                     }
-                    act[rb] = QG ? jet_sin_adjoint_q(gl * sd, zl.next_load(), w, val, m12, qc[0], qc[1])
-                                 : jet_sin_adjoint<MIX>(gl * sd, zl.next_load(), w, val, m12, s1);
+                    act[rb] = QG    ? jet_sin_adjoint_q(gl * sd, zl.next_load(), w, val, m12, qc[0], qc[1])
+                              : MIX ? jet_sin_adjoint<MIX>(gl * sd, zl.next_load(), w, val, m12, s1)
+                                    : jet_sin_adjoint_d(gl * sd, zl.next_load(), val, m12);
                 }
                 jstore_tile(dbuf + (int64_t)lh * lstride + toff, act);
             }
@@ -293,8 +306,9 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
             {
 #pragma unroll
                 for (int rb = 0; rb < NB; ++rb) {
-                    act[rb] = QG ? jet_sin_adjoint_q(acc[rb], zl.next_load(), wl, val, m12, qc[0], qc[1])
-                                 : jet_sin_adjoint<MIX>(acc[rb], zl.next_load(), wl, val, m12, s1);
+                    act[rb] = QG    ? jet_sin_adjoint_q(acc[rb], zl.next_load(), wl, val, m12, qc[0], qc[1])
+                              : MIX ? jet_sin_adjoint<MIX>(acc[rb], zl.next_load(), wl, val, m12, s1)
+                                    : jet_sin_adjoint_d(acc[rb], zl.next_load(), val, m12);
                 }
             }
             jstore_tile(dbuf + (int64_t)lm * lstride + toff, act);

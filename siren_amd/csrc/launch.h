@@ -35,6 +35,9 @@ void launch_w0(dim3 grid, hipStream_t st, const FusedArgs& a);
 // tu_w1deep.hip: MODE_FWDS / MODE_REV of the W1 kernel at 4..5 hidden layers (hidden 256)
 void launch_w1_deep(int mode, dim3 grid, hipStream_t st, const FusedArgs& a);
 void launch_w0s(dim3 grid, hipStream_t st, const FusedArgs& a);
+// tu_w1nt.hip: MODE_FWDS without a_l tiles (a.abuf == NULL) / MODE_REV without delta tiles (a.dbuf == NULL), 1..5
+// hidden layers; launch_w0s and launch_w1(MODE_REV) route here when the tile pointer is NULL
+void launch_w1_notile(int mode, dim3 grid, hipStream_t st, const FusedArgs& a);
 // tu_w1x.hip: split-bf16 W1 (bf16x6 products on the bf16 matrix pipe; 3 hidden layers, d_in 2 / 3, d_out 1,
 // gy = ones); the stream holds split_stream_words(lh) 32-bit words
 int64_t split_stream_words(int lh);

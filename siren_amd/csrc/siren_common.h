@@ -43,7 +43,9 @@ enum { MODE_W1 = 0, MODE_STORE = 1, MODE_FWD = 2, MODE_JET = 3, MODE_FWDS = 4, M
 // MODE_O1S specialises d_out == 1 with the all-ones output cotangent (gy == NULL); MODE_D(k) fixes d_in = k at
 // compile time. Both only remove runtime-uniform branches and selects from the epilogues (whose VALU count is the
 // kernel's overhead, see sincos_fast).
-enum { MODE_BASE = 15, MODE_PROF = 64, MODE_O1S = 128 };
+// MODE_NOTILE: MODE_FWDS without the a_l tiles (lane-major cos only) / MODE_REV without the delta tiles (gx only), so
+// the slice loops count the epilogues' vector-memory ops at compile time.
+enum { MODE_BASE = 15, MODE_NOTILE = 32, MODE_PROF = 64, MODE_O1S = 128 };
 constexpr int MODE_D(int k) { return k << 8; }
 constexpr int mode_din(int mode) { return (mode >> 8) & 7; }
 // MODE_PROF (diagnostics, siren_w1_phase_profile): s_memtime stamps at tile start, after each GEMM and at tile end
@@ -212,6 +214,39 @@ __device__ __forceinline__ f32x4 jet_sin_adjoint(const f32x4& u, const f32x4& z,
         const float t0 = __builtin_fmaf(w2s, __builtin_fmaf(u1, z1, u2 * z2),
                                         u3 * __builtin_fmaf(w2s, z3, (w * w * wc) * q2));
         out[r] = __builtin_fmaf(wc, u[r], -__builtin_fmaf(m12, t12, m0 * t0));
+    }
+    return out;
+}
+
+// The reverse needs each coordinate's jet of z only through four combinations, one per stream lane:
+//   P = w c (lane 0),  R_i = w^2 s z_i (lanes 1, 2),  T = w^2 s z_3 + w^3 c (z_1^2 + z_2^2) (lane 3)
+// so the forward stores those (jet_sin_d) in the z-jet scratch in place of z, and the reverse (jet_sin_adjoint_d) is
+// linear in them: no sine, cosine or range reduction (the adjoint epilogue was 3.3 VALU per MFMA).
+// Per-lane coefficients dA = w [s == 0], dB = w^2 [s != 0], dC = w^3 [s == 3]: D = dA c + dB s z + dC c (z_1^2 + z_2^2).
+__device__ __forceinline__ f32x4 jet_sin_d(const f32x4& z, float w, float ka, float kb, float kg, float dA, float dB,
+                                           float dC, f32x4& D) {
+    f32x4 out;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float z0 = quad_bcast<0>(z[r]), t1 = quad_bcast<1>(z[r]), t2 = quad_bcast<2>(z[r]);
+        float sn, cs;
+        sincos_fast(w * z0, sn, cs);
+        const float q2 = __builtin_fmaf(t1, t1, t2 * t2);
+        out[r] = __builtin_fmaf(ka, sn, __builtin_fmaf(kb * cs, z[r], -(kg * sn) * q2));
+        D[r] = __builtin_fmaf(dA, cs, __builtin_fmaf(dB * sn, z[r], (dC * cs) * q2));
+    }
+    return out;
+}
+//   zb_3 = P u_3,  zb_i = P u_i - 2 R_i u_3,  zb_0 = P u_0 - (R_1 u_1 + R_2 u_2 + T u_3)      (m0 = [s == 0],
+// m12 = [s == 1 or 2]; the same cotangent as jet_sin_adjoint<false>)
+__device__ __forceinline__ f32x4 jet_sin_adjoint_d(const f32x4& u, const f32x4& D, float m0, float m12) {
+    f32x4 out;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float P = quad_bcast<0>(D[r]), u3 = quad_bcast<3>(u[r]);
+        const float e = D[r] * u[r];
+        const float rest = quad_bcast<1>(e) + quad_bcast<2>(e) + quad_bcast<3>(e);
+        out[r] = __builtin_fmaf(P, u[r], -__builtin_fmaf(m12, (2.f * D[r]) * u3, m0 * rest));
     }
     return out;
 }

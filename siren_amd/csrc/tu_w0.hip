@@ -21,6 +21,10 @@ void launch_w0(dim3 grid, hipStream_t st, const FusedArgs& a) {
 
 // MODE_FWDS: W0 + a_l tiles (a.abuf) and lane-major cos (a.dbuf) for the stored-forward W2 split
 void launch_w0s(dim3 grid, hipStream_t st, const FusedArgs& a) {
+    if (a.abuf == nullptr) {  // lane-major cos only
+        launch_w1_notile(MODE_FWDS, grid, st, a);
+        return;
+    }
 #define SIREN_L(LHV)                                                                                             \
     hipLaunchKernelGGL((w1_kernel<LHV, MODE_FWDS>), grid, dim3(THREADS), 0, st, a.ws, a.x, a.n, (const float*)nullptr, \
                        a.y, (float*)nullptr, a.d, a.o, a.w0, a.w, a.abuf, a.dbuf, a.n_pad, a.ws_bstride)

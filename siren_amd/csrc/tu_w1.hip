@@ -14,6 +14,8 @@ void launch_w1(int mode, dim3 grid, hipStream_t st, const FusedArgs& a) {
             case 2: SIREN_L(2, MODE_STORE); break;
             default: SIREN_L(3, MODE_STORE); break;
         }
+    } else if (mode == MODE_REV && a.dbuf == nullptr) {  // gx only
+        launch_w1_notile(MODE_REV, grid, st, a);
     } else if (mode == MODE_REV) {  // a.abuf = lane-major cos from MODE_FWDS, a.dbuf = delta tiles
         switch (a.lh) {
             case 1: SIREN_L(1, MODE_REV); break;

@@ -1,5 +1,5 @@
 // tu_w1deep.hip — the stored-split halves of the W1 kernel at 4..5 hidden layers (hidden 256): MODE_FWDS (forward +
-// lane-major cos, optional a_l tiles) and MODE_REV (reverse GEMMs from the stored cos). At these depths cos(w z_l) of
+// lane-major cos and a_l tiles) and MODE_REV (reverse GEMMs from the stored cos, delta tiles; tu_w1nt.hip without tiles). At these depths cos(w z_l) of
 // every layer no longer fits the register file beside the accumulators, so W1 / W2 / the kept W3 run through HBM
 // (siren_capi.hip deep()); one translation unit of its own so the fully unrolled bodies compile in parallel.
 #include "launch.h"

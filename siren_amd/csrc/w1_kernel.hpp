@@ -36,6 +36,7 @@
 
 #include "lds_ops.h"
 #include "siren_common.h"
+#include "tile_io.h"
 
 namespace siren {
 
@@ -67,7 +68,16 @@ constexpr int w1_epi_pair() {
            : (MODE & MODE_BASE) == MODE_JET ? W1_EPI_JET
                                              : W1_EPI_MEM;
 }
-static_assert(W1_EPI_MEM >= 4, "the REV cos prefetch lands at the mid-slice wait (pair 4)");
+// MODE_REV reloads the cos block of epilogue E at the mid-slice of slice E - W1_COS_LEAD (before that mid's ring issue)
+// into cq[E % W1_COS_SLOTS]. Lead 2 makes the mid-slice wait of slice E - 1 wait for it one slice after its issue; lead
+// 3 lets it ride with ring slice E (two slices); lead 4 lands it one slice before the slice that runs its epilogue, which
+// is what an epilogue placed ahead of the mid-slice wait (W1_EPI_MEM < 4) needs.
+#ifndef W1_COS_LEAD
+#define W1_COS_LEAD 3
+#endif
+constexpr int W1_COS_SLOTS = W1_COS_LEAD <= 3 ? 3 : 4;
+static_assert(W1_COS_LEAD >= 2 && W1_COS_LEAD <= 4, "cos reload lead of 2..4 slices");
+static_assert(W1_EPI_MEM >= 4 || W1_COS_LEAD >= 4, "an epilogue ahead of the mid-slice wait needs the cos lead of 4");
 
 enum { EPI_FIRST = 0, EPI_SINCOS = 1, EPI_SEED = 2, EPI_DELTA = 3 };
 
@@ -118,6 +128,81 @@ constexpr int gemm0() { return (MODE & MODE_BASE) == MODE_REV ? LH : 0; }
 template <int MODE>
 constexpr bool is_rev() { return (MODE & MODE_BASE) == MODE_REV; }
 
+// ---- the memory modes' epilogue stores (STORE / FWDS / REV) ----------------------------------------------------------
+// Epilogue E of a tile (E = (G - G0) NB + b builds block b of GEMM G's B operand; E % NB == 0 runs before the GEMM, the
+// others inside slice E - 1) writes its tile blocks (a_l: FIRST / SINCOS / STORE's SEED; delta_l: SEED / DELTA), and
+// FWDS its lane-major cos block. Every store is ONE inline-asm instruction, so the mid-slice wait of slice S counts the
+// ops issued after the ring slice it publishes exactly (w1_allow) instead of waiting for every store of the last two
+// epilogues. Tile blocks leave as the four 64 B dword pieces from the epilogue itself; W1_STAGE=1 instead transposes
+// them through LDS into one coalesced 1 KiB store flushed at the start of slice E (STORE / REV only: FWDS runs two
+// workgroups per CU and has no LDS left for the scratch), measured 1.5 % slower on the REV kernel of the image-fit
+// step (profiles/r05_w1_mem_ab.log).
+#ifndef W1_STAGE
+#define W1_STAGE 0
+#endif
+template <int MODE>
+constexpr bool w1_mem() {
+    return (MODE & MODE_BASE) == MODE_STORE || (MODE & MODE_BASE) == MODE_FWDS || (MODE & MODE_BASE) == MODE_REV;
+}
+template <int MODE>
+constexpr bool w1_staged() { return W1_STAGE != 0 && w1_mem<MODE>() && (MODE & MODE_BASE) != MODE_FWDS; }
+template <int MODE>
+constexpr bool w1_tiles() { return w1_mem<MODE>() && (MODE & MODE_NOTILE) == 0; }
+constexpr bool w1_mem_rt(int mode) {
+    return (mode & MODE_BASE) == MODE_STORE || (mode & MODE_BASE) == MODE_FWDS || (mode & MODE_BASE) == MODE_REV;
+}
+constexpr int w1_nslices(int lh, int mode) {
+    return (mode & MODE_BASE) == MODE_STORE || (mode & MODE_BASE) == MODE_W1 ? 2 * lh * NB : lh * NB;
+}
+// tile blocks epilogue E writes (STORE's SEED: a_L and delta_L)
+constexpr int w1_ntile(int e, int lh, int mode) {
+    if (!w1_mem_rt(mode) || (mode & MODE_NOTILE) != 0 || e < 0 || e >= w1_nslices(lh, mode)) return 0;
+    const int g = ((mode & MODE_BASE) == MODE_REV ? lh : 0) + e / NB;
+    return (mode & MODE_BASE) == MODE_STORE && g == lh ? 2 : 1;
+}
+// Vector-memory instructions of epilogue E by position in the slice sequence, in half slices (half 2 s: slice s before
+// its mid-slice wait, 2 s + 1: after it). The epilogue's own stores run at pair W1_EPI_MEM of slice E - 1 (E % NB == 0:
+// after slice E - 1, before the GEMM); its staged tile blocks leave at the start of slice E (half 2 E).
+constexpr int w1_direct(int e, int lh, int mode) {
+    if (e < 0 || e >= w1_nslices(lh, mode)) return 0;
+    return (W1_STAGE != 0 && (mode & MODE_BASE) != MODE_FWDS ? 0 : 4 * w1_ntile(e, lh, mode)) +
+           ((mode & MODE_BASE) == MODE_FWDS ? 1 : 0);
+}
+constexpr int w1_direct_half(int e) { return e % NB != 0 && W1_EPI_MEM < 4 ? 2 * (e - 1) : 2 * (e - 1) + 1; }
+constexpr int w1_ops_in_half(int h, int lh, int mode) {
+    int n = 0;
+    for (int e = h / 2; e <= h / 2 + 1; ++e)
+        if (w1_direct_half(e) == h) n += w1_direct(e, lh, mode);
+    if (h % 2 == 0 && W1_STAGE != 0 && (mode & MODE_BASE) != MODE_FWDS) n += w1_ntile(h / 2, lh, mode);
+    return n;
+}
+// s_waitcnt vmcnt allowance of slice S's mid-slice wait (S + 2 < NS): ring slice S + 1 (issued at the mid of S - 2) and,
+// in REV, the cos reload of the epilogue that runs before the next mid-slice wait (S + 1; S + 2 when the epilogue sits
+// ahead of the wait) must have landed; everything issued after the later of the two may stay in flight. The mid of m
+// issues the cos reload of epilogue m + W1_COS_LEAD, then ring slice m + 3. The first two slices of a tile count 4 (the
+// previous tile's serial tail or the prologue sits between: 4 waits for more than needed, never less).
+constexpr int w1_allow_rt(int S, int lh, int mode) {
+    if (!w1_mem_rt(mode) || S < 2) return 4;
+    const bool rev = (mode & MODE_BASE) == MODE_REV;
+    const int ns = w1_nslices(lh, mode);
+    const int need = S + 1 + (W1_EPI_MEM < 4 ? 1 : 0);  // REV: the cos reload that must have landed
+    const int mc = need - W1_COS_LEAD;                 // ... issued at this mid
+    int m0 = S - 2, n = 0;
+    if (rev && mc > S - 2) {
+        m0 = mc;
+        n += 4;  // that mid's ring issue, behind the cos reload
+    }
+    for (int h = 2 * m0 + 1; h <= 2 * S; ++h) n += w1_ops_in_half(h, lh, mode);
+    for (int m = m0 + 1; m < S; ++m) n += (rev && m + W1_COS_LEAD < ns ? 1 : 0) + 4;
+    return n;
+}
+template <int S, int LH, int MODE>
+constexpr int w1_allow() {
+    constexpr int n = w1_allow_rt(S, LH, MODE);
+    static_assert(n >= 0 && n < 64, "vmcnt is 6 bits");
+    return n;
+}
+
 template <int LH, int MODE>
 struct W1State {
     f32x4 act[NB];     // B operand of the current GEMM (filled one block ahead)
@@ -128,7 +213,8 @@ struct W1State {
     float xv[MAXD];    // this lane's coordinate
     float gyv[MAXO];   // this lane's output cotangent
     float yp[MAXO];    // partial y over this lane's neurons
-    f32x4 cq[3];       // MODE_REV: cos blocks of the next epilogues, prefetched two slices ahead (slot e % 3)
+    f32x4 cq[W1_COS_SLOTS];  // MODE_REV: cos blocks of the next epilogues (slot e % W1_COS_SLOTS, W1_COS_LEAD)
+    f32x4 tq[2];       // W1_STAGE: the last epilogue's tile blocks, transposed (stored at the start of the next slice)
 };
 
 struct W1Ctx {
@@ -141,12 +227,15 @@ struct W1Ctx {
     // undoes the first layer's scale in gx
     float w0, w, wsd, inv_s0;
     bool seed_ones;
-    float* abuf;  // STORE / FWDS: lane-adjusted tile base of layer 0; layer l at + l * lstride
+    float* abuf;  // STORE / FWDS: lane-adjusted tile base of layer 0; layer l at + l * lstride (the serial tails)
     float* dbuf;  // STORE / REV: delta tiles, same layout
-    float* cst;   // FWDS: this lane's cos store base (cos_off(tile, wave, LH, 0, 0, lane))
+    const char* ta;     // STORE / FWDS: wave-uniform a_l tile base of (tile, wave), layer 0; layer l at + l * lbytes
+    const char* td;     // STORE / REV: the same for the delta tiles
+    const char* cs;     // FWDS: wave-uniform lane-major cos base of (tile, wave) (cos_off(tile, wave, LH, 0, 0, 0))
     const char* cbase;  // REV: wave-uniform cos base of (tile, wave) (SGPRs), + 16 * lane per lane
-    bool dstore;        // REV: store the delta tiles (false: gx only — the stored jet forward's dPhi/dx)
-    bool astore;  // FWDS: a_l tiles wanted (abuf != NULL; the deep W1's forward half keeps only the lane-major cos)
+    unsigned vl, vt;    // this lane's byte offset: 16 lane (coalesced blocks), 4 (4 g 16 + c) (the 64 B pieces)
+    unsigned tw, tr;    // W1_STAGE: LDS transpose scratch of the wave, this lane's write / read address
+    int64_t lbytes;
     bool more;    // persistent grid: this workgroup runs another coordinate tile after the current one, so the
                   // ring keeps streaming (slices 0..2 of the next tile are issued during the last 3 slices)
     int64_t lstride;
@@ -174,13 +263,14 @@ __device__ __forceinline__ void ring_issue4(const float* __restrict__ stream, fl
 }
 
 // MODE_REV: cos block of epilogue index E (E = (G - LH) NB + b handles block b of reverse GEMM G's epilogue: layer
-// LH for the SEED epilogue G = LH, layer 2 LH - G for DELTA) as a saddr-form global_load_dwordx4 into cq[E % 3].
+// LH for the SEED epilogue G = LH, layer 2 LH - G for DELTA) as a saddr-form global_load_dwordx4 into
+// cq[E % W1_COS_SLOTS].
 // Issued before a ring issue, so the ring's counted s_waitcnt vmcnt(4) one slice later also covers it.
 template <int E, int LH, int MODE>
 __device__ __forceinline__ void cos_issue(W1State<LH, MODE>& st, const W1Ctx& cx) {
     constexpr int GE = LH + E / NB, BE = E % NB;
     constexpr int LC = GE == LH ? LH : 2 * LH - GE;
-    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(st.cq[E % 3]) : "v"(16u * cx.lane),
+    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(st.cq[E % W1_COS_SLOTS]) : "v"(16u * cx.lane),
                  "s"(cx.cbase + (LC * NB + BE) * 1024));
 }
 
@@ -212,6 +302,42 @@ __device__ __forceinline__ void epi_load(EpiParams<KIND, G, LH>& ep, const W1Ctx
 #pragma unroll
     for (int i = 0; i < epi_nparams<KIND>(); ++i)
         ep.v[i] = *(const f32x4*)((const char*)cx.sm + epi_param_off<KIND, G, LH>(i, b) + 16 * cx.g);
+}
+
+// Tile block b of an epilogue (layer base wave-uniform): staged into tq[K] for the flush at the start of the next slice,
+// or (FWDS) stored at once as the four 64 B pieces.
+// Byte offset of (layer l, block b) in a tile buffer. The layer stride is made opaque at each use: hipcc would otherwise
+// keep the products l * lbytes of every layer live in SGPRs across the tile (spilled to VGPR lanes).
+__device__ __forceinline__ int64_t w1_tile_off(const W1Ctx& cx, int l, int b) {
+    int64_t lb = cx.lbytes;
+    asm volatile("" : "+s"(lb));
+    return l * lb + b * 1024;
+}
+template <int MODE, int K, int LH>
+__device__ __forceinline__ void w1_tile_put(W1State<LH, MODE>& st, const W1Ctx& cx, const char* base, int l, int b,
+                                            const f32x4& v) {
+    if constexpr (w1_staged<MODE>())
+        w3_stage(st.tq[K], v, cx.tw, cx.tr);
+    else
+        w3_store_tile(w3_at(base, w1_tile_off(cx, l, b)), cx.vt, v);
+}
+
+// The staged tile blocks of epilogue E, stored at the start of slice E (after the lgkmcnt wait that retired them).
+template <int E, int LH, int MODE>
+__device__ __forceinline__ void w1_flush(W1State<LH, MODE>& st, const W1Ctx& cx) {
+    if constexpr (w1_staged<MODE>() && w1_ntile(E, LH, MODE) > 0) {
+        constexpr int GE = gemm0<MODE, LH>() + E / NB, BE = E % NB, K = epi_kind<GE, LH>();
+        constexpr int L = K == EPI_DELTA ? 2 * LH - GE : (K == EPI_SEED ? LH : GE);
+        if constexpr (w1_ntile(E, LH, MODE) == 2) {  // STORE's SEED: a_L, delta_L
+            asm volatile("" : "+v"(st.tq[0]), "+v"(st.tq[1]));
+            w3_store16(w3_at(cx.ta, w1_tile_off(cx, L, BE)), cx.vl, st.tq[0]);
+            w3_store16(w3_at(cx.td, w1_tile_off(cx, L, BE)), cx.vl, st.tq[1]);
+        } else {
+            asm volatile("" : "+v"(st.tq[0]));
+            const char* base = (K == EPI_FIRST || K == EPI_SINCOS) ? cx.ta : cx.td;
+            w3_store16(w3_at(base, w1_tile_off(cx, L, BE)), cx.vl, st.tq[0]);
+        }
+    }
 }
 
 // Epilogue for one 16-neuron block b of GEMM G (see the table at the top).
@@ -248,11 +374,8 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
             cs4[r] = cs;
         }
         if constexpr (!FWD) st.C[0][b] = pin(cs4);
-        if constexpr (STORE) store_block(cx.abuf, b, st.act[b]);
-        if constexpr (FWDS) {
-            if (cx.astore) store_block(cx.abuf, b, st.act[b]);
-        }
-        if constexpr (FWDS) *(f32x4*)(cx.cst + b * 256) = cs4;
+        if constexpr (w1_tiles<MODE>()) w1_tile_put<MODE, 0>(st, cx, cx.ta, 0, b, st.act[b]);
+        if constexpr (FWDS) w3_store16(w3_at(cx.cs, b * 1024), cx.vl, cs4);
     } else if constexpr (KIND == EPI_SINCOS) {
         const f32x4 z = st.acc[(G + 1) & 1][b] + ep.v[0];
         f32x4 cs4;
@@ -264,21 +387,18 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
             cs4[r] = cs;
         }
         if constexpr (!FWD) st.C[G][b] = to_agpr(cs4);
-        if constexpr (STORE) store_block(cx.abuf + G * cx.lstride, b, st.act[b]);
-        if constexpr (FWDS) {
-            if (cx.astore) store_block(cx.abuf + G * cx.lstride, b, st.act[b]);
-        }
-        if constexpr (FWDS) *(f32x4*)(cx.cst + (G * NB + b) * 256) = cs4;
+        if constexpr (w1_tiles<MODE>()) w1_tile_put<MODE, 0>(st, cx, cx.ta, G, b, st.act[b]);
+        if constexpr (FWDS) w3_store16(w3_at(cx.cs, (G * NB + b) * 1024), cx.vl, cs4);
     } else if constexpr (KIND == EPI_SEED && REV) {
         // delta_L = (gy Wout) . cos(w z_L) . w with cos from the forward's store
-        const f32x4 cs = st.cq[((G - LH) * NB + b) % 3];
+        const f32x4 cs = st.cq[((G - LH) * NB + b) % W1_COS_SLOTS];
         f32x4 ga = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < MAXO; ++j)
             if (j < cx.o && !cx.seed_ones) ga += st.gyv[j] * ep.v[1 + j];
         if (cx.seed_ones) ga = ep.v[5];
         st.act[b] = (ga * cs) * opaque(cx.wsd);
-        if (cx.dstore) store_block(cx.dbuf + LH * cx.lstride, b, st.act[b]);
+        if constexpr (w1_tiles<MODE>()) w1_tile_put<MODE, 0>(st, cx, cx.td, LH, b, st.act[b]);
     } else if constexpr (KIND == EPI_SEED) {
         const f32x4 z = st.acc[(G + 1) & 1][b] + ep.v[0];
         f32x4 sn, cs;
@@ -289,7 +409,7 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
             sn[r] = a;
             cs[r] = c;
         }
-        if constexpr (STORE) store_block(cx.abuf + LH * cx.lstride, b, sn);
+        if constexpr (STORE) w1_tile_put<MODE, 0>(st, cx, cx.ta, LH, b, sn);
         f32x4 ga = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < MAXO; ++j) {
@@ -301,17 +421,14 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
         }
         if (cx.seed_ones) ga = ep.v[5];
         st.act[b] = (ga * cs) * opaque(cx.wsd);
-        if constexpr (STORE) store_block(cx.dbuf + LH * cx.lstride, b, st.act[b]);
+        if constexpr (STORE) w1_tile_put<MODE, 1>(st, cx, cx.td, LH, b, st.act[b]);
     } else {
         constexpr int L = 2 * LH - G;  // delta_L = u_L . cos(w z_L) . w,  1 <= L < LH
         if constexpr (REV)
-            st.act[b] = (st.acc[(G + 1) & 1][b] * st.cq[((G - LH) * NB + b) % 3]) * cx.w;
+            st.act[b] = (st.acc[(G + 1) & 1][b] * st.cq[((G - LH) * NB + b) % W1_COS_SLOTS]) * cx.w;
         else
             st.act[b] = (st.acc[(G + 1) & 1][b] * from_agpr(st.C[L][b])) * cx.w;
-        if constexpr (STORE) store_block(cx.dbuf + L * cx.lstride, b, st.act[b]);
-        if constexpr (REV) {
-            if (cx.dstore) store_block(cx.dbuf + L * cx.lstride, b, st.act[b]);
-        }
+        if constexpr (w1_tiles<MODE>()) w1_tile_put<MODE, 0>(st, cx, cx.td, L, b, st.act[b]);
     }
 }
 
@@ -339,9 +456,9 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
             // tile are the next tile's slices 0..2 (NS is a multiple of the ring size, so the slots line up).
             if (S + 1 < NS || cx.more) {
                 if constexpr (S + 2 < NS) {
-                    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(w1_allow<S, LH, MODE>()) : "memory");
                 } else if constexpr (is_rev<MODE>() && S + 2 == NS) {
-                    // the last epilogue's cos block (issued at slice NS - 3) is retired whether or not the next
+                    // the last epilogue's cos block (issued W1_COS_LEAD slices earlier) is retired whether or not the next
                     // tile's ring slices were issued behind it: one wait shape on every path (a `more`-dependent
                     // vmcnt(4) / vmcnt(0) pair compiles into branches the static ISA check cannot correlate)
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -351,9 +468,10 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
                 if constexpr (is_rev<MODE>()) {
-                    // the cos block issued one slice ago (epilogue S + 1) has landed; prefetch epilogue S + 2's
-                    asm volatile("" : "+v"(st.cq[(S + 1) % 3]));
-                    if constexpr (S + 2 < NS) cos_issue<S + 2, LH, MODE>(st, cx);
+                    // the cos block of the epilogue before the next mid-slice wait has landed; reload epilogue S + W1_COS_LEAD's
+                    constexpr int NEED = S + 1 + (W1_EPI_MEM < 4 ? 1 : 0);
+                    if constexpr (NEED < NS) asm volatile("" : "+v"(st.cq[NEED % W1_COS_SLOTS]));
+                    if constexpr (S + W1_COS_LEAD < NS) cos_issue<S + W1_COS_LEAD, LH, MODE>(st, cx);
                 }
                 __builtin_amdgcn_s_barrier();
                 if (S + 3 < NS || cx.more) {
@@ -389,6 +507,7 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
 #pragma unroll
             for (int i = 0; i < epi_nparams<KIND>(); ++i) asm volatile("" : "+v"(ep.v[i]));
         }
+        if constexpr (p == 0) w1_flush<S, LH, MODE>(st, cx);  // the wait above retired the transpose
         if constexpr (p == EPI_AT && EPI) {
             __builtin_amdgcn_sched_barrier(0);
             w1_epilogue<G, LH, MODE>(st, cx, KB + 1, ep);
@@ -453,7 +572,8 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
     constexpr bool FWDS = (MODE & MODE_BASE) == MODE_FWDS;  // abuf = a_l tiles, dbuf = lane-major cos buffer
     constexpr bool REV = is_rev<MODE>();                     // abuf = lane-major cos buffer, dbuf = delta tiles
     constexpr int NS = npasses<MODE>() * LH * NB;
-    __shared__ __attribute__((aligned(16))) float lds[W1_NBUF * SLICE + small_floats_ct(LH)];
+    constexpr int SMALL4 = (small_floats_ct(LH) + 3) / 4 * 4;
+    __shared__ __attribute__((aligned(16))) float lds[W1_NBUF * SLICE + SMALL4 + (w1_staged<MODE>() ? WAVES * STB_SCRATCH : 0)];
     W1Ctx cx;
     W1State<LH, MODE> st;
     cx.ring = lds;
@@ -497,16 +617,23 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
         cx.inv_s0 = two_pi / w0;
     }
     cx.seed_ones = gy == nullptr;
-    cx.dstore = dbuf != nullptr;
     cx.abuf = cx.dbuf = nullptr;
+    cx.ta = cx.td = cx.cs = nullptr;
     cx.more = false;
-    cx.astore = abuf != nullptr;
     cx.prof = nullptr;
     cx.stream = ws + small_pad(LH) + (REV ? (int64_t)LH * NB * SLICE : 0);
     cx.lstride = n_pad * H;
     const unsigned lds_base = (unsigned)(uintptr_t)((__attribute__((address_space(3))) float*)lds);
     cx.ring_vaddr = lds_base + cx.lane * 16;
     cx.sm_vaddr = lds_base + W1_NBUF * SLICE * 4 + 16 * cx.g;
+    cx.lbytes = cx.lstride * 4;
+    cx.vl = 16u * cx.lane;
+    cx.vt = 4u * (4 * cx.g * 16 + c);
+    {
+        const unsigned scr = lds_base + 4u * (W1_NBUF * SLICE + SMALL4 + cx.wave * STB_SCRATCH);
+        cx.tw = scr + 4u * (4 * cx.g * STB_ROW + c);                      // row 4 g + r (r by the offsets), column c
+        cx.tr = scr + 4u * ((cx.lane >> 2) * STB_ROW + 4 * (cx.lane & 3));  // row lane / 4, columns 4 (lane & 3)
+    }
 
     {
         const int nf4 = (small_floats(LH) + 3) / 4;
@@ -566,18 +693,26 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
 #pragma unroll
             for (int k = 0; k < MAXD; ++k) cx.jcf[k] = cx.ja * st.xv[k] + (js == k + 1 ? 1.f : 0.f);
         }
-        if constexpr (STORE || FWDS || REV) {
-            const int64_t toff = (tile * WAVES + cx.wave) * (H * 16) + 4 * cx.g * 16 + c;
-            if constexpr (!REV) cx.abuf = abuf + toff;
-            if constexpr (!FWDS) cx.dbuf = dbuf + toff;
+        if constexpr (w1_tiles<MODE>()) {
+            const int64_t tbase = (tile * WAVES + cx.wave) * (H * 16);  // wave-uniform
+            const int64_t toff = tbase + 4 * cx.g * 16 + c;
+            if constexpr (!REV) {
+                cx.abuf = abuf + toff;
+                cx.ta = (const char*)(abuf + tbase);
+            }
+            if constexpr (!FWDS) {
+                cx.dbuf = dbuf + toff;
+                cx.td = (const char*)(dbuf + tbase);
+            }
         }
-        if constexpr (FWDS) cx.cst = dbuf + cos_off(tile, cx.wave, LH, 0, 0, cx.lane);
+        if constexpr (FWDS) cx.cs = (const char*)(dbuf + cos_off(tile, cx.wave, LH, 0, 0, 0));
         if constexpr (REV) {
             // cos blocks of the first two epilogues (SEED blocks 0, 1); later ones are prefetched by the slices
             cx.cbase = (const char*)(abuf + cos_off(tile, cx.wave, LH, 0, 0, 0));
-            cos_issue<0, LH, MODE>(st, cx);
-            cos_issue<1, LH, MODE>(st, cx);
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(st.cq[0]), "+v"(st.cq[1])::"memory");
+            static_for<0, W1_COS_LEAD>([&](auto E) { cos_issue<decltype(E)::value, LH, MODE>(st, cx); });
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int e = 0; e < W1_COS_LEAD; ++e) asm volatile("" : "+v"(st.cq[e]));
         }
 
         if constexpr ((MODE & MODE_PROF) != 0) {
@@ -634,8 +769,8 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
                     cs4[r] = cc;
                 }
                 if constexpr (FWDS) {
-                    if (cx.astore) store_block(cx.abuf + LH * cx.lstride, rb, sn);
-                    *(f32x4*)(cx.cst + (LH * NB + rb) * 256) = cs4;
+                    if constexpr (w1_tiles<MODE>()) store_block(cx.abuf + LH * cx.lstride, rb, sn);
+                    w3_store16(w3_at(cx.cs, (LH * NB + rb) * 1024), cx.vl, cs4);
                 }
 #pragma unroll
                 for (int j = 0; j < MAXO; ++j) {
@@ -672,10 +807,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
 #pragma unroll
                 for (int rb = 0; rb < NB; ++rb) st.act[rb] = (st.acc[GL][rb] * st.C[0][rb]) * cx.w0;
             }
-            if constexpr (STORE) store_tile(cx.dbuf, st.act);
-            if constexpr (REV) {
-                if (cx.dstore) store_tile(cx.dbuf, st.act);
-            }
+            if constexpr (w1_tiles<MODE>()) store_tile(cx.dbuf, st.act);
 #pragma unroll
             for (int k = 0; k < MAXD; ++k) {
                 if (k < d) {

@@ -17,7 +17,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, 'siren_amd', 'csrc')
-TUS = ['tu_w1.hip', 'tu_w1deep.hip', 'tu_w0.hip', 'tu_w4.hip', 'tu_w3.hip', 'tu_wide.hip', 'tu_jet.hip', 'tu_wide_jet.hip',
+TUS = ['tu_w1.hip', 'tu_w1deep.hip', 'tu_w1nt.hip', 'tu_w0.hip', 'tu_w4.hip', 'tu_w3.hip', 'tu_wide.hip', 'tu_jet.hip', 'tu_wide_jet.hip',
        'tu_train.hip', 'tu_w1x.hip', 'tu_hess.hip', 'tu_w3i_tt.hip', 'tu_w3i_tf.hip', 'tu_w3i_ft.hip', 'tu_w3i_ff.hip',
        'tu_qfi.hip', 'tu_widei_fa.hip', 'tu_widei_ra.hip']
 

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Kernel time of the kernels matching a name filter on one profile_paths path, for the product library and then every
 # A/B library tools/probe/lib_*.so (built by tools/variant_build.sh): one rocprofv3 kernel trace per library.
-# usage (gpurun, from the repo root): bash tools/lib_ab.sh <name filter> <path>
+# usage (gpurun, from the repo root): [REPS=n] bash tools/lib_ab.sh <name filter> <path>
 set -o pipefail
 F=$1; P=$2
 R=$PWD
@@ -10,7 +10,7 @@ mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 for lib in product $(ls $R/tools/probe/lib_*.so 2>/dev/null); do
   if [ "$lib" = product ]; then t=product; unset SIREN_AMD_LIB; else t=$(basename $lib .so); export SIREN_AMD_LIB=$lib; fi
-  timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$t -o run -- python3 $R/tools/profile_paths.py $P > $O/$t.log 2>&1 || { echo "$t failed"; tail -5 $O/$t.log; exit 1; }
+  timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$t -o run -- python3 $R/tools/profile_paths.py $P --reps ${REPS:-5} > $O/$t.log 2>&1 || { echo "$t failed"; tail -5 $O/$t.log; exit 1; }
   python3 - "$O/$t" "$F" "$t" <<'PY'
 import csv, glob, sys
 f = glob.glob(sys.argv[1] + '/**/run_kernel_stats.csv', recursive=True)
