@@ -226,6 +226,48 @@ def split_leg(eng, flat, x, steps, warmup):
             'parity': 'tests/test_gpu_split.py: G1/G2 reference goldens vs fp64 within the fp32 kernel\'s error'}
 
 
+# the bf16x6 W2 unit per coordinate on the bf16 pipe: forward (LH H^2), recomputed forward + reverse (2 LH H^2) and
+# the hidden wgrad (LH H^2), six products each
+SPLIT_TRAIN_MFMA_FLOP = 6 * 2 * 4 * 3 * 256 * 256
+
+
+def split_train_leg(device, fp32_rate, n=1 << 18):
+    """image_mse training with precision='bf16x6' (the drop-in module, Adam included) at the image_w2 size, beside the
+    fp32 step's rate, with the split kernels' durations from a trace-free HIP-event timing of one backward."""
+    from siren_amd.engine import SirenEngine
+    rate = train_step_rate(device, n=n, precision='bf16x6')
+    eng = SirenEngine(2, 256, 3, 1, 30., 30., True)
+    torch.manual_seed(0)
+    from siren_amd.modules import FCBlock
+    net = FCBlock(2, 1, 3, 256, outermost_linear=True, nonlinearity='sine')
+    flat = torch.cat([p.detach().reshape(-1) for p in net.parameters()]).to(device)
+    x = torch.rand(n, 2, device=device) * 2 - 1
+    gy = torch.randn(n, 1, device=device) / n
+    st = torch.cuda.current_stream()
+    wsx = eng.pack_split(flat)
+    times = {}
+    for name, fn in (('forward_split', lambda: eng.forward_split(wsx, x)),
+                     ('backward_split', lambda: eng.backward_split(wsx, x, gy))):
+        fn()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+        for a, b in ev:
+            a.record(st)
+            fn()
+            b.record(st)
+        torch.cuda.synchronize()
+        times[name] = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    unit_ms = times['forward_split'] + times['backward_split']
+    achieved = SPLIT_TRAIN_MFMA_FLOP * n / (unit_ms * 1e-3) / 1e12
+    return {'value': round(rate, 3), 'unit': 'Mcoords/s', 'fp32_value': fp32_rate,
+            'speedup_vs_fp32': round(rate / fp32_rate, 3) if fp32_rate else None,
+            'forward_ms': round(times['forward_split'], 4), 'backward_ms': round(times['backward_split'], 4),
+            'roofline': {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': PEAK_BF16_MFMA_TFLOPS,
+                         'unit': 'TFLOP/s', 'frac': round(achieved / PEAK_BF16_MFMA_TFLOPS, 4),
+                         'flop_per_coord': SPLIT_TRAIN_MFMA_FLOP,
+                         'note': 'forward + backward launches (split W0, split store, bf16x6 wgrad, edge, reduce)'},
+            'parity': 'tests/test_gpu_split.py: G1 image_mse theta-grads vs fp64 within the fp32 pipeline\'s error'}
+
+
 HEADLINE_KERNEL = 'w1_kernel<3,640>'   # MODE_W1 | MODE_O1S | MODE_D(2), as tools/pmc_summary.py shortens it
 PMC_FILE = os.path.join(ROOT, 'profiles', 'pmc_headline.json')
 
@@ -251,11 +293,12 @@ def pmc_traffic(n):
     return None, 'profiles/pmc_headline.json lacks %s at n=%d' % (HEADLINE_KERNEL, n)
 
 
-def train_step_rate(device, n=1 << 18, steps=10, warmup=3):
-    """W2: image_mse training steps (fused forward, fused backward + MFMA wgrad, Adam) in Mcoords/s."""
+def train_step_rate(device, n=1 << 18, steps=10, warmup=3, precision='fp32'):
+    """W2: image_mse training steps (fused forward, fused backward + MFMA wgrad, Adam) in Mcoords/s. precision
+    'bf16x6': the split-bf16 leg (split W0 forward, siren_backward_split: split-bf16 recompute + reverse, bf16x6 wgrad)."""
     from siren_amd.modules import SingleBVPNet
     torch.manual_seed(0)
-    model = SingleBVPNet(verbose=False, jet=False).to(device)
+    model = SingleBVPNet(verbose=False, jet=False, precision=precision).to(device)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     x = torch.rand(1, n, 2, device=device) * 2 - 1
     gt = torch.sin(5 * x[..., :1])
@@ -657,6 +700,8 @@ def main():
     extra = {}
     if rank == 0 and not args.no_extra:
         extra['w2_image_mse_train_mcoords_s'] = round(train_step_rate(device), 3)
+        if split is not None:  # the opt-in bf16x6 training leg beside the fp32 one
+            split['train_w2_image_mse'] = split_train_leg(device, extra['w2_image_mse_train_mcoords_s'])
         # config 2's own N (2^20 coordinates per step) beside the 2^18 leg the per-path profile is taken at
         extra['w2_image_mse_train_n2p20_mcoords_s'] = round(train_step_rate(device, n=1 << 20), 3)
         extra['configs'] = config_rates(device)

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SIREN_ABI_VERSION 6
+#define SIREN_ABI_VERSION 7
 
 enum {
     SIREN_OK = 0,
@@ -257,6 +257,13 @@ int32_t siren_forward_grad_split(const siren_cfg* cfg, const float* wsx, const f
 /* The forward-only W0 (model_out, SingleBVPNet.forward modules.py:143-160) on the same split image: the forward GEMMs
  * only, two waves per SIMD sharing one weight ring (dense evaluation: sdf_meshing.create_mesh, summaries). */
 int32_t siren_forward_split(const siren_cfg* cfg, const float* wsx, const float* x, int64_t n, float* y, void* stream);
+/* The training backward of the bf16x6 leg (precision='bf16x6' under a parameter-gradient graph: the image-fit W2 unit
+ * with siren_forward_split as its forward): the split-bf16 kernel recomputes the forward, runs the reverse seeded with
+ * gy (n) and writes a_l / delta_l tiles, then the fp32 split-K MFMA wgrad, edge layers and slab reduction of
+ * siren_backward. Replaces siren_backward(cfg, ws, x, n, gy, tws, NULL, gx, gparams, stream) for the networks
+ * siren_forward_grad_split covers; gx (n, d_in) nullable; tws: siren_train_ws_floats(cfg, n) floats. */
+int32_t siren_backward_split(const siren_cfg* cfg, const float* wsx, const float* x, int64_t n, const float* gy,
+                             float* tws, float* gx, float* gparams, void* stream);
 
 /* Diagnostics: the W1 kernel (hidden 256, 3 hidden layers) with s_memtime stamps. stamps receives
  * 256 workgroups x 4 tiles x 4 waves x 8 events (uint64; event 0 tile start, 1..6 after GEMM 0..5, 7 tile end);

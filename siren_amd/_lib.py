@@ -11,7 +11,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('SIREN_AMD_LIB', os.path.join(_HERE, 'libsiren_amd.so'))
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 # Error codes (include/siren_amd.h)
 SIREN_OK, SIREN_EINVAL, SIREN_EUNSUPPORTED, SIREN_EHIP = 0, 1, 2, 3
@@ -82,6 +82,7 @@ _SIGS = {
     'siren_pack_split': [_CFG, _P, _P, _P],
     'siren_forward_grad_split': [_CFG, _P, _P, _I64, _P, _P, _P],
     'siren_forward_split': [_CFG, _P, _P, _I64, _P, _P],
+    'siren_backward_split': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P],
     'siren_hessian_backward_ws_floats': [_CFG, _I64, ctypes.POINTER(_I64)],
     'siren_hessian_backward': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P],
     'siren_hessian_ws_floats': [_CFG, _I64, ctypes.c_int32, ctypes.POINTER(_I64)],

@@ -168,6 +168,45 @@ class SirenFunction(torch.autograd.Function):
         return None, None, gx, gp, None
 
 
+class SirenSplitFunction(torch.autograd.Function):
+    """precision 'bf16x6' under a parameter-gradient graph (the image-fit training step): y from the
+    split-bf16 forward (siren_forward_split); the backward recomputes the forward on the split-bf16 kernel, runs the
+    reverse from gy and reduces the θ-gradients with the fp32 MFMA wgrad (siren_backward_split). An x-only or
+    create_graph backward runs on the fp32 kernels (the split kernels cover gy = ones / first order only)."""
+
+    @staticmethod
+    def forward(ctx, engine, jet, x, flat):
+        wsx = engine.pack_split(flat)
+        y = engine.forward_split(wsx, x)
+        # the fp32 image too: a derivative of y (diff_operators.gradient / laplace through siren_node_of) runs on the
+        # fp32 kernels
+        ctx.engine, ctx.jet, ctx.wsx, ctx.ws = engine, jet, wsx, engine.pack(flat)
+        ctx.save_for_backward(x, flat)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, flat = ctx.saved_tensors
+        engine, ws = ctx.engine, ctx.ws
+        need_x = ctx.needs_input_grad[2] and _will_execute(ctx, 0)
+        need_p = ctx.needs_input_grad[3] and _will_execute(ctx, 1)
+        gx = gp = None
+        gy = gy.contiguous()
+        if not torch.is_grad_enabled():
+            if need_p:
+                gx, gp = engine.backward_split(ctx.wsx, x, gy, want_gx=need_x)
+            elif need_x:
+                _, gx = engine.forward_grad(ws, x, gy, want_y=False)
+            return None, None, gx, gp
+        if need_x:
+            if ctx.jet is not None and not need_p:
+                ctx.jet.observe_x_gradient_request()
+            gx = SirenVJP.apply(engine, ws, x, flat, gy)
+        if need_p:
+            gp = _torch_path.vjp_params(engine.cfg, x, flat, gy, create_graph=True)
+        return None, None, gx, gp
+
+
 class SirenJetFunction(torch.autograd.Function):
     """(y, J) = (Phi(x; theta), dPhi/dx) for d_out == 1 from ONE W1 launch, as ONE graph node with two outputs.
 
@@ -586,7 +625,7 @@ def siren_node_of(y, x):
         if node is None:
             return None
         name = type(node).__name__
-        if name in ('SirenFunctionBackward', 'SirenJetFunctionBackward'):
+        if name in ('SirenFunctionBackward', 'SirenJetFunctionBackward', 'SirenSplitFunctionBackward'):
             break
         if name not in _VIEW_NODES:
             return None

@@ -44,6 +44,14 @@ int64_t split_stream_words(int lh);
 void launch_pack_split(const float* p, unsigned* stream, int d, int o, int lh, float s, hipStream_t st);
 void launch_w1x(dim3 grid, hipStream_t st, const float* ws_small, const unsigned* stream, const float* x, int64_t n,
                 float* y, float* gx, int d, float w0, float w);
+// the W2 stage of the bf16x6 training leg (forward recompute + reverse from gy (n), a_l / delta_l tiles into abuf / dbuf
+// of L + 1 layers of n_pad H floats; gx nullable)
+void launch_w1x_store(dim3 grid, hipStream_t st, const float* ws_small, const unsigned* stream, const float* x,
+                      int64_t n, const float* gy, float* y, float* gx, float* abuf, float* dbuf, int64_t n_pad, int d,
+                      float w0, float w);
+// its hidden-layer weight gradient on the bf16 pipe (wgradx_kernel.hpp): grid (S, LH), tps even, slabs as launch_wgrad
+void launch_wgradx(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, int64_t n_pad, int64_t tps,
+                   float* partial, int64_t P, int d, int o, int lh);
 // the forward-only split W0 (8 waves, 128 coordinates per workgroup tile)
 int split_fwd_tile();
 void launch_w0x(dim3 grid, hipStream_t st, const float* ws_small, const unsigned* stream, const float* x, int64_t n,

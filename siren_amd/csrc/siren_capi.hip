@@ -397,6 +397,40 @@ int32_t siren_forward_split(const siren_cfg* cfg, const float* wsx, const float*
     return hip_status("siren_forward_split");
 }
 
+int32_t siren_backward_split(const siren_cfg* cfg, const float* wsx, const float* x, int64_t n, const float* gy,
+                             float* tws, float* gx, float* gparams, void* stream) {
+    if (int rc = split_ok(cfg)) return rc;
+    if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    if (gparams == nullptr) return fail(SIREN_EINVAL, "gparams is NULL");
+    const hipStream_t st = (hipStream_t)stream;
+    const int64_t P = param_count(cfg);
+    if (n == 0) {  // empty tensors may carry NULL data pointers: only gparams is written
+        (void)hipMemsetAsync(gparams, 0, P * sizeof(float), st);
+        return hip_status("siren_backward_split");
+    }
+    if (wsx == nullptr || x == nullptr || gy == nullptr || tws == nullptr) return fail(SIREN_EINVAL, "wsx/x/gy/tws is NULL");
+    const TrainPlan plan(cfg, n);
+    if (plan.n_pad / siren::TILE > 0x7fffffffll) return fail(SIREN_EINVAL, "n too large");
+    float* abuf = tws;
+    float* dbuf = tws + plan.act_floats;
+    float* partial = tws + 2 * plan.act_floats;
+    const int64_t spad = small_pad(cfg);
+    siren::launch_w1x_store(tile_grid(cfg, plan.n_pad / siren::TILE, 1), st, wsx + spad,
+                            (const unsigned*)(wsx + 2 * spad), x, n, gy, nullptr, gx, abuf, dbuf, plan.n_pad,
+                            cfg->d_in, cfg->omega_first, cfg->omega_hidden);
+    if (int rc = hip_status("siren_backward_split (split store)")) return rc;
+    // the bf16 wgrad takes whole tile pairs: tps rounded up to even (fewer splits, within the planned slabs)
+    const int64_t tpx = plan.tps + (plan.tps & 1), sx = (plan.tiles + tpx - 1) / tpx;
+    siren::launch_wgradx(dim3((unsigned)sx, (unsigned)cfg->n_hidden), st, abuf, dbuf, plan.n_pad, tpx, partial, P,
+                         cfg->d_in, cfg->d_out, cfg->n_hidden);
+    if (int rc = hip_status("siren_backward_split (wgrad)")) return rc;
+    siren::launch_small(plan.es.grid(cfg), st, abuf, dbuf, x, gy, n, plan.n_pad, plan.es.tps, partial + plan.eslab_off,
+                        plan.es.E, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden);
+    if (int rc = hip_status("siren_backward_split (small)")) return rc;
+    return finish_grads(cfg, st, partial, sx, 0, partial + plan.eslab_off, plan.es, gparams,
+                        "siren_backward_split (reduce)");
+}
+
 // diagnostics: while set, W3 launches record s_memtime phase stamps (w3_kernel.hpp) into stamps[256][16]
 static unsigned long long* g_w3_prof = nullptr;
 int32_t siren_w3_phase_profile(uint64_t* stamps) {

@@ -1,6 +1,7 @@
 // tu_w1x.hip — the split-bf16 W1 kernel (w1x_kernel.hpp) and its weight pack.
 #include "launch.h"
 #include "w1x_kernel.hpp"
+#include "wgradx_kernel.hpp"
 
 namespace siren {
 
@@ -15,11 +16,27 @@ void launch_pack_split(const float* p, unsigned* stream, int d, int o, int lh, f
 void launch_w1x(dim3 grid, hipStream_t st, const float* ws_small, const unsigned* stream, const float* x, int64_t n,
                 float* y, float* gx, int d, float w0, float w) {
     if (d == 2)
-        hipLaunchKernelGGL((w1x_kernel<3, 2, false>), grid, dim3(64 * x_waves<false>()), 0, st, ws_small, stream, x, n,
+        hipLaunchKernelGGL((w1x_kernel<3, 2, X_W1>), grid, dim3(64 * x_waves<false>()), 0, st, ws_small, stream, x, n,
                            y, gx, w0, w);
     else
-        hipLaunchKernelGGL((w1x_kernel<3, 3, false>), grid, dim3(64 * x_waves<false>()), 0, st, ws_small, stream, x, n,
+        hipLaunchKernelGGL((w1x_kernel<3, 3, X_W1>), grid, dim3(64 * x_waves<false>()), 0, st, ws_small, stream, x, n,
                            y, gx, w0, w);
+}
+
+void launch_w1x_store(dim3 grid, hipStream_t st, const float* ws_small, const unsigned* stream, const float* x,
+                      int64_t n, const float* gy, float* y, float* gx, float* abuf, float* dbuf, int64_t n_pad, int d,
+                      float w0, float w) {
+    if (d == 2)
+        hipLaunchKernelGGL((w1x_kernel<3, 2, X_STORE>), grid, dim3(64 * x_waves<false>()), 0, st, ws_small, stream, x,
+                           n, y, gx, w0, w, gy, abuf, dbuf, n_pad);
+    else
+        hipLaunchKernelGGL((w1x_kernel<3, 3, X_STORE>), grid, dim3(64 * x_waves<false>()), 0, st, ws_small, stream, x,
+                           n, y, gx, w0, w, gy, abuf, dbuf, n_pad);
+}
+
+void launch_wgradx(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, int64_t n_pad, int64_t tps,
+                   float* partial, int64_t P, int d, int o, int lh) {
+    hipLaunchKernelGGL(wgradx_kernel, grid, dim3(THREADS), 0, st, abuf, dbuf, n_pad, tps, partial, P, d, o, lh);
 }
 
 int split_fwd_tile() { return 16 * x_waves<true>(); }
@@ -27,10 +44,10 @@ int split_fwd_tile() { return 16 * x_waves<true>(); }
 void launch_w0x(dim3 grid, hipStream_t st, const float* ws_small, const unsigned* stream, const float* x, int64_t n,
                 float* y, int d, float w0, float w) {
     if (d == 2)
-        hipLaunchKernelGGL((w1x_kernel<3, 2, true>), grid, dim3(64 * x_waves<true>()), 0, st, ws_small, stream, x, n,
+        hipLaunchKernelGGL((w1x_kernel<3, 2, X_FWD>), grid, dim3(64 * x_waves<true>()), 0, st, ws_small, stream, x, n,
                            y, (float*)nullptr, w0, w);
     else
-        hipLaunchKernelGGL((w1x_kernel<3, 3, true>), grid, dim3(64 * x_waves<true>()), 0, st, ws_small, stream, x, n,
+        hipLaunchKernelGGL((w1x_kernel<3, 3, X_FWD>), grid, dim3(64 * x_waves<true>()), 0, st, ws_small, stream, x, n,
                            y, (float*)nullptr, w0, w);
 }
 

@@ -31,10 +31,16 @@
 
 #include "lds_ops.h"
 #include "siren_common.h"
+#include "tile_io.h"
 
 namespace siren {
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// kernel modes: W1 (y, gx with gy = ones), FWD (the forward-only W0, 8 waves), STORE (the W2 stage of the bf16x6
+// training leg: the forward recomputed, the reverse seeded with a per-coordinate gy (d_out 1), and a_l / delta_l written
+// as 16-coordinate tiles in the wgrad layout, as w1_kernel MODE_STORE)
+enum { X_W1 = 0, X_FWD = 1, X_STORE = 2 };
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int X_OBS = 8;                            // output blocks per slice (half a K-step)
@@ -87,6 +93,7 @@ __device__ __forceinline__ void split_block(const f32x4& v, u32x4 (&p)[3]) {
 
 template <int LH>
 struct XState {
+    float gyv;         // X_STORE: this lane's output cotangent
     u32x4 bx[2][3];    // B operand pieces (hi, mid, lo) of K-step s in bx[s & 1]
     f32x4 acc[2][NB];  // ping-pong accumulators (GEMM G in acc[G & 1])
     f32x4 C[LH][NB];   // cos(w z_l), 1 <= l < LH (layer 0's is recomputed at the end: 64 fewer live registers)
@@ -102,6 +109,10 @@ struct XCtx {
     int d, wave, lane, g;
     float w0, w, wsd, inv_s0;
     bool more;
+    const char* ta;        // X_STORE: wave-uniform a_l tile base of (tile, wave), layer 0; layer l at + l * lbytes
+    const char* td;        // X_STORE: the same for delta_l
+    int64_t lbytes;
+    unsigned vt;           // X_STORE: this lane's byte offset in a tile block, 4 (4 g 16 + c)
     unsigned ring_vaddr;   // LDS byte address of this lane's 16 B in slot 0
     unsigned ring_vaddr2;  // ... in slot 2
 };
@@ -185,8 +196,43 @@ __device__ __forceinline__ f32x4 x_pin(f32x4 v) {
 
 // Epilogue of block B producing the B operand of GEMM E (see the table at the top; the previous GEMM's output is
 // acc[(E + 1) & 1]).
-template <int E, int B, int LH, int D, bool FWD>
+// X_STORE: tile block B of layer l (the four 64 B pieces of the lane, as w1_kernel's memory modes); the layer stride
+// is made opaque at each use so hipcc keeps no per-layer SGPR pairs live across the tile
+__device__ __forceinline__ void x_tile_store(const char* base, const XCtx& cx, int l, int b, const f32x4& v) {
+    int64_t lb = cx.lbytes;
+    asm volatile("" : "+s"(lb));
+    w3_store_tile(w3_at(base, l * lb + b * 1024), cx.vt, v);
+}
+// dword stores an epilogue producing GEMM E's B operand issues per block (X_STORE): a_E, and at E = LH also delta_L;
+// delta_{2 LH - E} beyond
+constexpr int x_epi_nst(int e, int lh) { return e == lh ? 8 : 4; }
+// stores of the in-slice epilogue of slice s (after its mid-slice wait: block 2 (KS + 1) + HALF of GEMM s / X_SPG's
+// input when KS + 1 < X_KSTEPS), and of the two pre-GEMM blocks run before slice s when s starts a GEMM
+constexpr int x_st_slice(int s, int lh) {
+    return (s < 0 || s >= x_slices(lh) || ((s % X_SPG) >> 1) + 1 >= X_KSTEPS) ? 0 : x_epi_nst(s / X_SPG, lh);
+}
+constexpr int x_st_pre(int s, int lh) {
+    return (s <= 0 || s >= x_slices(lh) || s % X_SPG != 0) ? 0 : 2 * x_epi_nst(s / X_SPG, lh);
+}
+// s_waitcnt vmcnt allowance of slice S's mid-slice wait (S + 2 < NS): ring slice S + 1 was issued at the mid of S - 2;
+// after it come the epilogue stores of S - 2, the pre-GEMM blocks before S - 1, ring slice S + 2 (CPW pieces), the
+// epilogue stores of S - 1 and the pre-GEMM blocks before S. The first two slices of a tile count CPW (the previous
+// tile's serial tail sits between: CPW waits for more than needed, never less).
+template <int S, int LH, int XM, int CPW>
+constexpr int x_allow() {
+    if constexpr (XM != X_STORE || S < 2) {
+        return CPW;
+    } else {
+        constexpr int n = CPW + x_st_slice(S - 2, LH) + x_st_pre(S - 1, LH) + x_st_slice(S - 1, LH) + x_st_pre(S, LH);
+        static_assert(n < 64, "vmcnt is 6 bits");
+        return n;
+    }
+}
+static_assert(X_EPI_AT >= 4, "the in-slice epilogue's stores are counted after the mid-slice wait");
+
+template <int E, int B, int LH, int D, int XM>
 __device__ __forceinline__ void x_epilogue(XState<LH>& st, const XCtx& cx) {
+    constexpr bool FWD = XM == X_FWD, ST = XM == X_STORE;
     constexpr int KS = B >> 1, HALF = B & 1;
     const int nb = 16 * B + 4 * cx.g;
     u32x4(&p)[3] = st.bx[KS & 1];
@@ -203,6 +249,7 @@ __device__ __forceinline__ void x_epilogue(XState<LH>& st, const XCtx& cx) {
             cs[r] = c_;
         }
         split_block<HALF>(sn, p);
+        if constexpr (ST) x_tile_store(cx.ta, cx, 0, B, sn);
     } else if constexpr (E < LH) {
         const f32x4 z = st.acc[(E + 1) & 1][B] + *(const f32x4*)(cx.sm + SM_BIAS + E * H + nb);
         f32x4 sn, cs;
@@ -215,6 +262,7 @@ __device__ __forceinline__ void x_epilogue(XState<LH>& st, const XCtx& cx) {
         }
         if constexpr (!FWD) st.C[E][B] = x_to_agpr(cs);
         split_block<HALF>(sn, p);
+        if constexpr (ST) x_tile_store(cx.ta, cx, E, B, sn);
     } else if constexpr (E == LH) {
         const f32x4 z = st.acc[(E + 1) & 1][B] + *(const f32x4*)(cx.sm + SM_BIAS + LH * H + nb);
         f32x4 sn, cs;
@@ -227,20 +275,28 @@ __device__ __forceinline__ void x_epilogue(XState<LH>& st, const XCtx& cx) {
         }
         const f32x4 wo = *(const f32x4*)(cx.sm + SM_WO + nb);
         st.yp += wo[0] * sn[0] + wo[1] * sn[1] + wo[2] * sn[2] + wo[3] * sn[3];
-        const f32x4 dl = (*(const f32x4*)(cx.sm + SM_SEED + nb) * cs) * cx.wsd;
+        // delta_L = (gy Wout) . cos . w (W1: gy = ones, the seed row sum_j Wout_j)
+        const f32x4 sd = ST ? opaque(st.gyv) * wo : *(const f32x4*)(cx.sm + SM_SEED + nb);
+        const f32x4 dl = (sd * cs) * cx.wsd;
         split_block<HALF>(dl, p);
+        if constexpr (ST) {
+            x_tile_store(cx.ta, cx, LH, B, sn);
+            x_tile_store(cx.td, cx, LH, B, dl);
+        }
     } else {
         constexpr int L = 2 * LH - E;  // delta_L = u_L . cos(w z_L) . w, 1 <= L < LH
         const f32x4 dl = (st.acc[(E + 1) & 1][B] * x_from_agpr(st.C[L][B])) * cx.w;
         split_block<HALF>(dl, p);
+        if constexpr (ST) x_tile_store(cx.td, cx, L, B, dl);
     }
 }
 
 // Slice (G, KS, HALF): the output blocks ob = 8 HALF .. 8 HALF + 7 of K-step KS, six MFMAs each; the mid-slice ring
 // barrier after block 3; the next block's (or the next slice's first block's) A pieces read one block ahead; then
 // the epilogue block of K-step KS + 1 (block 2 (KS + 1) + HALF) of the previous GEMM's output.
-template <int G, int KS, int HALF, int LH, int D, bool FWD>
+template <int G, int KS, int HALF, int LH, int D, int XM>
 __device__ __forceinline__ void x_slice(XState<LH>& st, const XCtx& cx) {
+    constexpr bool FWD = XM == X_FWD;
     constexpr int NS = x_ns<FWD, LH>();
     constexpr int CPW = 24 / x_waves<FWD>();
     constexpr int S = G * X_SPG + 2 * KS + HALF;
@@ -255,7 +311,9 @@ __device__ __forceinline__ void x_slice(XState<LH>& st, const XCtx& cx) {
         constexpr int NBI = NS * X_OBS;
         if constexpr (obl == 4) {
             if (S + 1 < NS || cx.more) {
-                if (S + 2 < NS || cx.more)
+                if constexpr (S + 2 < NS)
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(x_allow<S, LH, XM, CPW>()) : "memory");
+                else if (cx.more)
                     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(CPW) : "memory");
                 else
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -292,40 +350,41 @@ __device__ __forceinline__ void x_slice(XState<LH>& st, const XCtx& cx) {
         // blocks' MFMAs (after the last block it ran as a cluster with the matrix pipe idle)
         if constexpr (obl == X_EPI_AT && KS + 1 < X_KSTEPS) {
             if (X_EPI_FENCE) __builtin_amdgcn_sched_barrier(0);
-            x_epilogue<G, 2 * (KS + 1) + HALF, LH, D, FWD>(st, cx);
+            x_epilogue<G, 2 * (KS + 1) + HALF, LH, D, XM>(st, cx);
             if (X_EPI_FENCE) __builtin_amdgcn_sched_barrier(0);
         }
     });
 }
 
-template <int G, int LH, int D, bool FWD>
+template <int G, int LH, int D, int XM>
 __device__ __forceinline__ void x_gemm(XState<LH>& st, const XCtx& cx) {
 #pragma unroll
     for (int ob = 0; ob < NB; ++ob) st.acc[G & 1][ob] = f32x4{0.f, 0.f, 0.f, 0.f};
-    x_epilogue<G, 0, LH, D, FWD>(st, cx);
-    x_epilogue<G, 1, LH, D, FWD>(st, cx);
+    x_epilogue<G, 0, LH, D, XM>(st, cx);
+    x_epilogue<G, 1, LH, D, XM>(st, cx);
     xstatic_for<0, X_KSTEPS>([&](auto KS) {
-        x_slice<G, decltype(KS)::value, 0, LH, D, FWD>(st, cx);
-        x_slice<G, decltype(KS)::value, 1, LH, D, FWD>(st, cx);
+        x_slice<G, decltype(KS)::value, 0, LH, D, XM>(st, cx);
+        x_slice<G, decltype(KS)::value, 1, LH, D, XM>(st, cx);
     });
 }
 
-template <int G, int LH, int D, bool FWD>
+template <int G, int LH, int D, int XM>
 __device__ __forceinline__ void x_run(XState<LH>& st, const XCtx& cx) {
-    if constexpr (G < (FWD ? LH : 2 * LH)) {
-        x_gemm<G, LH, D, FWD>(st, cx);
-        x_run<G + 1, LH, D, FWD>(st, cx);
+    if constexpr (G < (XM == X_FWD ? LH : 2 * LH)) {
+        x_gemm<G, LH, D, XM>(st, cx);
+        x_run<G + 1, LH, D, XM>(st, cx);
     }
 }
 
 // ws: the split image of siren_pack_split (small block at ws_small, bf16 stream at stream); x (n, D); y (n) / gx
-// (n, D) (y nullable). w0 / w as the fp32 kernel (phase-scaled pack).
-template <int LH, int D, bool FWD>
-__global__ __launch_bounds__(64 * x_waves<FWD>(), 1) void w1x_kernel(const float* __restrict__ ws_small,
-                                                         const unsigned* __restrict__ stream,
-                                                         const float* __restrict__ x, int64_t n,
-                                                         float* __restrict__ y, float* __restrict__ gx, float w0,
-                                                         float w) {
+// (n, D) (y nullable; X_STORE: gx nullable). w0 / w as the fp32 kernel (phase-scaled pack). X_STORE: gy (n) the output
+// cotangent, abuf / dbuf the a_l / delta_l tiles (L + 1 layers of n_pad H floats each, the wgrad layout).
+template <int LH, int D, int XM>
+__global__ __launch_bounds__(64 * x_waves<XM == X_FWD>(), 1) void w1x_kernel(
+    const float* __restrict__ ws_small, const unsigned* __restrict__ stream, const float* __restrict__ x, int64_t n,
+    float* __restrict__ y, float* __restrict__ gx, float w0, float w, const float* __restrict__ gy = nullptr,
+    float* __restrict__ abuf = nullptr, float* __restrict__ dbuf = nullptr, int64_t n_pad = 0) {
+    constexpr bool FWD = XM == X_FWD, ST = XM == X_STORE;
     constexpr int NS = x_ns<FWD, LH>();
     constexpr int NW = x_waves<FWD>(), NT = 64 * NW, TILEX = 16 * NW, CPW = 24 / NW;
     static_assert(NS % X_NBUF == 0, "the ring must wrap onto slot 0 at a tile boundary");
@@ -353,6 +412,9 @@ __global__ __launch_bounds__(64 * x_waves<FWD>(), 1) void w1x_kernel(const float
         cx.inv_s0 = two_pi / w0;
     }
     cx.more = false;
+    cx.ta = cx.td = nullptr;
+    cx.lbytes = n_pad * H * 4;
+    cx.vt = 4u * (4 * cx.g * 16 + c);
     cx.ring_vaddr = lds_addr(cx.ring) + cx.lane * 16;
     cx.ring_vaddr2 = cx.ring_vaddr + 2 * X_SLICE * 4;
     {
@@ -360,12 +422,13 @@ __global__ __launch_bounds__(64 * x_waves<FWD>(), 1) void w1x_kernel(const float
         for (int e = threadIdx.x; e < nf4; e += NT) ((f32x4*)sm)[e] = ((const f32x4*)ws_small)[e];
     }
     const int64_t tiles = (n + TILEX - 1) / TILEX;
-    float xn[4];
+    float xn[4], gn = 0.f;
     auto load_inputs = [&](int64_t tile) {
         const int64_t cd = tile * TILEX + cx.wave * 16 + c;
         const bool ok = tile < tiles && cd < n;
 #pragma unroll
         for (int k = 0; k < 4; ++k) xn[k] = (ok && k < D) ? x[cd * D + k] : 0.f;
+        if constexpr (ST) gn = ok ? gy[cd] : 0.f;
     };
     load_inputs(blockIdx.x);
     __syncthreads();
@@ -384,8 +447,14 @@ __global__ __launch_bounds__(64 * x_waves<FWD>(), 1) void w1x_kernel(const float
 #pragma unroll
         for (int k = 0; k < 4; ++k) st.xv[k] = xn[k];
         st.yp = 0.f;
+        st.gyv = gn;
+        if constexpr (ST) {
+            const int64_t tbase = (tile * NW + cx.wave) * (H * 16);  // wave-uniform
+            cx.ta = (const char*)(abuf + tbase);
+            cx.td = (const char*)(dbuf + tbase);
+        }
         load_inputs(tile + gridDim.x);
-        x_run<0, LH, D, FWD>(st, cx);
+        x_run<0, LH, D, XM>(st, cx);
         if constexpr (FWD) {
             // last hidden layer: a_L = sin(w z_L) and y = a_L Wout^T + bout (serial over the 16 blocks)
             constexpr int GL = (LH - 1) & 1;
@@ -426,6 +495,7 @@ __global__ __launch_bounds__(64 * x_waves<FWD>(), 1) void w1x_kernel(const float
                 c0[r] = cs_;
             }
             const f32x4 dl = (st.acc[GL][rb] * c0) * cx.w0;
+            if constexpr (ST) x_tile_store(cx.td, cx, 0, rb, dl);
 #pragma unroll
             for (int k = 0; k < D; ++k) {
                 const f32x4 wk = *(const f32x4*)(sm + SM_W0 + k * H + 16 * rb + 4 * cx.g);
@@ -435,7 +505,7 @@ __global__ __launch_bounds__(64 * x_waves<FWD>(), 1) void w1x_kernel(const float
 #pragma unroll
         for (int k = 0; k < D; ++k) {
             const float qk = sum_groups(q[k]) * cx.inv_s0;
-            if (valid && cx.g == 0) gx[coord * D + k] = qk;
+            if (valid && cx.g == 0 && (!ST || gx != nullptr)) gx[coord * D + k] = qk;
         }
     }
 }

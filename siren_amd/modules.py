@@ -27,7 +27,7 @@ import torch
 from torch import nn
 
 from . import _lib
-from .autograd import JetState, SirenBatchedFunction, SirenFunction, SirenJetFunction
+from .autograd import JetState, SirenBatchedFunction, SirenFunction, SirenJetFunction, SirenSplitFunction
 from .engine import SirenEngine
 
 
@@ -162,8 +162,9 @@ PRECISIONS = ('fp32', 'bf16x6')
 
 def _fused_apply(engine, jet, coords, weights_biases, precision='fp32'):
     """Run the fused SIREN on coords (..., d_in) with [(W, b), ...]; returns (..., d_out). precision 'bf16x6' runs
-    the jet forward (y and dPhi/dx in one launch) on the split-bf16 kernel where it covers the network
-    (DESIGN.md §3.13); everything else stays on the fp32 kernels."""
+    the jet forward (y and dPhi/dx in one launch), a no-graph forward and a parameter-gradient training step
+    (SirenSplitFunction) on the split-bf16 kernels where they cover the network; everything else
+    stays on the fp32 kernels."""
     if coords.device.type != 'cuda':
         raise RuntimeError('siren_amd runs on ROCm devices (MI355X) only; move the model and coords to "cuda". '
                            'The CPU restatement of the reference lives in oracle/ (test infrastructure).')
@@ -191,6 +192,11 @@ def _fused_apply(engine, jet, coords, weights_biases, precision='fp32'):
           and not (torch.is_grad_enabled() and (x2d.requires_grad or flat.requires_grad))):
         # no graph is recorded (dense evaluation: create_mesh, summaries under no_grad): the split-bf16 forward
         y = engine.forward_split(engine.pack_split(flat.detach()), x2d.detach().contiguous())
+    elif (precision == 'bf16x6' and engine.split_supported and torch.is_grad_enabled() and flat.requires_grad
+          and not (jet is not None and jet.laplace(JetState.key(x2d)))):
+        # a training step: the split-bf16 forward and the bf16x6 W2 backward (a Laplacian consumer keeps the fp32
+        # node, whose forward can speculate the jet sweep)
+        y = SirenSplitFunction.apply(engine, jet, x2d, flat)
     else:
         # a graph that will want parameter gradients: the forward keeps a_l / cos for a reverse-only backward
         # (the jet state only matters when a graph is recorded: a derivative can be requested of y only then)
@@ -304,8 +310,9 @@ class SingleBVPNet(MetaModule):
     Extra keyword `precision` ('fp32' | 'bf16x6'): 'bf16x6' evaluates that jet forward on the split-bf16 kernel
     (fp32 operands split exactly into bf16 hi/mid/lo, fp32-level error, 1.6x the fp32 kernel at 5x256 d2/d3 o1)
     where it covers the network, and a forward that records no graph (no_grad: create_mesh, summaries) on the split
-    W0 kernel (1.85x); a backward through the jet node recomputes on the fp32 kernels, so it is an evaluation mode --
-    training is faster with the default (its stored forward feeds the backward).
+    W0 kernel (1.85x), and a step whose loss needs parameter gradients of model_out only (image fitting) on the
+    split W0 forward plus the bf16x6 W2 backward (siren_backward_split: split-bf16 recompute + reverse, fp32 MFMA
+    wgrad). A backward through the jet node recomputes on the fp32 kernels.
     """
 
     def __init__(self, out_features=1, type='sine', in_features=2, mode='mlp', hidden_features=256,

@@ -235,3 +235,84 @@ def test_split_distinct_omegas(cuda, w0, w, d, n):
     ey32, eg32 = np.max(np.abs(y32.cpu().numpy() - ry)), np.max(np.abs(gx32.cpu().numpy() - rg))
     assert ey <= max(1e-4, 2 * ey32) and eg <= max(tol_rel(rg), 2 * eg32 + 1e-6), (ey, eg, ey32, eg32)
     assert np.max(np.abs(yf.cpu().numpy() - ry)) <= max(1e-4, 2 * ey32)
+
+
+# ---- the bf16x6 training leg: siren_backward_split (split-bf16 recompute + reverse from gy, fp32 MFMA wgrad) ----
+W2_KEYS = ['net.net.%d.0.%s' % (i, k) for i in range(5) for k in ('weight', 'bias')]
+
+
+def test_backward_split_vs_reference_golden(cuda, g1):
+    """image_mse θ-gradients of the reference (G1, fp64) from the bf16x6 W2 backward: within the fp32 pipeline's
+    tolerance and at its level of error (an fp32-equivalent mode)."""
+    flat, layers = weights_of(g1)
+    eng = engine()
+    fdev = to_dev(flat, cuda)
+    ws, wsx = eng.pack(fdev), eng.pack_split(fdev)
+    x = to_dev(g1['coords'][0], cuda)
+    y = eng.forward_split(wsx, x)
+    gy = 2. * (y - to_dev(g1['gt_img'][0], cuda)) / y.numel()
+    gx, gp = eng.backward_split(wsx, x, gy, want_gx=True)
+    gx32, gp32 = eng.backward_params(ws, x, gy)
+    ref = np.concatenate([g1['G1_image_mse_grad_' + k].reshape(-1) for k in W2_KEYS])
+    e, e32 = np.max(np.abs(gp.cpu().numpy() - ref)), np.max(np.abs(gp32.cpu().numpy() - ref))
+    print('theta-grads |d| split %.2e fp32 kernels %.2e (max |g| %.2e)' % (e, e32, np.max(np.abs(ref))))
+    assert e <= 1e-4 * np.max(np.abs(ref))
+    assert e <= 2 * e32 + 1e-6 * np.max(np.abs(ref))
+    _, rgx = O.forward_grad(g1['coords'][0], layers, gy.cpu().numpy())
+    assert np.max(np.abs(gx.cpu().numpy() - rgx)) <= 1e-4 * np.max(np.abs(rgx))
+    _, gp_nogx = eng.backward_split(wsx, x, gy)  # gx not requested: the same θ-gradients
+    assert torch.equal(gp_nogx, gp)
+
+
+@pytest.mark.parametrize('n,d', [(1, 2), (100, 3), (5000, 2), (70000, 3)])
+def test_backward_split_shapes(cuda, n, d):
+    """Ragged sizes (partial tiles, one coordinate, a persistent grid's several tiles per workgroup) against fp64
+    autograd of the oracle's network, and against the fp32 W2 pipeline."""
+    layers = random_layers(d, seed=n)
+    eng = engine(d)
+    fdev = to_dev(O.flatten(layers), cuda)
+    ws, wsx = eng.pack(fdev), eng.pack_split(fdev)
+    rng = np.random.default_rng(n)
+    x = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    gy = (rng.normal(size=(n, 1)) / n).astype(np.float32)
+    gx, gp = eng.backward_split(wsx, to_dev(x, cuda), to_dev(gy, cuda), want_gx=True)
+    gx32, gp32 = eng.backward_params(ws, to_dev(x, cuda), to_dev(gy, cuda))
+    xt = torch.tensor(x, dtype=torch.float64, requires_grad=True)
+    params = [torch.tensor(np.asarray(t), dtype=torch.float64, requires_grad=True) for W, b in layers for t in (W, b)]
+    yt = O.torch_forward(xt, params)
+    g = torch.autograd.grad(yt, [xt] + params, torch.tensor(gy, dtype=torch.float64))
+    rgp = torch.cat([t.reshape(-1) for t in g[1:]]).numpy()
+    assert np.max(np.abs(gp.cpu().numpy() - rgp)) <= 1e-4 * np.max(np.abs(rgp))
+    assert np.max(np.abs(gx.cpu().numpy() - g[0].numpy())) <= tol_rel(g[0].numpy())
+    assert np.max(np.abs(gp.cpu().numpy() - gp32.cpu().numpy())) <= 2e-5 * np.max(np.abs(rgp))
+
+
+def test_backward_split_zero_coords(cuda):
+    eng = engine()
+    fdev = to_dev(O.flatten(random_layers(2)), cuda)
+    wsx = eng.pack_split(fdev)
+    gx, gp = eng.backward_split(wsx, torch.empty(0, 2, device=cuda), torch.empty(0, 1, device=cuda), want_gx=True)
+    assert gx.shape == (0, 2) and torch.count_nonzero(gp) == 0
+
+
+def test_module_precision_bf16x6_training_step(cuda, g1, monkeypatch):
+    """SingleBVPNet(precision='bf16x6') under image_mse training: the θ-gradients come from siren_backward_split (the
+    fp32 W2 entry points are forbidden here) and match G1's fp64 golden; y is the split forward's."""
+    from siren_amd import loss_functions as Lf, modules
+    from siren_amd.engine import SirenEngine
+
+    def boom(*a, **k):
+        raise AssertionError('the fp32 W2 path ran')
+    for nm in ('backward_params', 'backward_stored', 'forward_store', 'forward'):
+        monkeypatch.setattr(SirenEngine, nm, boom)
+    sd = {k[2:]: np.asarray(g1[k]) for k in g1.keys() if k.startswith('w_net.')}
+    m = modules.SingleBVPNet(in_features=2, verbose=False, precision='bf16x6').to(cuda)
+    m.load_state_dict({k: torch.tensor(v) for k, v in sd.items()})
+    out = m({'coords': to_dev(g1['coords'], cuda)})
+    assert np.max(np.abs(out['model_out'].detach().cpu().numpy()[0] - g1['G1_model_out_f64'][0])) <= 1e-4
+    loss = Lf.image_mse(None, out, {'img': to_dev(g1['gt_img'], cuda)})['img_loss']
+    m.zero_grad()
+    loss.backward()
+    for k, p in m.named_parameters():
+        ref = g1['G1_image_mse_grad_' + k]
+        assert np.max(np.abs(p.grad.cpu().numpy() - ref)) <= 1e-4 * max(np.max(np.abs(ref)), 1e-30) + 1e-12, k
