@@ -80,7 +80,10 @@ enum { JET_BOTH = 0, JET_FWD = 1, JET_REV = 2 };
 // nullable outputs; glap unused (JET_BOTH only)
 // (The backward of a Hessian node that kept its forward jets is qf_kernel.hpp: reverse GEMMs only, on the node's own
 // 8-coordinate layout.)
-template <int PHASE, bool MIX = false, bool QG = false>
+// PH (!MIX): ws is the phase-scaled image (w1_ws: weights and biases carry w / 2 pi, W0 and b0 w0 / 2 pi), the jets are
+// in revolutions (jet_sin_d_rev) and the reverse GEMMs return s u (s = w / 2 pi): the scratch holds D / s, the seed is
+// s u_L, and gx undoes W0's scale (the zb / a-jet tiles are the true ones either way)
+template <int PHASE, bool MIX = false, bool QG = false, bool PH = false>
 __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
     const float* __restrict__ ws, const float* __restrict__ x, int64_t n, const float* __restrict__ glap,
     float* __restrict__ gx, int d, int o, int lh, float w0, float w, float* __restrict__ spill,
@@ -122,13 +125,20 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
             jcf[k] = val * xv[k] + (js == k + 1 ? 1.f : 0.f);
         }
     }
-    const float kb0 = js == 0 ? 0.f : w0, kg0 = js == 3 ? w0 * w0 : 0.f;
-    const float kb = js == 0 ? 0.f : w, kg = js == 3 ? w * w : 0.f;
-    // !MIX: the scratch holds the reverse's combinations of the z jet (jet_sin_d), per layer scale w0 / w
-    const float dA0 = js == 0 ? w0 : 0.f, dB0 = js == 0 ? 0.f : w0 * w0, dC0 = js == 3 ? w0 * w0 * w0 : 0.f;
-    const float dA = js == 0 ? w : 0.f, dB = js == 0 ? 0.f : w * w, dC = js == 3 ? w * w * w : 0.f;
+    static_assert(!(PH && MIX), "the phase-scaled jets cover the Laplacian's jet only");
+    constexpr float two_pi = 6.28318530717958648f, four_pi2 = 39.4784176043574344f;
+    const float s_h = w * 0.159154943091895336f;  // PH: the hidden layers' pack scale s = w / 2 pi
+    const float rw0 = w0 / s_h;                   // PH: layer 0's w0 over the reverse scale
+    const float kb0 = js == 0 ? 0.f : (PH ? two_pi : w0), kg0 = js == 3 ? (PH ? four_pi2 : w0 * w0) : 0.f;
+    const float kb = js == 0 ? 0.f : (PH ? two_pi : w), kg = js == 3 ? (PH ? four_pi2 : w * w) : 0.f;
+    // !MIX: the scratch holds the reverse's combinations of the z jet (jet_sin_d), per layer scale w0 / w; PH: in
+    // revolutions and over s (layer l's dA, dB, dC = (w_l / s) (1, 2 pi, 4 pi^2): 2 pi (1, 2 pi, 4 pi^2) for l >= 1)
+    const float dA0 = js == 0 ? (PH ? rw0 : w0) : 0.f, dB0 = js == 0 ? 0.f : (PH ? two_pi * rw0 : w0 * w0),
+                dC0 = js == 3 ? (PH ? four_pi2 * rw0 : w0 * w0 * w0) : 0.f;
+    const float dA = js == 0 ? (PH ? two_pi : w) : 0.f, dB = js == 0 ? 0.f : (PH ? four_pi2 : w * w),
+                dC = js == 3 ? (PH ? two_pi * four_pi2 : w * w * w) : 0.f;
     const float m12 = (js == 1 || js == 2) ? 1.f : 0.f;
-    const float gl = (PHASE != JET_FWD && valid && js == 3) ? (MIX ? 1.f : glap[coord]) : 0.f;
+    const float gl = (PHASE != JET_FWD && valid && js == 3) ? (MIX ? 1.f : (PH ? s_h : 1.f) * glap[coord]) : 0.f;
     const bool s1 = js == 1;
     // QG: this lane's row of 2 Q (streams 1, 2; Q = sym(G), G (n, d, d), d <= 2) for jet_sin_q / jet_sin_adjoint_q
     f32x2 qreg = {0.f, 0.f};
@@ -180,7 +190,8 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
                 act[rb] = jet_sin<MIX>(z, w0, val, kb0, kg0);
             } else {
                 f32x4 dz;
-                act[rb] = jet_sin_d(z, w0, val, kb0, kg0, dA0, dB0, dC0, dz);
+                act[rb] = PH ? jet_sin_d_rev(z, val, kb0, kg0, dA0, dB0, dC0, dz)
+                             : jet_sin_d(z, w0, val, kb0, kg0, dA0, dB0, dC0, dz);
                 zs.next_store(dz);
             }
         }
@@ -226,7 +237,8 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
                     act[rb] = jet_sin<MIX>(z, w, val, kb, kg);
                 } else {
                     f32x4 dz;
-                    act[rb] = jet_sin_d(z, w, val, kb, kg, dA, dB, dC, dz);
+                    act[rb] = PH ? jet_sin_d_rev(z, val, kb, kg, dA, dB, dC, dz)
+                                 : jet_sin_d(z, w, val, kb, kg, dA, dB, dC, dz);
                     zs.next_store(dz);
                 }
             }
@@ -326,7 +338,7 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
                 const f32x4 wk = *(const f32x4*)(sm + SM_W0 + k * H + 16 * rb + 4 * g);
                 q += wk[0] * act[rb][0] + wk[1] * act[rb][1] + wk[2] * act[rb][2] + wk[3] * act[rb][3];
             }
-            q = sum_groups(q);
+            q = sum_groups(q) * (PH ? two_pi / w0 : 1.f);  // PH: LDS W0^T carries w0 / 2 pi
             if (valid && g == 0 && js == 0) gx[coord * d + k] = q;
             if (MIX && gv != nullptr && valid && g == 0 && js == 1) gv[coord * d + k] = q;
         }

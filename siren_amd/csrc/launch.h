@@ -59,13 +59,16 @@ void launch_w0x(dim3 grid, hipStream_t st, const float* ws_small, const unsigned
 // tu_w4.hip: JET mode (16 coordinates per workgroup); lap (n) = sum_j Laplacian(y_j), gx (n, d) = sum_j grad y_j
 void launch_w4(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, float* y, float* gx, float* lap,
                int d, int o, int lh, float w0, float w);
+// W4s split, forward half (MODE_JETS): W4 + the a-jet tiles and the z-jet scratch of jet_store_kernel<JET_REV, PH>
+void launch_w4s(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, float* y, float* gx, float* lap,
+                float* abuf, float* spill, int64_t n_pad, int d, int o, int lh, float w0, float w);
 // tu_jet.hip: W4s (backward of the fused Laplacian), tiles of 16 columns = 4 coordinates x 4 jet streams
 void launch_jet_store(dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n, const float* glap,
                       float* gx, int d, int o, int lh, float w0, float w, float* spill, float* abuf, float* dbuf,
-                      int64_t n_pad);
+                      int64_t n_pad, bool ph);
 void launch_jet_phase(int phase, dim3 grid, hipStream_t st, const float* ws, const float* x, int64_t n,
                       const float* glap, float* gx, int d, int o, int lh, float w0, float w, float* spill, float* abuf,
-                      float* dbuf, int64_t n_pad, float* y, float* lap);
+                      float* dbuf, int64_t n_pad, float* y, float* lap, bool ph);
 void launch_small_jet(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, const float* x,
                       const float* glap, int64_t n, int64_t n_pad, int64_t tps, float* eslab, int64_t E, int d,
                       int o, int lh);

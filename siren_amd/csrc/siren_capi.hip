@@ -659,6 +659,10 @@ int32_t siren_backward_stored(const siren_cfg* cfg, const float* ws, const float
 
 // ---- W4s: backward of the fused Laplacian (laplace_mse training) ------------------------------------------
 namespace {
+// the Laplacian's jet kernels (W4s) run on the phase-scaled image whenever it exists (jet_kernel.hpp PH: sincos in
+// revolutions, 3 VALU fewer per element of the forward jet); zero omegas keep the unscaled image
+const float* jet_ws(const siren_cfg* cfg, const float* ws) { return w1_ok(cfg) ? w1_ws(cfg, ws) : ws; }
+
 int check_jet(const siren_cfg* cfg) {
     if (int rc = check_cfg(cfg, true)) return rc;
     if (wide(cfg) || layered(cfg) || cfg->d_in > 2 || !cfg->outermost_linear || cfg->n_hidden > 5)
@@ -717,8 +721,9 @@ int32_t siren_laplace_backward(const siren_cfg* cfg, const float* ws, const floa
     float* dbuf = abuf + plan.buf_floats;
     float* spill = dbuf + plan.buf_floats;
     float* partial = spill + plan.buf_floats;
-    siren::launch_jet_store(dim3((unsigned)(plan.n_pad / 16)), st, ws, x, n, glap, gx, cfg->d_in, cfg->d_out,
-                            cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, spill, abuf, dbuf, plan.n_pad);
+    siren::launch_jet_store(dim3((unsigned)(plan.n_pad / 16)), st, jet_ws(cfg, ws), x, n, glap, gx, cfg->d_in,
+                            cfg->d_out, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, spill, abuf, dbuf,
+                            plan.n_pad, w1_ok(cfg));
     if (int rc = hip_status("siren_laplace_backward (jet store)")) return rc;
     siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden), st, abuf, dbuf, plan.cols, plan.tps,
                         partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1, siren::H, 1);
@@ -741,9 +746,13 @@ int32_t siren_forward_laplace_store(const siren_cfg* cfg, const float* ws, const
     float* abuf = tws;
     float* dbuf = abuf + plan.buf_floats;
     float* spill = dbuf + plan.buf_floats;
-    siren::launch_jet_phase(1, dim3((unsigned)(plan.n_pad / 16)), (hipStream_t)stream, ws, x, n, nullptr, gx,
-                            cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, spill, abuf,
-                            dbuf, plan.n_pad, y, lap);
+    if (w1_ok(cfg))  // the W4 kernel with the stores (interleaved epilogues, phase-scaled image)
+        siren::launch_w4s(dim3((unsigned)(plan.n_pad / 16)), (hipStream_t)stream, w1_ws(cfg, ws), x, n, y, gx, lap, abuf,
+                          spill, plan.n_pad, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden);
+    else
+        siren::launch_jet_phase(1, dim3((unsigned)(plan.n_pad / 16)), (hipStream_t)stream, ws, x, n, nullptr, gx,
+                                cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, spill, abuf,
+                                dbuf, plan.n_pad, y, lap, false);
     return hip_status("siren_forward_laplace_store");
 }
 
@@ -765,9 +774,9 @@ int32_t siren_laplace_backward_stored(const siren_cfg* cfg, const float* ws, con
     float* dbuf = abuf + plan.buf_floats;
     float* spill = dbuf + plan.buf_floats;
     float* partial = spill + plan.buf_floats;
-    siren::launch_jet_phase(2, dim3((unsigned)(plan.n_pad / 16)), st, ws, x, n, glap, gx, cfg->d_in, cfg->d_out,
-                            cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, spill, abuf, dbuf, plan.n_pad, nullptr,
-                            nullptr);
+    siren::launch_jet_phase(2, dim3((unsigned)(plan.n_pad / 16)), st, jet_ws(cfg, ws), x, n, glap, gx, cfg->d_in,
+                            cfg->d_out, cfg->n_hidden, cfg->omega_first, cfg->omega_hidden, spill, abuf, dbuf,
+                            plan.n_pad, nullptr, nullptr, w1_ok(cfg));
     if (int rc = hip_status("siren_laplace_backward_stored (jet reverse)")) return rc;
     siren::launch_wgrad(dim3((unsigned)plan.splits, (unsigned)cfg->n_hidden), st, abuf, dbuf, plan.cols, plan.tps,
                         partial, P, cfg->d_in, cfg->d_out, cfg->n_hidden, 1, siren::H, 1);

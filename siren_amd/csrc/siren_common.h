@@ -38,7 +38,9 @@ constexpr int MAX_LH_DEEP = 5;    // hidden 256, 4..5 hidden layers: derivatives
 // MODE_FWDS (W2 split, forward half): MODE_FWD + a_l tiles (wgrad layout) and cos(w z_l) (lane-major) to HBM, so
 // the backward needs no forward recompute. MODE_REV (W2 split, backward half): the L reverse GEMMs only, cos read
 // back from HBM, delta_l tiles stored like MODE_STORE.
-enum { MODE_W1 = 0, MODE_STORE = 1, MODE_FWD = 2, MODE_JET = 3, MODE_FWDS = 4, MODE_REV = 5 };
+// MODE_JETS (W4s split, forward half): MODE_JET + the a-jet tiles (wgrad layout, 4 n_pad H floats per layer) and the
+// reverse's combinations of the z jet (jet_sin_d_rev, lane-major) for jet_store_kernel<JET_REV, PH>.
+enum { MODE_W1 = 0, MODE_STORE = 1, MODE_FWD = 2, MODE_JET = 3, MODE_FWDS = 4, MODE_REV = 5, MODE_JETS = 6 };
 // w1_kernel modifier bits (MODE & MODE_BASE is the mode proper): MODE_PROF records per-GEMM s_memtime stamps;
 // MODE_O1S specialises d_out == 1 with the all-ones output cotangent (gy == NULL); MODE_D(k) fixes d_in = k at
 // compile time. Both only remove runtime-uniform branches and selects from the epilogues (whose VALU count is the
@@ -51,7 +53,7 @@ constexpr int mode_din(int mode) { return (mode >> 8) & 7; }
 // MODE_PROF (diagnostics, siren_w1_phase_profile): s_memtime stamps at tile start, after each GEMM and at tile end
 constexpr int PROF_TILES = 4, PROF_EVENTS = 8, PROF_BLOCKS = 256;
 __host__ __device__ constexpr bool forward_only(int mode) {
-    return mode == MODE_FWD || mode == MODE_JET || mode == MODE_FWDS;
+    return mode == MODE_FWD || mode == MODE_JET || mode == MODE_FWDS || mode == MODE_JETS;
 }
 // lane-major cos(w z_l) buffer of MODE_FWDS / MODE_REV: per (tile, wave) (LH + 1) layers x NB blocks x 64 lanes x f32x4
 // (one coalesced dwordx4 per lane per block): float offset of (tile, wave, layer, block, lane)
@@ -231,6 +233,23 @@ __device__ __forceinline__ f32x4 jet_sin_d(const f32x4& z, float w, float ka, fl
         const float z0 = quad_bcast<0>(z[r]), t1 = quad_bcast<1>(z[r]), t2 = quad_bcast<2>(z[r]);
         float sn, cs;
         sincos_fast(w * z0, sn, cs);
+        const float q2 = __builtin_fmaf(t1, t1, t2 * t2);
+        out[r] = __builtin_fmaf(ka, sn, __builtin_fmaf(kb * cs, z[r], -(kg * sn) * q2));
+        D[r] = __builtin_fmaf(dA, cs, __builtin_fmaf(dB * sn, z[r], (dC * cs) * q2));
+    }
+    return out;
+}
+// jet_sin_d on a phase-scaled jet (w1_kernel's revolution-domain pack, jet_sin_rev): sincos_rev of the value stream
+// (2 reduction VALU instead of sincos_fast's 5 and the scale multiply), kb = 2 pi, kg = 4 pi^2 on every layer and the
+// scratch combinations divided by the reverse GEMMs' scale s (jet_store_kernel PH)
+__device__ __forceinline__ f32x4 jet_sin_d_rev(const f32x4& z, float ka, float kb, float kg, float dA, float dB,
+                                               float dC, f32x4& D) {
+    f32x4 out;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float z0 = quad_bcast<0>(z[r]), t1 = quad_bcast<1>(z[r]), t2 = quad_bcast<2>(z[r]);
+        float sn, cs;
+        sincos_rev(z0, sn, cs);
         const float q2 = __builtin_fmaf(t1, t1, t2 * t2);
         out[r] = __builtin_fmaf(ka, sn, __builtin_fmaf(kb * cs, z[r], -(kg * sn) * q2));
         D[r] = __builtin_fmaf(dA, cs, __builtin_fmaf(dB * sn, z[r], (dC * cs) * q2));

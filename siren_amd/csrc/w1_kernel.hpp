@@ -127,6 +127,8 @@ template <int MODE, int LH>
 constexpr int gemm0() { return (MODE & MODE_BASE) == MODE_REV ? LH : 0; }
 template <int MODE>
 constexpr bool is_rev() { return (MODE & MODE_BASE) == MODE_REV; }
+template <int MODE>
+constexpr bool is_jet() { return (MODE & MODE_BASE) == MODE_JET || (MODE & MODE_BASE) == MODE_JETS; }
 
 // ---- the memory modes' epilogue stores (STORE / FWDS / REV) ----------------------------------------------------------
 // Epilogue E of a tile (E = (G - G0) NB + b builds block b of GEMM G's B operand; E % NB == 0 runs before the GEMM, the
@@ -142,14 +144,20 @@ constexpr bool is_rev() { return (MODE & MODE_BASE) == MODE_REV; }
 #endif
 template <int MODE>
 constexpr bool w1_mem() {
-    return (MODE & MODE_BASE) == MODE_STORE || (MODE & MODE_BASE) == MODE_FWDS || (MODE & MODE_BASE) == MODE_REV;
+    return (MODE & MODE_BASE) == MODE_STORE || (MODE & MODE_BASE) == MODE_FWDS || (MODE & MODE_BASE) == MODE_REV ||
+           (MODE & MODE_BASE) == MODE_JETS;
+}
+// the forward halves (two workgroups per CU: no LDS for the transpose scratch) store their tiles directly
+constexpr bool w1_fwd_half(int mode) {
+    return (mode & MODE_BASE) == MODE_FWDS || (mode & MODE_BASE) == MODE_JETS;
 }
 template <int MODE>
-constexpr bool w1_staged() { return W1_STAGE != 0 && w1_mem<MODE>() && (MODE & MODE_BASE) != MODE_FWDS; }
+constexpr bool w1_staged() { return W1_STAGE != 0 && w1_mem<MODE>() && !w1_fwd_half(MODE); }
 template <int MODE>
 constexpr bool w1_tiles() { return w1_mem<MODE>() && (MODE & MODE_NOTILE) == 0; }
 constexpr bool w1_mem_rt(int mode) {
-    return (mode & MODE_BASE) == MODE_STORE || (mode & MODE_BASE) == MODE_FWDS || (mode & MODE_BASE) == MODE_REV;
+    return (mode & MODE_BASE) == MODE_STORE || (mode & MODE_BASE) == MODE_FWDS || (mode & MODE_BASE) == MODE_REV ||
+           (mode & MODE_BASE) == MODE_JETS;
 }
 constexpr int w1_nslices(int lh, int mode) {
     return (mode & MODE_BASE) == MODE_STORE || (mode & MODE_BASE) == MODE_W1 ? 2 * lh * NB : lh * NB;
@@ -165,15 +173,14 @@ constexpr int w1_ntile(int e, int lh, int mode) {
 // after slice E - 1, before the GEMM); its staged tile blocks leave at the start of slice E (half 2 E).
 constexpr int w1_direct(int e, int lh, int mode) {
     if (e < 0 || e >= w1_nslices(lh, mode)) return 0;
-    return (W1_STAGE != 0 && (mode & MODE_BASE) != MODE_FWDS ? 0 : 4 * w1_ntile(e, lh, mode)) +
-           ((mode & MODE_BASE) == MODE_FWDS ? 1 : 0);
+    return (W1_STAGE != 0 && !w1_fwd_half(mode) ? 0 : 4 * w1_ntile(e, lh, mode)) + (w1_fwd_half(mode) ? 1 : 0);
 }
 constexpr int w1_direct_half(int e) { return e % NB != 0 && W1_EPI_MEM < 4 ? 2 * (e - 1) : 2 * (e - 1) + 1; }
 constexpr int w1_ops_in_half(int h, int lh, int mode) {
     int n = 0;
     for (int e = h / 2; e <= h / 2 + 1; ++e)
         if (w1_direct_half(e) == h) n += w1_direct(e, lh, mode);
-    if (h % 2 == 0 && W1_STAGE != 0 && (mode & MODE_BASE) != MODE_FWDS) n += w1_ntile(h / 2, lh, mode);
+    if (h % 2 == 0 && W1_STAGE != 0 && !w1_fwd_half(mode)) n += w1_ntile(h / 2, lh, mode);
     return n;
 }
 // s_waitcnt vmcnt allowance of slice S's mid-slice wait (S + 2 < NS): ring slice S + 1 (issued at the mid of S - 2) and,
@@ -247,6 +254,7 @@ struct W1Ctx {
     float jcf[MAXD];      // first layer: z = sum_k jcf[k] W0[:, k] + jcb b0  (value: x_k; tangent s: e_{s-1})
     float jcb;            // 1 on the value stream (bias), else 0
     float ja, jb0, jg0, jb, jg;  // a = ja sin + jb cos dz - jg sin |dz|^2  (jb0/jg0 with w0, jb/jg with w)
+    float jdA0, jdB0, jdC0, jdA, jdB, jdC;  // JETS: the reverse's z-jet combinations (jet_sin_d_rev), layer 0 / >= 1
 };
 
 // Four 1 KiB global->LDS pieces of slice s for this wave, as saddr-form global_load_lds_dwordx4: SGPR slice base
@@ -359,6 +367,21 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
     } else if constexpr ((MODE & MODE_BASE) == MODE_JET && KIND == EPI_SINCOS) {
         const f32x4 z = st.acc[(G + 1) & 1][b] + cx.jcb * ep.v[0];
         st.act[b] = jet_sin_rev(z, cx.ja, cx.jb, cx.jg);
+    } else if constexpr ((MODE & MODE_BASE) == MODE_JETS) {
+        f32x4 z, dz;
+        if constexpr (KIND == EPI_FIRST) {
+            z = cx.jcf[0] * ep.v[0];
+#pragma unroll
+            for (int k = 1; k < MAXD; ++k)
+                if (k < cx.d) z += cx.jcf[k] * ep.v[k];
+            z += cx.jcb * ep.v[4];
+            st.act[b] = jet_sin_d_rev(z, cx.ja, cx.jb0, cx.jg0, cx.jdA0, cx.jdB0, cx.jdC0, dz);
+        } else {
+            z = st.acc[(G + 1) & 1][b] + cx.jcb * ep.v[0];
+            st.act[b] = jet_sin_d_rev(z, cx.ja, cx.jb, cx.jg, cx.jdA, cx.jdB, cx.jdC, dz);
+        }
+        w1_tile_put<MODE, 0>(st, cx, cx.ta, G, b, st.act[b]);
+        w3_store16(w3_at(cx.cs, w1_tile_off(cx, G, b)), cx.vl, dz);
     } else if constexpr (KIND == EPI_FIRST) {
         f32x4 z = st.xv[0] * ep.v[0];  // phase u_0 = w0 (x W0^T + b0) / 2 pi: the pack carries the scale
 #pragma unroll
@@ -560,15 +583,19 @@ __device__ __forceinline__ void w1_run(W1State<LH, MODE>& st, const W1Ctx& cx) {
 constexpr int small_floats_ct(int lh) { return SM_BIAS + (lh + 1) * H; }
 
 // JET mode: 16 coordinates per workgroup (4 per wave); lap (n) receives sum_j Laplacian(y_j), gx (n, d) sum_j
-// grad y_j (the quantities diff_operators.laplace / gradient return); abuf is reused as the lap pointer.
+// grad y_j (the quantities diff_operators.laplace / gradient return); abuf is reused as the lap pointer. JETS: the same
+// outputs (lap in the last argument), abuf = a-jet tiles, dbuf = the reverse's z-jet scratch (jet_kernel.hpp layout).
 template <int LH, int MODE>
 __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) void w1_kernel(const float* __restrict__ ws, const float* __restrict__ x,
                                                         int64_t n, const float* __restrict__ gy, float* __restrict__ y,
                                                         float* __restrict__ gx, int d, int o, float w0, float w,
                                                         float* __restrict__ abuf, float* __restrict__ dbuf,
-                                                        int64_t n_pad, int64_t ws_bstride) {
+                                                        int64_t n_pad, int64_t ws_bstride,
+                                                        float* __restrict__ lap = nullptr) {
     constexpr bool STORE = (MODE & MODE_BASE) == MODE_STORE;
-    constexpr bool JET = (MODE & MODE_BASE) == MODE_JET;
+    constexpr bool JET = is_jet<MODE>();
+    constexpr bool JETS = (MODE & MODE_BASE) == MODE_JETS;
+    if constexpr (!JETS) lap = abuf;
     constexpr bool FWDS = (MODE & MODE_BASE) == MODE_FWDS;  // abuf = a_l tiles, dbuf = lane-major cos buffer
     constexpr bool REV = is_rev<MODE>();                     // abuf = lane-major cos buffer, dbuf = delta tiles
     constexpr int NS = npasses<MODE>() * LH * NB;
@@ -622,7 +649,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
     cx.more = false;
     cx.prof = nullptr;
     cx.stream = ws + small_pad(LH) + (REV ? (int64_t)LH * NB * SLICE : 0);
-    cx.lstride = n_pad * H;
+    cx.lstride = (JETS ? 4 : 1) * n_pad * H;  // jet tiles: 4 streams per coordinate
     const unsigned lds_base = (unsigned)(uintptr_t)((__attribute__((address_space(3))) float*)lds);
     cx.ring_vaddr = lds_base + cx.lane * 16;
     cx.sm_vaddr = lds_base + W1_NBUF * SLICE * 4 + 16 * cx.g;
@@ -640,7 +667,8 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
         for (int e = threadIdx.x; e < nf4; e += THREADS) ((f32x4*)sm)[e] = ((const f32x4*)ws)[e];
     }
     const int js = c & 3;  // JET stream of this lane
-    const int64_t tiles = JET ? (n + 15) / 16 : (n + TILE - 1) / TILE;
+    // (JETS writes its tiles for all n_pad coordinates: the wgrad and the reverse read every column, padding included)
+    const int64_t tiles = JETS ? n_pad / 16 : JET ? (n + 15) / 16 : (n + TILE - 1) / TILE;
     auto coord_of = [&](int64_t tile) -> int64_t {
         return JET ? tile * 16 + cx.wave * 4 + (c >> 2) : tile * TILE + cx.wave * 16 + c;
     };
@@ -662,6 +690,15 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
         cx.ja = val;
         cx.jb0 = cx.jb = js == 0 ? 0.f : 6.28318530717958648f;
         cx.jg0 = cx.jg = js == 3 ? 39.4784176043574344f : 0.f;
+        // JETS scratch coefficients (jet_kernel.hpp PH): (w_l / s) (1, 2 pi, 4 pi^2) on streams (0, != 0, 3)
+        constexpr float two_pi = 6.28318530717958648f, four_pi2 = 39.4784176043574344f;
+        const float rw0 = w0 / (w * 0.159154943091895336f);
+        cx.jdA0 = js == 0 ? rw0 : 0.f;
+        cx.jdB0 = js == 0 ? 0.f : two_pi * rw0;
+        cx.jdC0 = js == 3 ? four_pi2 * rw0 : 0.f;
+        cx.jdA = js == 0 ? two_pi : 0.f;
+        cx.jdB = js == 0 ? 0.f : four_pi2;
+        cx.jdC = js == 3 ? two_pi * four_pi2 : 0.f;
     }
     __syncthreads();
     // ring prologue: slices 0..2 in flight; slice 0 published; its first operand pair read
@@ -700,10 +737,11 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
                 cx.abuf = abuf + toff;
                 cx.ta = (const char*)(abuf + tbase);
             }
-            if constexpr (!FWDS) {
+            if constexpr (!FWDS && !JETS) {
                 cx.dbuf = dbuf + toff;
                 cx.td = (const char*)(dbuf + tbase);
             }
+            if constexpr (JETS) cx.cs = (const char*)(dbuf + tbase);  // lane-major, + 16 lane
         }
         if constexpr (FWDS) cx.cs = (const char*)(dbuf + cos_off(tile, cx.wave, LH, 0, 0, 0));
         if constexpr (REV) {
@@ -731,7 +769,15 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
             for (int rb = 0; rb < NB; ++rb) {
                 const int nb = 16 * rb + 4 * cx.g;
                 const f32x4 z = st.acc[GL][rb] + cx.jcb * *(const f32x4*)(sm + SM_BIAS + LH * H + nb);
-                const f32x4 a = jet_sin_rev(z, cx.ja, cx.jb, cx.jg);
+                f32x4 a;
+                if constexpr (JETS) {
+                    f32x4 dz;
+                    a = jet_sin_d_rev(z, cx.ja, cx.jb, cx.jg, cx.jdA, cx.jdB, cx.jdC, dz);
+                    w3_store_tile(w3_at(cx.ta, w1_tile_off(cx, LH, rb)), cx.vt, a);
+                    w3_store16(w3_at(cx.cs, w1_tile_off(cx, LH, rb)), cx.vl, dz);
+                } else {
+                    a = jet_sin_rev(z, cx.ja, cx.jb, cx.jg);
+                }
 #pragma unroll
                 for (int j = 0; j < MAXO; ++j) {
                     if (j < o) {
@@ -750,7 +796,9 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
                 }
             }
             if (valid && cx.g == 0) {
-                if (js == 3) abuf[coord] = tot;
+                if (js == 3) {
+                    if (lap != nullptr) lap[coord] = tot;
+                }
                 else if (js >= 1 && js <= d && gx != nullptr) gx[coord * d + js - 1] = tot;
             }
         } else if constexpr ((MODE & MODE_BASE) == MODE_FWD || FWDS) {

@@ -180,7 +180,10 @@ def test_laplace_mse_step_runs_on_hip_kernels(cuda, g1, monkeypatch):
 
 @pytest.mark.parametrize('n,d,L', [(1, 2, 3), (4097, 2, 3), (1000, 1, 2), (333, 2, 5)])
 def test_split_laplace_forward_backward_matches(cuda, n, d, L):
-    """Split W4 / W4s (forward jet keeps its stores, reverse-only backward) == the single-launch kernels."""
+    """Split W4 / W4s (forward jet keeps its stores, reverse-only backward) == the single-launch kernels. The split's
+    forward is the interleaved W4 kernel (w1_kernel MODE_JETS) and the single launch jet_store_kernel: same arithmetic
+    per element, different GEMM accumulation order, so they agree to fp32 rounding (both are pinned against the fp64
+    goldens by the tests above)."""
     from siren_amd.engine import SirenEngine
     rng = np.random.default_rng(n + L)
     dims = [d] + [256] * (L + 1) + [1]
@@ -198,7 +201,8 @@ def test_split_laplace_forward_backward_matches(cuda, n, d, L):
     assert float((lap_s - lap_r).abs().max()) <= 1e-5 * max(1., float(lap_r.abs().max()))
     gx_s, gp_s = eng.laplace_backward_stored(ws, x, glap, tws)
     gx_r, gp_r = eng.laplace_backward(ws, x, glap)
-    assert torch.equal(gx_s, gx_r) and torch.equal(gp_s, gp_r)
+    assert float((gx_s - gx_r).abs().max()) <= 1e-5 * max(1., float(gx_r.abs().max()))
+    assert float((gp_s - gp_r).abs().max()) <= 1e-5 * float(gp_r.abs().max())
 
 
 def test_laplace_mse_one_forward_sweep(cuda, g1, monkeypatch):
