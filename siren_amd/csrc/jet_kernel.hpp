@@ -165,10 +165,13 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
     if (PHASE == JET_REV) {
         // seed from the stored z_L jet (the JET_FWD launch's scratch)
         LaneBlocks zl{sp + (int64_t)lh * lstride};
+        f32x4 dv[NB];  // every block in flight at once (as the reverse epilogues below)
+#pragma unroll
+        for (int rb = 0; rb < NB; ++rb) dv[rb] = zl.next_load();
 #pragma unroll
         for (int rb = 0; rb < NB; ++rb) {
             const f32x4 u = gl * *(const f32x4*)(sm + SM_SEED + 16 * rb + 4 * g);
-            act[rb] = jet_sin_adjoint_d(u, zl.next_load(), val, m12);
+            act[rb] = jet_sin_adjoint_d(u, dv[rb], val, m12);
         }
         jstore_tile(dbuf + (int64_t)lh * lstride + toff, act);
     } else {
@@ -315,12 +318,19 @@ __global__ __launch_bounds__(THREADS, 2) void jet_store_kernel(
             LaneBlocks zl{sp + (int64_t)lm * lstride};
             const float wl = lm == 0 ? w0 : w;
             const f32x2 qc = qload();
-            {
+            if constexpr (!MIX) {
+                // all 16 blocks of the combinations in flight at once (a load per block one block ahead waited out
+                // 16 memory latencies per layer; the linear adjoint leaves the registers for it)
+                f32x4 dv[NB];
+#pragma unroll
+                for (int rb = 0; rb < NB; ++rb) dv[rb] = zl.next_load();
+#pragma unroll
+                for (int rb = 0; rb < NB; ++rb) act[rb] = jet_sin_adjoint_d(acc[rb], dv[rb], val, m12);
+            } else {
 #pragma unroll
                 for (int rb = 0; rb < NB; ++rb) {
-                    act[rb] = QG    ? jet_sin_adjoint_q(acc[rb], zl.next_load(), wl, val, m12, qc[0], qc[1])
-                              : MIX ? jet_sin_adjoint<MIX>(acc[rb], zl.next_load(), wl, val, m12, s1)
-                                    : jet_sin_adjoint_d(acc[rb], zl.next_load(), val, m12);
+                    act[rb] = QG ? jet_sin_adjoint_q(acc[rb], zl.next_load(), wl, val, m12, qc[0], qc[1])
+                                 : jet_sin_adjoint<MIX>(acc[rb], zl.next_load(), wl, val, m12, s1);
                 }
             }
             jstore_tile(dbuf + (int64_t)lm * lstride + toff, act);
