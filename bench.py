@@ -226,9 +226,9 @@ def split_leg(eng, flat, x, steps, warmup):
             'parity': 'tests/test_gpu_split.py: G1/G2 reference goldens vs fp64 within the fp32 kernel\'s error'}
 
 
-# the bf16x6 W2 unit per coordinate on the bf16 pipe: forward (LH H^2), recomputed forward + reverse (2 LH H^2) and
-# the hidden wgrad (LH H^2), six products each
-SPLIT_TRAIN_MFMA_FLOP = 6 * 2 * 4 * 3 * 256 * 256
+# the bf16x6 W2 unit per coordinate on the bf16 pipe (stored split): forward (LH H^2), reverse (LH H^2) and the hidden
+# wgrad (LH H^2), six products each
+SPLIT_TRAIN_MFMA_FLOP = 6 * 2 * 3 * 3 * 256 * 256
 
 
 def split_train_leg(device, fp32_rate, n=1 << 18):
@@ -246,8 +246,9 @@ def split_train_leg(device, fp32_rate, n=1 << 18):
     st = torch.cuda.current_stream()
     wsx = eng.pack_split(flat)
     times = {}
-    for name, fn in (('forward_split', lambda: eng.forward_split(wsx, x)),
-                     ('backward_split', lambda: eng.backward_split(wsx, x, gy))):
+    _, tws = eng.forward_store_split(wsx, x)
+    for name, fn in (('forward_split', lambda: eng.forward_store_split(wsx, x)),
+                     ('backward_split', lambda: eng.backward_stored_split(wsx, x, gy, tws))):
         fn()
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
         for a, b in ev:
@@ -264,7 +265,7 @@ def split_train_leg(device, fp32_rate, n=1 << 18):
             'roofline': {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': PEAK_BF16_MFMA_TFLOPS,
                          'unit': 'TFLOP/s', 'frac': round(achieved / PEAK_BF16_MFMA_TFLOPS, 4),
                          'flop_per_coord': SPLIT_TRAIN_MFMA_FLOP,
-                         'note': 'forward + backward launches (split W0, split store, bf16x6 wgrad, edge, reduce)'},
+                         'note': 'forward + backward launches (split forward with stores, split reverse, bf16x6 wgrad, edge, reduce)'},
             'parity': 'tests/test_gpu_split.py: G1 image_mse theta-grads vs fp64 within the fp32 pipeline\'s error'}
 
 

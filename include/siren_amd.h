@@ -264,6 +264,15 @@ int32_t siren_forward_split(const siren_cfg* cfg, const float* wsx, const float*
  * siren_forward_grad_split covers; gx (n, d_in) nullable; tws: siren_train_ws_floats(cfg, n) floats. */
 int32_t siren_backward_split(const siren_cfg* cfg, const float* wsx, const float* x, int64_t n, const float* gy,
                              float* tws, float* gx, float* gparams, void* stream);
+/* The stored-forward form of the same unit (what SirenSplitFunction runs): siren_forward_store_split is
+ * siren_forward_split plus the a_l tiles and cos(w z_l) into tws; siren_backward_stored_split runs the reverse GEMMs
+ * only from them (delta_l tiles), then the bf16x6 wgrad, edge layers and slab reduction. tws:
+ * siren_train_split_ws_floats(cfg, n) floats, passed unchanged from the forward to the backward. */
+int32_t siren_train_split_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count);
+int32_t siren_forward_store_split(const siren_cfg* cfg, const float* wsx, const float* x, int64_t n, float* y,
+                                  float* tws, void* stream);
+int32_t siren_backward_stored_split(const siren_cfg* cfg, const float* wsx, const float* x, int64_t n, const float* gy,
+                                    float* tws, float* gx, float* gparams, void* stream);
 
 /* Diagnostics: the W1 kernel (hidden 256, 3 hidden layers) with s_memtime stamps. stamps receives
  * 256 workgroups x 4 tiles x 4 waves x 8 events (uint64; event 0 tile start, 1..6 after GEMM 0..5, 7 tile end);

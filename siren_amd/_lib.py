@@ -83,6 +83,9 @@ _SIGS = {
     'siren_forward_grad_split': [_CFG, _P, _P, _I64, _P, _P, _P],
     'siren_forward_split': [_CFG, _P, _P, _I64, _P, _P],
     'siren_backward_split': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P],
+    'siren_train_split_ws_floats': [_CFG, _I64, ctypes.POINTER(_I64)],
+    'siren_forward_store_split': [_CFG, _P, _P, _I64, _P, _P, _P],
+    'siren_backward_stored_split': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P],
     'siren_hessian_backward_ws_floats': [_CFG, _I64, ctypes.POINTER(_I64)],
     'siren_hessian_backward': [_CFG, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P],
     'siren_hessian_ws_floats': [_CFG, _I64, ctypes.c_int32, ctypes.POINTER(_I64)],

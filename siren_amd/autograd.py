@@ -169,15 +169,16 @@ class SirenFunction(torch.autograd.Function):
 
 
 class SirenSplitFunction(torch.autograd.Function):
-    """precision 'bf16x6' under a parameter-gradient graph (the image-fit training step): y from the
-    split-bf16 forward (siren_forward_split); the backward recomputes the forward on the split-bf16 kernel, runs the
-    reverse from gy and reduces the θ-gradients with the fp32 MFMA wgrad (siren_backward_split). An x-only or
-    create_graph backward runs on the fp32 kernels (the split kernels cover gy = ones / first order only)."""
+    """precision 'bf16x6' under a parameter-gradient graph (the image-fit training step): the stored
+    split on the split-bf16 kernels — the forward (siren_forward_store_split) keeps a_l and cos(w z_l), the parameter
+    backward (siren_backward_stored_split) runs the reverse GEMMs only and reduces the θ-gradients with the bf16x6
+    wgrad. An x-only or create_graph backward runs on the fp32 kernels (the split kernels are first order)."""
 
     @staticmethod
     def forward(ctx, engine, jet, x, flat):
         wsx = engine.pack_split(flat)
-        y = engine.forward_split(wsx, x)
+        # the stored split: the forward keeps a_l / cos(w z_l), the parameter backward is reverse-only
+        y, ctx.tws = engine.forward_store_split(wsx, x)
         # the fp32 image too: a derivative of y (diff_operators.gradient / laplace through siren_node_of) runs on the
         # fp32 kernels
         ctx.engine, ctx.jet, ctx.wsx, ctx.ws = engine, jet, wsx, engine.pack(flat)
@@ -194,7 +195,7 @@ class SirenSplitFunction(torch.autograd.Function):
         gy = gy.contiguous()
         if not torch.is_grad_enabled():
             if need_p:
-                gx, gp = engine.backward_split(ctx.wsx, x, gy, want_gx=need_x)
+                gx, gp = engine.backward_stored_split(ctx.wsx, x, gy, ctx.tws, want_gx=need_x)
             elif need_x:
                 _, gx = engine.forward_grad(ws, x, gy, want_y=False)
             return None, None, gx, gp

@@ -49,6 +49,12 @@ void launch_w1x(dim3 grid, hipStream_t st, const float* ws_small, const unsigned
 void launch_w1x_store(dim3 grid, hipStream_t st, const float* ws_small, const unsigned* stream, const float* x,
                       int64_t n, const float* gy, float* y, float* gx, float* abuf, float* dbuf, int64_t n_pad, int d,
                       float w0, float w);
+// the stored split of that stage (X_FWDS: 8 waves, 128-coordinate tiles, a_l tiles + lane-major cos; X_REV: the
+// reverse from them, delta_l tiles); n_pad a multiple of 128
+void launch_w0xs(dim3 grid, hipStream_t st, const float* ws_small, const unsigned* stream, const float* x, int64_t n,
+                 float* y, float* abuf, float* cbuf, int64_t n_pad, int d, float w0, float w);
+void launch_w1xr(dim3 grid, hipStream_t st, const float* ws_small, const unsigned* stream, const float* x, int64_t n,
+                 const float* gy, float* gx, const float* cbuf, float* dbuf, int64_t n_pad, int d, float w0, float w);
 // its hidden-layer weight gradient on the bf16 pipe (wgradx_kernel.hpp): grid (S, LH), tps even, slabs as launch_wgrad
 void launch_wgradx(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, int64_t n_pad, int64_t tps,
                    float* partial, int64_t P, int d, int o, int lh);

@@ -431,6 +431,66 @@ int32_t siren_backward_split(const siren_cfg* cfg, const float* wsx, const float
                         "siren_backward_split (reduce)");
 }
 
+// ---- the stored split of the bf16x6 W2 unit: the forward keeps a_l tiles and cos(w z_l), the backward is reverse-only ----
+// workspace: [a_l tiles][delta_l tiles][partial slabs][lane-major cos, L + 1 layers], on n rounded up to 128 (the
+// split forward's tile)
+static int64_t split_n(int64_t n) { return (std::max<int64_t>(n, 1) + 127) / 128 * 128; }
+
+int32_t siren_train_split_ws_floats(const siren_cfg* cfg, int64_t n, int64_t* count) {
+    if (int rc = split_ok(cfg)) return rc;
+    if (count == nullptr || n < 0) return fail(SIREN_EINVAL, "count is NULL or n < 0");
+    const TrainPlan plan(cfg, split_n(n));
+    *count = plan.total + (int64_t)(cfg->n_hidden + 1) * plan.n_pad * cfg->hidden;
+    return SIREN_OK;
+}
+
+int32_t siren_forward_store_split(const siren_cfg* cfg, const float* wsx, const float* x, int64_t n, float* y,
+                                  float* tws, void* stream) {
+    if (int rc = split_ok(cfg)) return rc;
+    if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    if (n == 0) return SIREN_OK;
+    if (wsx == nullptr || x == nullptr || tws == nullptr) return fail(SIREN_EINVAL, "wsx/x/tws is NULL");
+    const TrainPlan plan(cfg, split_n(n));
+    if (plan.n_pad / 128 > 0x7fffffffll) return fail(SIREN_EINVAL, "n too large");
+    const int64_t spad = small_pad(cfg);
+    siren::launch_w0xs(tile_grid(cfg, plan.n_pad / 128, 1), (hipStream_t)stream, wsx + spad,
+                       (const unsigned*)(wsx + 2 * spad), x, n, y, tws, tws + plan.total, plan.n_pad, cfg->d_in,
+                       cfg->omega_first, cfg->omega_hidden);
+    return hip_status("siren_forward_store_split");
+}
+
+int32_t siren_backward_stored_split(const siren_cfg* cfg, const float* wsx, const float* x, int64_t n, const float* gy,
+                                    float* tws, float* gx, float* gparams, void* stream) {
+    if (int rc = split_ok(cfg)) return rc;
+    if (n < 0) return fail(SIREN_EINVAL, "n < 0");
+    if (gparams == nullptr) return fail(SIREN_EINVAL, "gparams is NULL");
+    const hipStream_t st = (hipStream_t)stream;
+    const int64_t P = param_count(cfg);
+    if (n == 0) {  // empty tensors may carry NULL data pointers: only gparams is written
+        (void)hipMemsetAsync(gparams, 0, P * sizeof(float), st);
+        return hip_status("siren_backward_stored_split");
+    }
+    if (wsx == nullptr || x == nullptr || gy == nullptr || tws == nullptr) return fail(SIREN_EINVAL, "wsx/x/gy/tws is NULL");
+    const TrainPlan plan(cfg, split_n(n));
+    float* abuf = tws;
+    float* dbuf = tws + plan.act_floats;
+    float* partial = tws + 2 * plan.act_floats;
+    const int64_t spad = small_pad(cfg);
+    siren::launch_w1xr(tile_grid(cfg, plan.n_pad / siren::TILE, 1), st, wsx + spad, (const unsigned*)(wsx + 2 * spad),
+                       x, n, gy, gx, tws + plan.total, dbuf, plan.n_pad, cfg->d_in, cfg->omega_first,
+                       cfg->omega_hidden);
+    if (int rc = hip_status("siren_backward_stored_split (split reverse)")) return rc;
+    const int64_t tpx = plan.tps + (plan.tps & 1), sx = (plan.tiles + tpx - 1) / tpx;
+    siren::launch_wgradx(dim3((unsigned)sx, (unsigned)cfg->n_hidden), st, abuf, dbuf, plan.n_pad, tpx, partial, P,
+                         cfg->d_in, cfg->d_out, cfg->n_hidden);
+    if (int rc = hip_status("siren_backward_stored_split (wgrad)")) return rc;
+    siren::launch_small(plan.es.grid(cfg), st, abuf, dbuf, x, gy, n, plan.n_pad, plan.es.tps, partial + plan.eslab_off,
+                        plan.es.E, cfg->d_in, cfg->d_out, cfg->n_hidden, cfg->hidden);
+    if (int rc = hip_status("siren_backward_stored_split (small)")) return rc;
+    return finish_grads(cfg, st, partial, sx, 0, partial + plan.eslab_off, plan.es, gparams,
+                        "siren_backward_stored_split (reduce)");
+}
+
 // diagnostics: while set, W3 launches record s_memtime phase stamps (w3_kernel.hpp) into stamps[256][16]
 static unsigned long long* g_w3_prof = nullptr;
 int32_t siren_w3_phase_profile(uint64_t* stamps) {

@@ -40,7 +40,15 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // kernel modes: W1 (y, gx with gy = ones), FWD (the forward-only W0, 8 waves), STORE (the W2 stage of the bf16x6
 // training leg: the forward recomputed, the reverse seeded with a per-coordinate gy (d_out 1), and a_l / delta_l written
 // as 16-coordinate tiles in the wgrad layout, as w1_kernel MODE_STORE)
-enum { X_W1 = 0, X_FWD = 1, X_STORE = 2 };
+// FWDS / REV: the stored-forward split of that W2 stage (as w1_kernel MODE_FWDS / MODE_REV): FWDS is the forward-only
+// W0 (8 waves) plus the a_l tiles and the lane-major cos(w z_l), l >= 1; REV runs the reverse GEMMs only, each
+// epilogue's cos block reloaded from that buffer (layer 0's recomputed from x, as every mode does), and writes the
+// delta_l tiles.
+enum { X_W1 = 0, X_FWD = 1, X_STORE = 2, X_FWDS = 3, X_REV = 4 };
+constexpr bool x_fwd_like(int xm) { return xm == X_FWD || xm == X_FWDS; }  // forward GEMMs only, two waves per SIMD
+// lane-major cos buffer of X_FWDS / X_REV: per 16-coordinate wave tile wt, (L + 1) layers x NB blocks x 64 lanes x f32x4
+// (w1_kernel's cos_off with tile WAVES + wave = wt)
+__host__ __device__ constexpr int64_t x_cos_off(int64_t wt, int lh) { return wt * (lh + 1) * NB * 256; }
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int X_OBS = 8;                            // output blocks per slice (half a K-step)
@@ -93,7 +101,8 @@ __device__ __forceinline__ void split_block(const f32x4& v, u32x4 (&p)[3]) {
 
 template <int LH>
 struct XState {
-    float gyv;         // X_STORE: this lane's output cotangent
+    float gyv;         // X_STORE / X_REV: this lane's output cotangent
+    f32x4 cq[4];       // X_REV: reloaded cos blocks: an in-slice epilogue block b in cq[b & 1], pre-GEMM blocks 0, 1 in 2, 3
     u32x4 bx[2][3];    // B operand pieces (hi, mid, lo) of K-step s in bx[s & 1]
     f32x4 acc[2][NB];  // ping-pong accumulators (GEMM G in acc[G & 1])
     f32x4 C[LH][NB];   // cos(w z_l), 1 <= l < LH (layer 0's is recomputed at the end: 64 fewer live registers)
@@ -111,7 +120,9 @@ struct XCtx {
     bool more;
     const char* ta;        // X_STORE: wave-uniform a_l tile base of (tile, wave), layer 0; layer l at + l * lbytes
     const char* td;        // X_STORE: the same for delta_l
+    const char* cs;        // X_FWDS / X_REV: wave-uniform lane-major cos base of the wave tile (x_cos_off), + 16 lane
     int64_t lbytes;
+    unsigned vl;           // 16 lane
     unsigned vt;           // X_STORE: this lane's byte offset in a tile block, 4 (4 g 16 + c)
     unsigned ring_vaddr;   // LDS byte address of this lane's 16 B in slot 0
     unsigned ring_vaddr2;  // ... in slot 2
@@ -168,8 +179,12 @@ __device__ __forceinline__ void xring_issue(const unsigned* __restrict__ stream,
 // registers fit twice per SIMD without the parked cos
 template <bool FWD>
 constexpr int x_waves() { return FWD ? 8 : 4; }
-template <bool FWD, int LH>
-constexpr int x_ns() { return FWD ? LH * X_SPG : x_slices(LH); }
+// slices per coordinate tile: the forward-only modes and X_REV run L GEMMs, the others 2 L
+template <int XM, int LH>
+constexpr int x_ns() { return (x_fwd_like(XM) || XM == X_REV) ? LH * X_SPG : x_slices(LH); }
+// the GEMM a tile starts at (X_REV: the reverse GEMMs G = LH .. 2 LH - 1)
+template <int XM, int LH>
+constexpr int x_g0() { return XM == X_REV ? LH : 0; }
 
 template <int I, int N, typename F>
 __device__ __forceinline__ void xstatic_for(F&& f) {
@@ -203,36 +218,59 @@ __device__ __forceinline__ void x_tile_store(const char* base, const XCtx& cx, i
     asm volatile("" : "+s"(lb));
     w3_store_tile(w3_at(base, l * lb + b * 1024), cx.vt, v);
 }
-// dword stores an epilogue producing GEMM E's B operand issues per block (X_STORE): a_E, and at E = LH also delta_L;
-// delta_{2 LH - E} beyond
-constexpr int x_epi_nst(int e, int lh) { return e == lh ? 8 : 4; }
+// vector-memory stores an epilogue producing GEMM E's B operand issues per block: X_STORE a_E (4 dwords), at E = LH also
+// delta_L, delta_{2 LH - E} beyond; X_FWDS a_E and (E >= 1) its cos block; X_REV delta
+constexpr int x_epi_nst(int e, int lh, int xm) {
+    return xm == X_STORE ? (e == lh ? 8 : 4) : xm == X_FWDS ? (e == 0 ? 4 : 5) : xm == X_REV ? 4 : 0;
+}
+constexpr int x_ns_rt(int xm, int lh) { return (x_fwd_like(xm) || xm == X_REV) ? lh * X_SPG : x_slices(lh); }
 // stores of the in-slice epilogue of slice s (after its mid-slice wait: block 2 (KS + 1) + HALF of GEMM s / X_SPG's
 // input when KS + 1 < X_KSTEPS), and of the two pre-GEMM blocks run before slice s when s starts a GEMM
-constexpr int x_st_slice(int s, int lh) {
-    return (s < 0 || s >= x_slices(lh) || ((s % X_SPG) >> 1) + 1 >= X_KSTEPS) ? 0 : x_epi_nst(s / X_SPG, lh);
+constexpr int x_st_slice(int s, int lh, int xm) {
+    return (s < 0 || s >= x_ns_rt(xm, lh) || ((s % X_SPG) >> 1) + 1 >= X_KSTEPS)
+               ? 0
+               : x_epi_nst((xm == X_REV ? lh : 0) + s / X_SPG, lh, xm);
 }
-constexpr int x_st_pre(int s, int lh) {
-    return (s <= 0 || s >= x_slices(lh) || s % X_SPG != 0) ? 0 : 2 * x_epi_nst(s / X_SPG, lh);
+constexpr int x_st_pre(int s, int lh, int xm) {
+    return (s <= 0 || s >= x_ns_rt(xm, lh) || s % X_SPG != 0)
+               ? 0
+               : 2 * x_epi_nst((xm == X_REV ? lh : 0) + s / X_SPG, lh, xm);
 }
 // s_waitcnt vmcnt allowance of slice S's mid-slice wait (S + 2 < NS): ring slice S + 1 was issued at the mid of S - 2;
 // after it come the epilogue stores of S - 2, the pre-GEMM blocks before S - 1, ring slice S + 2 (CPW pieces), the
 // epilogue stores of S - 1 and the pre-GEMM blocks before S. The first two slices of a tile count CPW (the previous
 // tile's serial tail sits between: CPW waits for more than needed, never less).
+// X_REV: the cos blocks an epilogue of slice S reads (its in-slice block; at S % X_SPG = X_SPG - 1 the next GEMM's
+// pre-GEMM blocks) are loaded at the mid of S - 1 ahead of ring slice S + 2, so only that ring slice and the stores
+// issued after it may stay in flight.
 template <int S, int LH, int XM, int CPW>
 constexpr int x_allow() {
-    if constexpr (XM != X_STORE || S < 2) {
+    if constexpr ((XM != X_STORE && XM != X_FWDS && XM != X_REV) || S < 2) {
         return CPW;
+    } else if constexpr (XM == X_REV) {
+        constexpr int n = CPW + x_st_slice(S - 1, LH, XM) + x_st_pre(S, LH, XM);
+        static_assert(n < 64, "vmcnt is 6 bits");
+        return n;
     } else {
-        constexpr int n = CPW + x_st_slice(S - 2, LH) + x_st_pre(S - 1, LH) + x_st_slice(S - 1, LH) + x_st_pre(S, LH);
+        constexpr int n = CPW + x_st_slice(S - 2, LH, XM) + x_st_pre(S - 1, LH, XM) + x_st_slice(S - 1, LH, XM) +
+                          x_st_pre(S, LH, XM);
         static_assert(n < 64, "vmcnt is 6 bits");
         return n;
     }
+}
+// the layer whose cos an epilogue producing GEMM E's input reads in X_REV: L for the seed (E = LH), 2 LH - E beyond
+constexpr int x_rev_layer(int e, int lh) { return e == lh ? lh : 2 * lh - e; }
+// X_REV: cos block B of layer l into r (saddr form: wave-uniform base + 16 lane)
+template <int L, int B>
+__device__ __forceinline__ void x_cos_issue(f32x4& r, const XCtx& cx) {
+    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(r) : "v"(cx.vl), "s"(w3_at(cx.cs, (L * NB + B) * 1024)));
 }
 static_assert(X_EPI_AT >= 4, "the in-slice epilogue's stores are counted after the mid-slice wait");
 
 template <int E, int B, int LH, int D, int XM>
 __device__ __forceinline__ void x_epilogue(XState<LH>& st, const XCtx& cx) {
-    constexpr bool FWD = XM == X_FWD, ST = XM == X_STORE;
+    constexpr bool FWD = x_fwd_like(XM), ST = XM == X_STORE, FWS = XM == X_FWDS, RV = XM == X_REV;
+    constexpr int CQ = B < 2 ? 2 + B : (B & 1);  // X_REV: the reloaded cos block's slot
     constexpr int KS = B >> 1, HALF = B & 1;
     const int nb = 16 * B + 4 * cx.g;
     u32x4(&p)[3] = st.bx[KS & 1];
@@ -249,7 +287,7 @@ __device__ __forceinline__ void x_epilogue(XState<LH>& st, const XCtx& cx) {
             cs[r] = c_;
         }
         split_block<HALF>(sn, p);
-        if constexpr (ST) x_tile_store(cx.ta, cx, 0, B, sn);
+        if constexpr (ST || FWS) x_tile_store(cx.ta, cx, 0, B, sn);
     } else if constexpr (E < LH) {
         const f32x4 z = st.acc[(E + 1) & 1][B] + *(const f32x4*)(cx.sm + SM_BIAS + E * H + nb);
         f32x4 sn, cs;
@@ -262,7 +300,14 @@ __device__ __forceinline__ void x_epilogue(XState<LH>& st, const XCtx& cx) {
         }
         if constexpr (!FWD) st.C[E][B] = x_to_agpr(cs);
         split_block<HALF>(sn, p);
-        if constexpr (ST) x_tile_store(cx.ta, cx, E, B, sn);
+        if constexpr (ST || FWS) x_tile_store(cx.ta, cx, E, B, sn);
+        if constexpr (FWS) w3_store16(w3_at(cx.cs, (E * NB + B) * 1024), cx.vl, cs);
+    } else if constexpr (E == LH && RV) {
+        // delta_L = (gy Wout) . cos(w z_L) . w with cos from X_FWDS
+        const f32x4 wo = *(const f32x4*)(cx.sm + SM_WO + nb);
+        const f32x4 dl = ((opaque(st.gyv) * wo) * st.cq[CQ]) * cx.wsd;
+        split_block<HALF>(dl, p);
+        x_tile_store(cx.td, cx, LH, B, dl);
     } else if constexpr (E == LH) {
         const f32x4 z = st.acc[(E + 1) & 1][B] + *(const f32x4*)(cx.sm + SM_BIAS + LH * H + nb);
         f32x4 sn, cs;
@@ -285,9 +330,9 @@ __device__ __forceinline__ void x_epilogue(XState<LH>& st, const XCtx& cx) {
         }
     } else {
         constexpr int L = 2 * LH - E;  // delta_L = u_L . cos(w z_L) . w, 1 <= L < LH
-        const f32x4 dl = (st.acc[(E + 1) & 1][B] * x_from_agpr(st.C[L][B])) * cx.w;
+        const f32x4 dl = (st.acc[(E + 1) & 1][B] * (RV ? st.cq[CQ] : x_from_agpr(st.C[L][B]))) * cx.w;
         split_block<HALF>(dl, p);
-        if constexpr (ST) x_tile_store(cx.td, cx, L, B, dl);
+        if constexpr (ST || RV) x_tile_store(cx.td, cx, L, B, dl);
     }
 }
 
@@ -296,10 +341,10 @@ __device__ __forceinline__ void x_epilogue(XState<LH>& st, const XCtx& cx) {
 // the epilogue block of K-step KS + 1 (block 2 (KS + 1) + HALF) of the previous GEMM's output.
 template <int G, int KS, int HALF, int LH, int D, int XM>
 __device__ __forceinline__ void x_slice(XState<LH>& st, const XCtx& cx) {
-    constexpr bool FWD = XM == X_FWD;
-    constexpr int NS = x_ns<FWD, LH>();
+    constexpr bool FWD = x_fwd_like(XM);
+    constexpr int NS = x_ns<XM, LH>();
     constexpr int CPW = 24 / x_waves<FWD>();
-    constexpr int S = G * X_SPG + 2 * KS + HALF;
+    constexpr int S = (G - x_g0<XM, LH>()) * X_SPG + 2 * KS + HALF;
     constexpr int SLOT = (S % X_NBUF) * X_SLICE * 4;
     constexpr int NSLOT = ((S + 1) % X_NBUF) * X_SLICE * 4;
     f32x4(&acc)[NB] = st.acc[G & 1];
@@ -317,6 +362,22 @@ __device__ __forceinline__ void x_slice(XState<LH>& st, const XCtx& cx) {
                     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(CPW) : "memory");
                 else
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if constexpr (XM == X_REV) {
+                    // landed: this slice's in-slice cos block and, in the last slice of a GEMM, the next GEMM's
+                    // pre-GEMM blocks; then the next slice's block and (second-to-last slice) the next GEMM's blocks
+                    constexpr int R = 2 * KS + HALF;  // slice within the GEMM
+                    if constexpr (KS + 1 < X_KSTEPS) asm volatile("" : "+v"(st.cq[HALF]));
+                    if constexpr (R == X_SPG - 1 && G + 1 < 2 * LH) asm volatile("" : "+v"(st.cq[2]), "+v"(st.cq[3]));
+                    constexpr int R1 = R + 1, KS1 = R1 >> 1, H1 = R1 & 1;
+                    if constexpr (R1 < X_SPG && KS1 + 1 < X_KSTEPS)
+                        x_cos_issue<x_rev_layer(G, LH), 2 * (KS1 + 1) + H1>(st.cq[H1], cx);
+                    if constexpr (R == X_SPG - 2 && G + 1 < 2 * LH) {
+                        x_cos_issue<x_rev_layer(G + 1, LH), 0>(st.cq[2], cx);
+                        x_cos_issue<x_rev_layer(G + 1, LH), 1>(st.cq[3], cx);
+                    }
+                    if constexpr (R == X_SPG - 1 && G + 1 < 2 * LH)  // the next GEMM's first in-slice block
+                        x_cos_issue<x_rev_layer(G + 1, LH), 2>(st.cq[0], cx);
+                }
                 __builtin_amdgcn_s_barrier();
                 if (S + 3 < NS || cx.more) {
                     const unsigned* sp = cx.stream;
@@ -370,7 +431,7 @@ __device__ __forceinline__ void x_gemm(XState<LH>& st, const XCtx& cx) {
 
 template <int G, int LH, int D, int XM>
 __device__ __forceinline__ void x_run(XState<LH>& st, const XCtx& cx) {
-    if constexpr (G < (XM == X_FWD ? LH : 2 * LH)) {
+    if constexpr (G < (x_fwd_like(XM) ? LH : 2 * LH)) {
         x_gemm<G, LH, D, XM>(st, cx);
         x_run<G + 1, LH, D, XM>(st, cx);
     }
@@ -380,12 +441,13 @@ __device__ __forceinline__ void x_run(XState<LH>& st, const XCtx& cx) {
 // (n, D) (y nullable; X_STORE: gx nullable). w0 / w as the fp32 kernel (phase-scaled pack). X_STORE: gy (n) the output
 // cotangent, abuf / dbuf the a_l / delta_l tiles (L + 1 layers of n_pad H floats each, the wgrad layout).
 template <int LH, int D, int XM>
-__global__ __launch_bounds__(64 * x_waves<XM == X_FWD>(), 1) void w1x_kernel(
+__global__ __launch_bounds__(64 * x_waves<x_fwd_like(XM)>(), 1) void w1x_kernel(
     const float* __restrict__ ws_small, const unsigned* __restrict__ stream, const float* __restrict__ x, int64_t n,
     float* __restrict__ y, float* __restrict__ gx, float w0, float w, const float* __restrict__ gy = nullptr,
     float* __restrict__ abuf = nullptr, float* __restrict__ dbuf = nullptr, int64_t n_pad = 0) {
-    constexpr bool FWD = XM == X_FWD, ST = XM == X_STORE;
-    constexpr int NS = x_ns<FWD, LH>();
+    // X_FWDS: abuf = a_l tiles, dbuf = the lane-major cos buffer; X_REV: abuf = that cos buffer, dbuf = delta_l tiles
+    constexpr bool FWD = x_fwd_like(XM), ST = XM == X_STORE, FWS = XM == X_FWDS, RV = XM == X_REV;
+    constexpr int NS = x_ns<XM, LH>();
     constexpr int NW = x_waves<FWD>(), NT = 64 * NW, TILEX = 16 * NW, CPW = 24 / NW;
     static_assert(NS % X_NBUF == 0, "the ring must wrap onto slot 0 at a tile boundary");
     // the small-parameter block FIRST: its epilogue reads are then one base register + immediate offsets (after the
@@ -397,7 +459,7 @@ __global__ __launch_bounds__(64 * x_waves<XM == X_FWD>(), 1) void w1x_kernel(
     cx.ring = lds + SMALL;
     float* sm = lds;
     cx.sm = sm;
-    cx.stream = stream;
+    cx.stream = stream + (RV ? (int64_t)LH * X_SPG * X_SLICE : 0);  // X_REV: the reverse GEMMs' slices
     cx.lane = threadIdx.x & 63;
     cx.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     cx.g = cx.lane >> 4;
@@ -412,29 +474,32 @@ __global__ __launch_bounds__(64 * x_waves<XM == X_FWD>(), 1) void w1x_kernel(
         cx.inv_s0 = two_pi / w0;
     }
     cx.more = false;
-    cx.ta = cx.td = nullptr;
+    cx.ta = cx.td = cx.cs = nullptr;
     cx.lbytes = n_pad * H * 4;
     cx.vt = 4u * (4 * cx.g * 16 + c);
+    cx.vl = 16u * cx.lane;
     cx.ring_vaddr = lds_addr(cx.ring) + cx.lane * 16;
     cx.ring_vaddr2 = cx.ring_vaddr + 2 * X_SLICE * 4;
     {
         const int nf4 = (SM_BIAS + (LH + 1) * H + 3) / 4;
         for (int e = threadIdx.x; e < nf4; e += NT) ((f32x4*)sm)[e] = ((const f32x4*)ws_small)[e];
     }
-    const int64_t tiles = (n + TILEX - 1) / TILEX;
+    // the stored split writes its tiles for every n_pad coordinate (the wgrad reads the padding too; n_pad a multiple of
+    // 128, the forward's tile)
+    const int64_t tiles = (FWS || RV) ? n_pad / TILEX : (n + TILEX - 1) / TILEX;
     float xn[4], gn = 0.f;
     auto load_inputs = [&](int64_t tile) {
         const int64_t cd = tile * TILEX + cx.wave * 16 + c;
         const bool ok = tile < tiles && cd < n;
 #pragma unroll
         for (int k = 0; k < 4; ++k) xn[k] = (ok && k < D) ? x[cd * D + k] : 0.f;
-        if constexpr (ST) gn = ok ? gy[cd] : 0.f;
+        if constexpr (ST || RV) gn = ok ? gy[cd] : 0.f;
     };
     load_inputs(blockIdx.x);
     __syncthreads();
-    xring_issue<CPW>(stream, cx.ring, 0, cx.wave, 16u * cx.lane);
-    xring_issue<CPW>(stream, cx.ring, 1, cx.wave, 16u * cx.lane);
-    xring_issue<CPW>(stream, cx.ring, 2, cx.wave, 16u * cx.lane);
+    xring_issue<CPW>(cx.stream, cx.ring, 0, cx.wave, 16u * cx.lane);
+    xring_issue<CPW>(cx.stream, cx.ring, 1, cx.wave, 16u * cx.lane);
+    xring_issue<CPW>(cx.stream, cx.ring, 2, cx.wave, 16u * cx.lane);
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * CPW) : "memory");
     __builtin_amdgcn_s_barrier();
     x_read_wait01(st.pa[0], st.pa[1], cx.ring_vaddr);
@@ -448,13 +513,29 @@ __global__ __launch_bounds__(64 * x_waves<XM == X_FWD>(), 1) void w1x_kernel(
         for (int k = 0; k < 4; ++k) st.xv[k] = xn[k];
         st.yp = 0.f;
         st.gyv = gn;
-        if constexpr (ST) {
-            const int64_t tbase = (tile * NW + cx.wave) * (H * 16);  // wave-uniform
-            cx.ta = (const char*)(abuf + tbase);
-            cx.td = (const char*)(dbuf + tbase);
+        {
+            const int64_t wt = tile * NW + cx.wave;  // the 16-coordinate wave tile (wave-uniform)
+            const int64_t tbase = wt * (H * 16);
+            if constexpr (ST) {
+                cx.ta = (const char*)(abuf + tbase);
+                cx.td = (const char*)(dbuf + tbase);
+            }
+            if constexpr (FWS) {
+                cx.ta = (const char*)(abuf + tbase);
+                cx.cs = (const char*)(dbuf + x_cos_off(wt, LH));
+            }
+            if constexpr (RV) {
+                cx.td = (const char*)(dbuf + tbase);
+                cx.cs = (const char*)(abuf + x_cos_off(wt, LH));
+                // the seed's pre-GEMM blocks 0, 1 and its first in-slice block; later ones are reloaded by the mids
+                x_cos_issue<LH, 0>(st.cq[2], cx);
+                x_cos_issue<LH, 1>(st.cq[3], cx);
+                x_cos_issue<LH, 2>(st.cq[0], cx);
+                asm volatile("s_waitcnt vmcnt(0)" : "+v"(st.cq[0]), "+v"(st.cq[2]), "+v"(st.cq[3])::"memory");
+            }
         }
         load_inputs(tile + gridDim.x);
-        x_run<0, LH, D, XM>(st, cx);
+        x_run<x_g0<XM, LH>(), LH, D, XM>(st, cx);
         if constexpr (FWD) {
             // last hidden layer: a_L = sin(w z_L) and y = a_L Wout^T + bout (serial over the 16 blocks)
             constexpr int GL = (LH - 1) & 1;
@@ -463,15 +544,22 @@ __global__ __launch_bounds__(64 * x_waves<XM == X_FWD>(), 1) void w1x_kernel(
                 const int nb = 16 * rb + 4 * cx.g;
                 const f32x4 z = st.acc[GL][rb] + *(const f32x4*)(sm + SM_BIAS + LH * H + nb);
                 const f32x4 wo = *(const f32x4*)(sm + SM_WO + nb);
+                f32x4 sn4, cs4;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     float sn_, cs_;
                     sincos_rev(z[r], sn_, cs_);
                     st.yp += wo[r] * sn_;
+                    sn4[r] = sn_;
+                    cs4[r] = cs_;
+                }
+                if constexpr (FWS) {  // a_L tile and cos(w z_L) for the reverse's seed
+                    x_tile_store(cx.ta, cx, LH, rb, sn4);
+                    w3_store16(w3_at(cx.cs, (LH * NB + rb) * 1024), cx.vl, cs4);
                 }
             }
             const float yv = sum_groups(st.yp) + sm[SM_BOUT];
-            if (valid && cx.g == 0) y[coord] = yv;
+            if (y != nullptr && valid && cx.g == 0) y[coord] = yv;
             continue;
         }
         {
@@ -495,7 +583,7 @@ __global__ __launch_bounds__(64 * x_waves<XM == X_FWD>(), 1) void w1x_kernel(
                 c0[r] = cs_;
             }
             const f32x4 dl = (st.acc[GL][rb] * c0) * cx.w0;
-            if constexpr (ST) x_tile_store(cx.td, cx, 0, rb, dl);
+            if constexpr (ST || RV) x_tile_store(cx.td, cx, 0, rb, dl);
 #pragma unroll
             for (int k = 0; k < D; ++k) {
                 const f32x4 wk = *(const f32x4*)(sm + SM_W0 + k * H + 16 * rb + 4 * cx.g);
@@ -505,7 +593,7 @@ __global__ __launch_bounds__(64 * x_waves<XM == X_FWD>(), 1) void w1x_kernel(
 #pragma unroll
         for (int k = 0; k < D; ++k) {
             const float qk = sum_groups(q[k]) * cx.inv_s0;
-            if (valid && cx.g == 0 && (!ST || gx != nullptr)) gx[coord * D + k] = qk;
+            if (valid && cx.g == 0 && (!(ST || RV) || gx != nullptr)) gx[coord * D + k] = qk;
         }
     }
 }

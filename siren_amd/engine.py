@@ -225,6 +225,39 @@ class SirenEngine:
                                                  _ptr(gx), _ptr(gp), _stream(x.device)), 'siren_backward_split')
         return gx, gp
 
+    def forward_store_split(self, wsx, x):
+        """Training forward of the bf16x6 leg (siren_forward_store_split): (y, tws) — y from the split-bf16 forward, tws
+        its a_l tiles and cos(w z_l) for backward_stored_split."""
+        self._require()
+        if not self.split_supported:
+            raise _lib.SirenUnsupported('the split-bf16 kernels cover hidden 256, 3 hidden layers, in_features 2 / 3, '
+                                        'out_features 1, linear output')
+        x = self._check_x(x)
+        n = x.shape[0]
+        cnt = ctypes.c_int64()
+        _lib.check(self.lib.siren_train_split_ws_floats(ctypes.byref(self.cfg), n, ctypes.byref(cnt)),
+                   'siren_train_split_ws_floats')
+        tws = torch.empty(cnt.value, dtype=torch.float32, device=x.device)
+        y = torch.empty(n, 1, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_forward_store_split(ctypes.byref(self.cfg), _ptr(wsx), _ptr(x), n, _ptr(y), _ptr(tws),
+                                                      _stream(x.device)), 'siren_forward_store_split')
+        return y, tws
+
+    def backward_stored_split(self, wsx, x, gy, tws, want_gx=False):
+        """Reverse-only backward of the bf16x6 leg from forward_store_split's tws: (gx or None, gparams)."""
+        self._require()
+        x = self._check_x(x)
+        n = x.shape[0]
+        gy = gy.contiguous()
+        if gy.shape != (n, 1) or gy.dtype != torch.float32 or gy.device != x.device:
+            raise ValueError('gy must be fp32 (%d, 1) on the coords device; got %s' % (n, tuple(gy.shape)))
+        gx = torch.empty(n, self.cfg.d_in, dtype=torch.float32, device=x.device) if want_gx else None
+        gp = torch.empty(self.param_count, dtype=torch.float32, device=x.device)
+        _lib.check(self.lib.siren_backward_stored_split(ctypes.byref(self.cfg), _ptr(wsx), _ptr(x), n, _ptr(gy),
+                                                        _ptr(tws), _ptr(gx), _ptr(gp), _stream(x.device)),
+                   'siren_backward_stored_split')
+        return gx, gp
+
     def _fwd_workspace(self, n, device):
         """siren_forward_ex's caller-owned scratch (the layered path's chunk scratch; None elsewhere)."""
         cnt = ctypes.c_int64()

@@ -296,14 +296,14 @@ def test_backward_split_zero_coords(cuda):
 
 
 def test_module_precision_bf16x6_training_step(cuda, g1, monkeypatch):
-    """SingleBVPNet(precision='bf16x6') under image_mse training: the θ-gradients come from siren_backward_split (the
-    fp32 W2 entry points are forbidden here) and match G1's fp64 golden; y is the split forward's."""
+    """SingleBVPNet(precision='bf16x6') under image_mse training: the θ-gradients come from the stored bf16x6 split (the
+    fp32 W2 entry points and the recompute form are forbidden here) and match G1's fp64 golden; y is the split forward's."""
     from siren_amd import loss_functions as Lf, modules
     from siren_amd.engine import SirenEngine
 
     def boom(*a, **k):
         raise AssertionError('the fp32 W2 path ran')
-    for nm in ('backward_params', 'backward_stored', 'forward_store', 'forward'):
+    for nm in ('backward_params', 'backward_stored', 'forward_store', 'forward', 'backward_split'):
         monkeypatch.setattr(SirenEngine, nm, boom)
     sd = {k[2:]: np.asarray(g1[k]) for k in g1.keys() if k.startswith('w_net.')}
     m = modules.SingleBVPNet(in_features=2, verbose=False, precision='bf16x6').to(cuda)
@@ -316,3 +316,40 @@ def test_module_precision_bf16x6_training_step(cuda, g1, monkeypatch):
     for k, p in m.named_parameters():
         ref = g1['G1_image_mse_grad_' + k]
         assert np.max(np.abs(p.grad.cpu().numpy() - ref)) <= 1e-4 * max(np.max(np.abs(ref)), 1e-30) + 1e-12, k
+
+
+@pytest.mark.parametrize('n,d', [(1, 2), (100, 3), (5000, 2), (70000, 3), (1 << 18, 2)])
+def test_stored_split_matches_recompute(cuda, n, d):
+    """The stored bf16x6 split (forward keeps a_l / cos, reverse-only backward) against the recompute form
+    (siren_backward_split) and fp64 autograd: same kernels' arithmetic, so the θ-gradients agree to the last bits
+    (bitwise where the tile sums meet in the same order), and y matches the split W0."""
+    layers = random_layers(d, seed=3 * n + d)
+    eng = engine(d)
+    fdev = to_dev(O.flatten(layers), cuda)
+    wsx = eng.pack_split(fdev)
+    rng = np.random.default_rng(n)
+    x = to_dev(rng.uniform(-1, 1, (n, d)), cuda)
+    gy = to_dev(rng.normal(size=(n, 1)) / n, cuda)
+    y, tws = eng.forward_store_split(wsx, x)
+    assert torch.equal(y, eng.forward_split(wsx, x))
+    gx, gp = eng.backward_stored_split(wsx, x, gy, tws, want_gx=True)
+    gx_r, gp_r = eng.backward_split(wsx, x, gy, want_gx=True)
+    scale = float(gp_r.abs().max())
+    assert float((gp - gp_r).abs().max()) <= 1e-6 * scale, float((gp - gp_r).abs().max()) / scale
+    assert float((gx - gx_r).abs().max()) <= 1e-6 * max(1., float(gx_r.abs().max()))
+    if n <= 5000:
+        xt = torch.tensor(x.cpu().numpy(), dtype=torch.float64)
+        params = [torch.tensor(np.asarray(t), dtype=torch.float64, requires_grad=True) for W, b in layers for t in (W, b)]
+        yt = O.torch_forward(xt, params)
+        g = torch.autograd.grad(yt, params, torch.tensor(gy.cpu().numpy(), dtype=torch.float64))
+        rgp = torch.cat([t.reshape(-1) for t in g]).numpy()
+        assert np.max(np.abs(gp.cpu().numpy() - rgp)) <= 1e-4 * np.max(np.abs(rgp))
+
+
+def test_stored_split_zero_coords(cuda):
+    eng = engine()
+    wsx = eng.pack_split(to_dev(O.flatten(random_layers(2)), cuda))
+    y, tws = eng.forward_store_split(wsx, torch.empty(0, 2, device=cuda))
+    gx, gp = eng.backward_stored_split(wsx, torch.empty(0, 2, device=cuda), torch.empty(0, 1, device=cuda), tws,
+                                       want_gx=True)
+    assert y.shape == (0, 1) and gx.shape == (0, 2) and torch.count_nonzero(gp) == 0

@@ -30,7 +30,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 PATHS = {  # name: (d, hidden, layers, o, n, work units of F)
     'image_w2': (2, 256, 3, 1, 1 << 18, 3),
-    'image_w2x': (2, 256, 3, 1, 1 << 18, 3),  # the bf16x6 training leg: split W0 forward + siren_backward_split
+    'image_w2x': (2, 256, 3, 1, 1 << 18, 3),  # the bf16x6 training leg: stored split-bf16 forward + reverse-only backward
     'sdf': (3, 256, 3, 1, 1 << 19, 8),
     'video': (3, 512, 3, 3, 1 << 20, 3),
     'poisson': (2, 256, 3, 1, 512 * 512, 15),
@@ -116,8 +116,8 @@ def build_step(name, dev):
     if name == 'image_w2x':
         def step():
             wsx = eng.pack_split(flat)  # once per weight update, as SirenSplitFunction does
-            eng.forward_split(wsx, x)
-            eng.backward_split(wsx, x, gy)
+            _, tws = eng.forward_store_split(wsx, x)
+            eng.backward_stored_split(wsx, x, gy, tws)
         return step
     if name in ('image_w2', 'video'):
         def step():
