@@ -353,3 +353,40 @@ def test_stored_split_zero_coords(cuda):
     gx, gp = eng.backward_stored_split(wsx, torch.empty(0, 2, device=cuda), torch.empty(0, 1, device=cuda), tws,
                                        want_gx=True)
     assert y.shape == (0, 1) and gx.shape == (0, 2) and torch.count_nonzero(gp) == 0
+
+
+def test_g5_psnr_trajectory_bf16x6(cuda, manifest, monkeypatch):
+    """Config 1 in the bf16x6 training mode: 300 Adam steps on the 256^2 synthetic image through the stored split-bf16
+    forward / reverse and the bf16x6 wgrad (the fp32 W2 entry points forbidden) track the reference's loss trajectory
+    within 2 % and reach its PSNR within 0.05 dB, as the fp32 engine does (test_gpu_parity.py)."""
+    import os
+    from siren_amd.modules import SingleBVPNet
+    from siren_amd import dataio
+    from siren_amd.engine import SirenEngine
+
+    def boom(*a, **k):
+        raise AssertionError('the fp32 W2 path ran')
+    for nm in ('backward_params', 'backward_stored', 'forward_store'):
+        monkeypatch.setattr(SirenEngine, nm, boom)
+    fit = dict(np.load(os.path.join(os.path.dirname(__file__), 'golden', 'golden_fit.npz')))
+    torch.manual_seed(0)
+    m = SingleBVPNet(verbose=False, precision='bf16x6').to(cuda)
+    for k, v in m.state_dict().items():
+        assert np.array_equal(v.cpu().numpy(), fit['init_' + k])
+    opt = torch.optim.Adam(m.parameters(), lr=1e-4)
+    grid = dataio.get_mgrid(256)[None].to(cuda)
+    img = dataio.synthetic_image(grid)
+    losses = []
+    for _ in range(300):
+        out = m({'coords': grid})
+        loss = ((out['model_out'] - img) ** 2).mean()
+        losses.append(float(loss))
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    with torch.no_grad():
+        p = dataio.psnr(m({'coords': grid})['model_out'], img)
+    ref = fit['losses']
+    assert abs(p - manifest['G5_psnr_final']) < 0.05, (p, manifest['G5_psnr_final'])
+    for i in range(0, 300, 10):
+        assert abs(losses[i] - ref[i]) <= 0.02 * ref[i] + 1e-6, (i, losses[i], ref[i])
