@@ -102,7 +102,7 @@ __device__ __forceinline__ void split_block(const f32x4& v, u32x4 (&p)[3]) {
 template <int LH>
 struct XState {
     float gyv;         // X_STORE / X_REV: this lane's output cotangent
-    f32x4 cq[4];       // X_REV: reloaded cos blocks: an in-slice epilogue block b in cq[b & 1], pre-GEMM blocks 0, 1 in 2, 3
+    f32x4 cq[8];       // X_REV: reloaded cos blocks, block u of the tile's consumption order in cq[u % 8] (x_cos_n)
     u32x4 bx[2][3];    // B operand pieces (hi, mid, lo) of K-step s in bx[s & 1]
     f32x4 acc[2][NB];  // ping-pong accumulators (GEMM G in acc[G & 1])
     f32x4 C[LH][NB];   // cos(w z_l), 1 <= l < LH (layer 0's is recomputed at the end: 64 fewer live registers)
@@ -240,17 +240,43 @@ constexpr int x_st_pre(int s, int lh, int xm) {
 // after it come the epilogue stores of S - 2, the pre-GEMM blocks before S - 1, ring slice S + 2 (CPW pieces), the
 // epilogue stores of S - 1 and the pre-GEMM blocks before S. The first two slices of a tile count CPW (the previous
 // tile's serial tail sits between: CPW waits for more than needed, never less).
-// X_REV: the cos blocks an epilogue of slice S reads (its in-slice block; at S % X_SPG = X_SPG - 1 the next GEMM's
-// pre-GEMM blocks) are loaded at the mid of S - 1 ahead of ring slice S + 2, so only that ring slice and the stores
-// issued after it may stay in flight.
+// X_REV reloads the cos block of each epilogue block X_COS_LEAD slices ahead (a split-bf16 slice is half a K-step,
+// ~0.35 us: one slice of lead exposed the load latency, 0.36 of wave cycles waiting). A tile consumes its cos blocks in
+// the order u = 16 r + b (block b of reverse GEMM r; b = 0, 1 before the GEMM's first slice, b >= 2 in slice 16 r + b
+// - 2); the mid of slice m loads the in-slice block of slice m + X_COS_LEAD and, when slice m + X_COS_LEAD + 1 starts a
+// GEMM, that GEMM's blocks 0, 1, into cq[u % 8] (the live blocks are a run of at most X_COS_LEAD + 3).
+#ifndef X_COS_LEAD
+#define X_COS_LEAD 4
+#endif
+constexpr int X_CQ = 8;
+static_assert(X_COS_LEAD >= 1 && X_COS_LEAD + 3 <= X_CQ, "cos reload slots");
+constexpr int x_cos_n(int m, int lh) {  // cos loads issued at the mid of slice m
+    const int ns = lh * X_SPG, t = m + X_COS_LEAD;
+    return (t < ns && t % X_SPG <= X_SPG - 3 ? 1 : 0) + (t + 1 < ns && (t + 1) % X_SPG == 0 ? 2 : 0);
+}
+// X_REV: at the mid of slice S the blocks loaded at the mid of S - X_COS_LEAD must have landed (the in-slice block of S,
+// and the next GEMM's pre-GEMM blocks when S ends a GEMM); after them: that mid's ring issue, the loads and ring issues
+// of the mids in between, the epilogue stores of slices S - X_COS_LEAD .. S - 1 and the pre-GEMM stores before the GEMMs
+// starting in (S - X_COS_LEAD, S]. Before slice X_COS_LEAD everything was loaded at the tile start (waited there).
+constexpr int x_allow_rev(int S, int lh, int cpw) {
+    int n = cpw;
+    for (int m = S - X_COS_LEAD + 1; m < S; ++m) n += x_cos_n(m, lh) + cpw;
+    for (int s = S - X_COS_LEAD; s < S; ++s) n += x_st_slice(s, lh, X_REV);
+    for (int s = S - X_COS_LEAD + 1; s <= S; ++s) n += x_st_pre(s, lh, X_REV);
+    return n;
+}
 template <int S, int LH, int XM, int CPW>
 constexpr int x_allow() {
     if constexpr ((XM != X_STORE && XM != X_FWDS && XM != X_REV) || S < 2) {
         return CPW;
     } else if constexpr (XM == X_REV) {
-        constexpr int n = CPW + x_st_slice(S - 1, LH, XM) + x_st_pre(S, LH, XM);
-        static_assert(n < 64, "vmcnt is 6 bits");
-        return n;
+        if constexpr (S < X_COS_LEAD) {
+            return CPW;
+        } else {
+            constexpr int n = x_allow_rev(S, LH, CPW);
+            static_assert(n < 64, "vmcnt is 6 bits");
+            return n;
+        }
     } else {
         constexpr int n = CPW + x_st_slice(S - 2, LH, XM) + x_st_pre(S - 1, LH, XM) + x_st_slice(S - 1, LH, XM) +
                           x_st_pre(S, LH, XM);
@@ -270,7 +296,7 @@ static_assert(X_EPI_AT >= 4, "the in-slice epilogue's stores are counted after t
 template <int E, int B, int LH, int D, int XM>
 __device__ __forceinline__ void x_epilogue(XState<LH>& st, const XCtx& cx) {
     constexpr bool FWD = x_fwd_like(XM), ST = XM == X_STORE, FWS = XM == X_FWDS, RV = XM == X_REV;
-    constexpr int CQ = B < 2 ? 2 + B : (B & 1);  // X_REV: the reloaded cos block's slot
+    constexpr int CQ = (XM == X_REV ? (16 * (E - LH) + B) % X_CQ : 0);  // X_REV: the reloaded cos block's slot
     constexpr int KS = B >> 1, HALF = B & 1;
     const int nb = 16 * B + 4 * cx.g;
     u32x4(&p)[3] = st.bx[KS & 1];
@@ -363,20 +389,19 @@ __device__ __forceinline__ void x_slice(XState<LH>& st, const XCtx& cx) {
                 else
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if constexpr (XM == X_REV) {
-                    // landed: this slice's in-slice cos block and, in the last slice of a GEMM, the next GEMM's
-                    // pre-GEMM blocks; then the next slice's block and (second-to-last slice) the next GEMM's blocks
-                    constexpr int R = 2 * KS + HALF;  // slice within the GEMM
-                    if constexpr (KS + 1 < X_KSTEPS) asm volatile("" : "+v"(st.cq[HALF]));
-                    if constexpr (R == X_SPG - 1 && G + 1 < 2 * LH) asm volatile("" : "+v"(st.cq[2]), "+v"(st.cq[3]));
-                    constexpr int R1 = R + 1, KS1 = R1 >> 1, H1 = R1 & 1;
-                    if constexpr (R1 < X_SPG && KS1 + 1 < X_KSTEPS)
-                        x_cos_issue<x_rev_layer(G, LH), 2 * (KS1 + 1) + H1>(st.cq[H1], cx);
-                    if constexpr (R == X_SPG - 2 && G + 1 < 2 * LH) {
-                        x_cos_issue<x_rev_layer(G + 1, LH), 0>(st.cq[2], cx);
-                        x_cos_issue<x_rev_layer(G + 1, LH), 1>(st.cq[3], cx);
+                    // landed: this slice's in-slice cos block and, in a GEMM's last slice, the next GEMM's blocks 0, 1
+                    if constexpr (S % X_SPG <= X_SPG - 3)
+                        asm volatile("" : "+v"(st.cq[(S + 2) % X_CQ]));  // u = 16 (S / 16) + S % 16 + 2
+                    if constexpr ((S + 1) % X_SPG == 0 && S + 1 < NS)
+                        asm volatile("" : "+v"(st.cq[(S + 1) % X_CQ]), "+v"(st.cq[(S + 2) % X_CQ]));
+                    // reload X_COS_LEAD slices ahead (x_cos_n)
+                    constexpr int T = S + X_COS_LEAD;
+                    if constexpr (T < NS && T % X_SPG <= X_SPG - 3)
+                        x_cos_issue<x_rev_layer(LH + T / X_SPG, LH), T % X_SPG + 2>(st.cq[(T + 2) % X_CQ], cx);
+                    if constexpr (T + 1 < NS && (T + 1) % X_SPG == 0) {
+                        x_cos_issue<x_rev_layer(LH + (T + 1) / X_SPG, LH), 0>(st.cq[(T + 1) % X_CQ], cx);
+                        x_cos_issue<x_rev_layer(LH + (T + 1) / X_SPG, LH), 1>(st.cq[(T + 2) % X_CQ], cx);
                     }
-                    if constexpr (R == X_SPG - 1 && G + 1 < 2 * LH)  // the next GEMM's first in-slice block
-                        x_cos_issue<x_rev_layer(G + 1, LH), 2>(st.cq[0], cx);
                 }
                 __builtin_amdgcn_s_barrier();
                 if (S + 3 < NS || cx.more) {
@@ -527,11 +552,12 @@ __global__ __launch_bounds__(64 * x_waves<x_fwd_like(XM)>(), 1) void w1x_kernel(
             if constexpr (RV) {
                 cx.td = (const char*)(dbuf + tbase);
                 cx.cs = (const char*)(abuf + x_cos_off(wt, LH));
-                // the seed's pre-GEMM blocks 0, 1 and its first in-slice block; later ones are reloaded by the mids
-                x_cos_issue<LH, 0>(st.cq[2], cx);
-                x_cos_issue<LH, 1>(st.cq[3], cx);
-                x_cos_issue<LH, 2>(st.cq[0], cx);
-                asm volatile("s_waitcnt vmcnt(0)" : "+v"(st.cq[0]), "+v"(st.cq[2]), "+v"(st.cq[3])::"memory");
+                // the seed's blocks 0 .. X_COS_LEAD + 1 (pre-GEMM 0, 1 and the first X_COS_LEAD slices' in-slice blocks);
+                // later ones are reloaded by the mids
+                xstatic_for<0, X_COS_LEAD + 2>([&](auto U) { x_cos_issue<LH, decltype(U)::value>(st.cq[decltype(U)::value], cx); });
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+                for (int u = 0; u < X_COS_LEAD + 2; ++u) asm volatile("" : "+v"(st.cq[u]));
             }
         }
         load_inputs(tile + gridDim.x);
