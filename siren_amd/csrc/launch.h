@@ -60,6 +60,7 @@ void launch_wgradx(dim3 grid, hipStream_t st, const float* abuf, const float* db
                    float* partial, int64_t P, int d, int o, int lh);
 // the forward-only split W0 (8 waves, 128 coordinates per workgroup tile)
 int split_fwd_tile();
+int split_rev_tile();  // the X_REV tile: 16 coordinates per wave
 void launch_w0x(dim3 grid, hipStream_t st, const float* ws_small, const unsigned* stream, const float* x, int64_t n,
                 float* y, int d, float w0, float w);
 // tu_w4.hip: JET mode (16 coordinates per workgroup); lap (n) = sum_j Laplacian(y_j), gx (n, d) = sum_j grad y_j

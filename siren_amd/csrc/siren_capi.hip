@@ -476,7 +476,7 @@ int32_t siren_backward_stored_split(const siren_cfg* cfg, const float* wsx, cons
     float* dbuf = tws + plan.act_floats;
     float* partial = tws + 2 * plan.act_floats;
     const int64_t spad = small_pad(cfg);
-    siren::launch_w1xr(tile_grid(cfg, plan.n_pad / siren::TILE, 1), st, wsx + spad, (const unsigned*)(wsx + 2 * spad),
+    siren::launch_w1xr(tile_grid(cfg, plan.n_pad / siren::split_rev_tile(), 1), st, wsx + spad, (const unsigned*)(wsx + 2 * spad),
                        x, n, gy, gx, tws + plan.total, dbuf, plan.n_pad, cfg->d_in, cfg->omega_first,
                        cfg->omega_hidden);
     if (int rc = hip_status("siren_backward_stored_split (split reverse)")) return rc;

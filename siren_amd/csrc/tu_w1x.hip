@@ -53,14 +53,15 @@ void launch_w0xs(dim3 grid, hipStream_t st, const float* ws_small, const unsigne
 void launch_w1xr(dim3 grid, hipStream_t st, const float* ws_small, const unsigned* stream, const float* x, int64_t n,
                  const float* gy, float* gx, const float* cbuf, float* dbuf, int64_t n_pad, int d, float w0, float w) {
     if (d == 2)
-        hipLaunchKernelGGL((w1x_kernel<3, 2, X_REV>), grid, dim3(64 * x_waves<false>()), 0, st, ws_small, stream, x,
+        hipLaunchKernelGGL((w1x_kernel<3, 2, X_REV>), grid, dim3(64 * x_nw<X_REV>()), 0, st, ws_small, stream, x,
                            n, (float*)nullptr, gx, w0, w, gy, const_cast<float*>(cbuf), dbuf, n_pad);
     else
-        hipLaunchKernelGGL((w1x_kernel<3, 3, X_REV>), grid, dim3(64 * x_waves<false>()), 0, st, ws_small, stream, x,
+        hipLaunchKernelGGL((w1x_kernel<3, 3, X_REV>), grid, dim3(64 * x_nw<X_REV>()), 0, st, ws_small, stream, x,
                            n, (float*)nullptr, gx, w0, w, gy, const_cast<float*>(cbuf), dbuf, n_pad);
 }
 
 int split_fwd_tile() { return 16 * x_waves<true>(); }
+int split_rev_tile() { return 16 * x_nw<X_REV>(); }
 
 void launch_w0x(dim3 grid, hipStream_t st, const float* ws_small, const unsigned* stream, const float* x, int64_t n,
                 float* y, int d, float w0, float w) {

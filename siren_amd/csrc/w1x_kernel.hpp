@@ -99,16 +99,21 @@ __device__ __forceinline__ void split_block(const f32x4& v, u32x4 (&p)[3]) {
     p[2][2 * HALF + 1] = l1;
 }
 
+// X_REV: cos reload slots (see x_cos_n)
+#ifndef X_CQ
+#define X_CQ 8
+#endif
 template <int LH>
 struct XState {
     float gyv;         // X_STORE / X_REV: this lane's output cotangent
-    f32x4 cq[8];       // X_REV: reloaded cos blocks, block u of the tile's consumption order in cq[u % 8] (x_cos_n)
+    f32x4 cq[X_CQ < 6 ? 6 : X_CQ];  // X_REV: reloaded cos blocks, block u of a tile's consumption order in cq[u % X_CQ]
     u32x4 bx[2][3];    // B operand pieces (hi, mid, lo) of K-step s in bx[s & 1]
     f32x4 acc[2][NB];  // ping-pong accumulators (GEMM G in acc[G & 1])
     f32x4 C[LH][NB];   // cos(w z_l), 1 <= l < LH (layer 0's is recomputed at the end: 64 fewer live registers)
     u32x4 pa[3][3];    // A pieces of output blocks b, b + 1, b + 2 of the tile's block sequence (b % 3)
     float xv[4];
     float yp;
+    float xn[4], gn;   // X_REV: the next tile's coordinates and cotangent, loaded at the mid of slice 0 (x_next_issue)
 };
 
 struct XCtx {
@@ -121,6 +126,9 @@ struct XCtx {
     const char* ta;        // X_STORE: wave-uniform a_l tile base of (tile, wave), layer 0; layer l at + l * lbytes
     const char* td;        // X_STORE: the same for delta_l
     const char* cs;        // X_FWDS / X_REV: wave-uniform lane-major cos base of the wave tile (x_cos_off), + 16 lane
+    const char* cs_next;   // X_REV: the same for the next tile (its first cos blocks are loaded at the mid of NS - 2)
+    const float* xq;       // X_REV: this lane's x row and gy entry of the next tile (clamped to coordinate n - 1)
+    const float* gq;
     int64_t lbytes;
     unsigned vl;           // 16 lane
     unsigned vt;           // X_STORE: this lane's byte offset in a tile block, 4 (4 g 16 + c)
@@ -193,6 +201,12 @@ __device__ __forceinline__ void xstatic_for(F&& f) {
         xstatic_for<I + 1, N>(f);
     }
 }
+#ifndef X_REV_WAVES
+#define X_REV_WAVES 4
+#endif
+// waves per workgroup of mode XM (X_REV: X_REV_WAVES)
+template <int XM>
+constexpr int x_nw() { return x_fwd_like(XM) ? 8 : XM == X_REV ? X_REV_WAVES : 4; }
 
 __device__ __forceinline__ f32x4 x_to_agpr(f32x4 v) {
     f32x4 r;
@@ -248,7 +262,6 @@ constexpr int x_st_pre(int s, int lh, int xm) {
 #ifndef X_COS_LEAD
 #define X_COS_LEAD 4
 #endif
-constexpr int X_CQ = 8;
 static_assert(X_COS_LEAD >= 1 && X_COS_LEAD + 3 <= X_CQ, "cos reload slots");
 constexpr int x_cos_n(int m, int lh) {  // cos loads issued at the mid of slice m
     const int ns = lh * X_SPG, t = m + X_COS_LEAD;
@@ -265,18 +278,38 @@ constexpr int x_allow_rev(int S, int lh, int cpw) {
     for (int s = S - X_COS_LEAD + 1; s <= S; ++s) n += x_st_pre(s, lh, X_REV);
     return n;
 }
-template <int S, int LH, int XM, int CPW>
+// X_REV, ring constraint: ring slice S + 1 must have landed at the mid of S. It was issued at the mid of S - 2 (for
+// S < 2 at the previous tile's mids NS - 2, NS - 1); after it come, in issue order, the epilogue stores of S - 2, the
+// pre-GEMM stores before S - 1, the mid of S - 1 (its cos reloads, at NS - 2 the next tile's first X_COS_LEAD + 2 cos
+// blocks (x_next_cos), its ring slice), the epilogue stores of S - 1 and the pre-GEMM stores before S. Across the tile
+// boundary: the previous tile's 64 delta_0 tile stores, the seed's two pre-GEMM blocks, and at the mid of slice 0 the
+// next tile's D + 1 input loads (x_next_issue) before its ring slice. The compiler's own conditional y / gx stores only
+// add younger operations (waiting for more, never less); 63 is the counter's maximum.
+constexpr int x_allow_ring_rev(int S, int lh, int cpw, int d) {
+    const int ns = lh * X_SPG, pre0 = 2 * x_epi_nst(lh, lh, X_REV);
+    int n = 0;
+    if (S == 0)
+        n = cpw + 64 + pre0;
+    else if (S == 1)
+        n = 64 + pre0 + x_cos_n(0, lh) + (d + 1) + cpw + x_st_slice(0, lh, X_REV);
+    else
+        n = x_st_slice(S - 2, lh, X_REV) + x_st_pre(S - 1, lh, X_REV) + x_cos_n(S - 1, lh) +
+            (S - 1 == ns - 2 ? X_COS_LEAD + 2 : 0) + cpw + x_st_slice(S - 1, lh, X_REV) + x_st_pre(S, lh, X_REV);
+    return n < 63 ? n : 63;
+}
+template <int S, int LH, int XM, int CPW, int D = 2>
 constexpr int x_allow() {
-    if constexpr ((XM != X_STORE && XM != X_FWDS && XM != X_REV) || S < 2) {
-        return CPW;
-    } else if constexpr (XM == X_REV) {
+    if constexpr (XM == X_REV) {
+        // the cos blocks of slices < X_COS_LEAD were waited at the tile start; later ones at the mid of S - X_COS_LEAD
+        constexpr int r = x_allow_ring_rev(S, LH, CPW, D);
         if constexpr (S < X_COS_LEAD) {
-            return CPW;
+            return r;
         } else {
-            constexpr int n = x_allow_rev(S, LH, CPW);
-            static_assert(n < 64, "vmcnt is 6 bits");
-            return n;
+            constexpr int c = x_allow_rev(S, LH, CPW);
+            return c < r ? c : r;
         }
+    } else if constexpr ((XM != X_STORE && XM != X_FWDS) || S < 2) {
+        return CPW;
     } else {
         constexpr int n = CPW + x_st_slice(S - 2, LH, XM) + x_st_pre(S - 1, LH, XM) + x_st_slice(S - 1, LH, XM) +
                           x_st_pre(S, LH, XM);
@@ -290,6 +323,28 @@ constexpr int x_rev_layer(int e, int lh) { return e == lh ? lh : 2 * lh - e; }
 template <int L, int B>
 __device__ __forceinline__ void x_cos_issue(f32x4& r, const XCtx& cx) {
     asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(r) : "v"(cx.vl), "s"(w3_at(cx.cs, (L * NB + B) * 1024)));
+}
+// X_REV, across the tile boundary: the next tile's first X_COS_LEAD + 2 cos blocks (the seed's pre-GEMM blocks 0, 1 and
+// the in-slice blocks of its first X_COS_LEAD slices) into cq[0 ..], issued at the mid of slice NS - 2, when every
+// block of this tile has been consumed, and waited (counted) at the next tile's start; and its D coordinates and gy
+// entry, issued at the mid of slice 0 (before that mid's ring slice). Both are inline asm the compiler does not count:
+// a compiler load consumed at the tile start made it drain the counter there (vmcnt(0) right after issuing the next
+// tile's loads), a full memory latency per 64-coordinate tile. The inputs land in AGPRs and stay there until the
+// tile start's wait names them (a VGPR destination was copied to an AGPR by the compiler while still in flight); so do
+// the next tile's first cos blocks.
+template <int LH, int U>
+__device__ __forceinline__ void x_next_cos1(f32x4& r, const XCtx& cx) {
+    asm volatile("global_load_dwordx4 %0, %1, %2" : "=a"(r) : "v"(cx.vl), "s"(w3_at(cx.cs_next, (LH * NB + U) * 1024)));
+}
+template <int LH>
+__device__ __forceinline__ void x_next_cos(XState<LH>& st, const XCtx& cx) {
+    xstatic_for<0, X_COS_LEAD + 2>([&](auto U) { x_next_cos1<LH, decltype(U)::value>(st.cq[decltype(U)::value], cx); });
+}
+template <int D, int LH>
+__device__ __forceinline__ void x_next_issue(XState<LH>& st, const XCtx& cx) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) asm volatile("global_load_dword %0, %1, off" : "=a"(st.xn[k]) : "v"(cx.xq + k) : "memory");
+    asm volatile("global_load_dword %0, %1, off" : "=a"(st.gn) : "v"(cx.gq) : "memory");
 }
 static_assert(X_EPI_AT >= 4, "the in-slice epilogue's stores are counted after the mid-slice wait");
 
@@ -369,7 +424,7 @@ template <int G, int KS, int HALF, int LH, int D, int XM>
 __device__ __forceinline__ void x_slice(XState<LH>& st, const XCtx& cx) {
     constexpr bool FWD = x_fwd_like(XM);
     constexpr int NS = x_ns<XM, LH>();
-    constexpr int CPW = 24 / x_waves<FWD>();
+    constexpr int CPW = 24 / x_nw<XM>();
     constexpr int S = (G - x_g0<XM, LH>()) * X_SPG + 2 * KS + HALF;
     constexpr int SLOT = (S % X_NBUF) * X_SLICE * 4;
     constexpr int NSLOT = ((S + 1) % X_NBUF) * X_SLICE * 4;
@@ -383,9 +438,9 @@ __device__ __forceinline__ void x_slice(XState<LH>& st, const XCtx& cx) {
         if constexpr (obl == 4) {
             if (S + 1 < NS || cx.more) {
                 if constexpr (S + 2 < NS)
-                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(x_allow<S, LH, XM, CPW>()) : "memory");
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(x_allow<S, LH, XM, CPW, D>()) : "memory");
                 else if (cx.more)
-                    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(CPW) : "memory");
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(XM == X_REV ? x_allow<S, LH, XM, CPW, D>() : CPW) : "memory");
                 else
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if constexpr (XM == X_REV) {
@@ -402,8 +457,12 @@ __device__ __forceinline__ void x_slice(XState<LH>& st, const XCtx& cx) {
                         x_cos_issue<x_rev_layer(LH + (T + 1) / X_SPG, LH), 0>(st.cq[(T + 1) % X_CQ], cx);
                         x_cos_issue<x_rev_layer(LH + (T + 1) / X_SPG, LH), 1>(st.cq[(T + 2) % X_CQ], cx);
                     }
+                    if constexpr (S == NS - 2) {
+                        if (cx.more) x_next_cos<LH>(st, cx);
+                    }
                 }
                 __builtin_amdgcn_s_barrier();
+                if constexpr (XM == X_REV && S == 0) x_next_issue<D>(st, cx);
                 if (S + 3 < NS || cx.more) {
                     const unsigned* sp = cx.stream;
                     asm volatile("" : "+s"(sp));
@@ -466,14 +525,14 @@ __device__ __forceinline__ void x_run(XState<LH>& st, const XCtx& cx) {
 // (n, D) (y nullable; X_STORE: gx nullable). w0 / w as the fp32 kernel (phase-scaled pack). X_STORE: gy (n) the output
 // cotangent, abuf / dbuf the a_l / delta_l tiles (L + 1 layers of n_pad H floats each, the wgrad layout).
 template <int LH, int D, int XM>
-__global__ __launch_bounds__(64 * x_waves<x_fwd_like(XM)>(), 1) void w1x_kernel(
+__global__ __launch_bounds__(64 * x_nw<XM>(), 1) void w1x_kernel(
     const float* __restrict__ ws_small, const unsigned* __restrict__ stream, const float* __restrict__ x, int64_t n,
     float* __restrict__ y, float* __restrict__ gx, float w0, float w, const float* __restrict__ gy = nullptr,
     float* __restrict__ abuf = nullptr, float* __restrict__ dbuf = nullptr, int64_t n_pad = 0) {
     // X_FWDS: abuf = a_l tiles, dbuf = the lane-major cos buffer; X_REV: abuf = that cos buffer, dbuf = delta_l tiles
     constexpr bool FWD = x_fwd_like(XM), ST = XM == X_STORE, FWS = XM == X_FWDS, RV = XM == X_REV;
     constexpr int NS = x_ns<XM, LH>();
-    constexpr int NW = x_waves<FWD>(), NT = 64 * NW, TILEX = 16 * NW, CPW = 24 / NW;
+    constexpr int NW = x_nw<XM>(), NT = 64 * NW, TILEX = 16 * NW, CPW = 24 / NW;
     static_assert(NS % X_NBUF == 0, "the ring must wrap onto slot 0 at a tile boundary");
     // the small-parameter block FIRST: its epilogue reads are then one base register + immediate offsets (after the
     // 96 KiB ring they were out of ds offset range, and the compiler kept ~50 per-block addresses live and spilled them)
@@ -520,7 +579,7 @@ __global__ __launch_bounds__(64 * x_waves<x_fwd_like(XM)>(), 1) void w1x_kernel(
         for (int k = 0; k < 4; ++k) xn[k] = (ok && k < D) ? x[cd * D + k] : 0.f;
         if constexpr (ST || RV) gn = ok ? gy[cd] : 0.f;
     };
-    load_inputs(blockIdx.x);
+    if constexpr (!RV) load_inputs(blockIdx.x);
     __syncthreads();
     xring_issue<CPW>(cx.stream, cx.ring, 0, cx.wave, 16u * cx.lane);
     xring_issue<CPW>(cx.stream, cx.ring, 1, cx.wave, 16u * cx.lane);
@@ -528,16 +587,51 @@ __global__ __launch_bounds__(64 * x_waves<x_fwd_like(XM)>(), 1) void w1x_kernel(
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * CPW) : "memory");
     __builtin_amdgcn_s_barrier();
     x_read_wait01(st.pa[0], st.pa[1], cx.ring_vaddr);
+    auto next_inputs = [&](int64_t tile) {  // X_REV: x_next_issue's addresses (clamped: the loads are unconditional)
+        int64_t cd = tile * TILEX + cx.wave * 16 + c;
+        cd = cd < n ? cd : n - 1;
+        cx.xq = x + cd * D;
+        cx.gq = gy + cd;
+    };
+    if constexpr (RV) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) st.xn[k] = 0.f;
+        st.gn = 0.f;
+        if (blockIdx.x < tiles) {
+            // the first tile's blocks and inputs, issued and waited in one statement (separate statements let the
+            // compiler copy the in-flight destinations before the wait)
+            static_assert(X_COS_LEAD + 2 <= 6, "the first-tile load names six cos blocks");
+            const char* cb = (const char*)(abuf + x_cos_off((int64_t)blockIdx.x * NW + cx.wave, LH));
+            next_inputs(blockIdx.x);
+            asm volatile(
+                "global_load_dwordx4 %0, %10, %11\n\tglobal_load_dwordx4 %1, %10, %12\n\t"
+                "global_load_dwordx4 %2, %10, %13\n\tglobal_load_dwordx4 %3, %10, %14\n\t"
+                "global_load_dwordx4 %4, %10, %15\n\tglobal_load_dwordx4 %5, %10, %16\n\t"
+                "global_load_dword %6, %17, off\n\tglobal_load_dword %7, %17, off offset:4\n\t"
+                "global_load_dword %8, %17, off offset:%c19\n\tglobal_load_dword %9, %18, off\n\t"
+                "s_waitcnt vmcnt(0)"
+                : "=&a"(st.cq[0]), "=&a"(st.cq[1]), "=&a"(st.cq[2]), "=&a"(st.cq[3]), "=&a"(st.cq[4]), "=&a"(st.cq[5]),
+                  "=&a"(st.xn[0]), "=&a"(st.xn[1]), "=&a"(st.xn[2]), "=&a"(st.gn)
+                : "v"(cx.vl), "s"(w3_at(cb, (LH * NB + 0) * 1024)), "s"(w3_at(cb, (LH * NB + 1) * 1024)),
+                  "s"(w3_at(cb, (LH * NB + 2) * 1024)), "s"(w3_at(cb, (LH * NB + 3) * 1024)),
+                  "s"(w3_at(cb, (LH * NB + 4) * 1024)), "s"(w3_at(cb, (LH * NB + 5) * 1024)), "v"(cx.xq), "v"(cx.gq),
+                  "i"(D == 3 ? 8 : 4)  // D = 2: the third load re-reads the row's second entry (xv zeroes k >= D)
+                : "memory");
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
 
 #pragma unroll 1
     for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
         cx.more = tile + gridDim.x < tiles;
         const int64_t coord = tile * TILEX + cx.wave * 16 + c;
         const bool valid = coord < n;
+        if constexpr (!RV) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) st.xv[k] = xn[k];
+            for (int k = 0; k < 4; ++k) st.xv[k] = xn[k];
+            st.gyv = gn;
+        }
         st.yp = 0.f;
-        st.gyv = gn;
         {
             const int64_t wt = tile * NW + cx.wave;  // the 16-coordinate wave tile (wave-uniform)
             const int64_t tbase = wt * (H * 16);
@@ -552,15 +646,23 @@ __global__ __launch_bounds__(64 * x_waves<x_fwd_like(XM)>(), 1) void w1x_kernel(
             if constexpr (RV) {
                 cx.td = (const char*)(dbuf + tbase);
                 cx.cs = (const char*)(abuf + x_cos_off(wt, LH));
-                // the seed's blocks 0 .. X_COS_LEAD + 1 (pre-GEMM 0, 1 and the first X_COS_LEAD slices' in-slice blocks);
-                // later ones are reloaded by the mids
-                xstatic_for<0, X_COS_LEAD + 2>([&](auto U) { x_cos_issue<LH, decltype(U)::value>(st.cq[decltype(U)::value], cx); });
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                cx.cs_next = (const char*)(abuf + x_cos_off(wt + (int64_t)gridDim.x * NW, LH));
+                // landed: this tile's first cos blocks (x_next_cos at the previous tile's mid NS - 2, or the prologue)
+                // and inputs (x_next_issue, older); after them only ring slices 1, 2 (2 CPW) and the 64 delta_0 stores
+                // were issued (capped at the counter's 63: also waits for those ring slices, which mids 0, 1 need)
+                static_assert(X_COS_LEAD + 2 <= 6, "the tile start's wait names six cos blocks");
+                asm volatile("s_waitcnt vmcnt(%10)"
+                             : "+a"(st.cq[0]), "+a"(st.cq[1]), "+a"(st.cq[2]), "+a"(st.cq[3]), "+a"(st.cq[4]),
+                               "+a"(st.cq[5]), "+a"(st.xn[0]), "+a"(st.xn[1]), "+a"(st.xn[2]), "+a"(st.gn)
+                             : "n"(2 * CPW + 64 < 63 ? 2 * CPW + 64 : 63)
+                             : "memory");
 #pragma unroll
-                for (int u = 0; u < X_COS_LEAD + 2; ++u) asm volatile("" : "+v"(st.cq[u]));
+                for (int k = 0; k < 4; ++k) st.xv[k] = (valid && k < D) ? st.xn[k] : 0.f;
+                st.gyv = valid ? st.gn : 0.f;
+                next_inputs(tile + gridDim.x);
             }
         }
-        load_inputs(tile + gridDim.x);
+        if constexpr (!RV) load_inputs(tile + gridDim.x);
         x_run<x_g0<XM, LH>(), LH, D, XM>(st, cx);
         if constexpr (FWD) {
             // last hidden layer: a_L = sin(w z_L) and y = a_L Wout^T + bout (serial over the 16 blocks)
@@ -622,6 +724,7 @@ __global__ __launch_bounds__(64 * x_waves<x_fwd_like(XM)>(), 1) void w1x_kernel(
             if (valid && cx.g == 0 && (!(ST || RV) || gx != nullptr)) gx[coord * D + k] = qk;
         }
     }
+    if constexpr (RV) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last x_next_issue (clamped, unused)
 }
 
 // The split image's bf16 stream from the flat parameters (state-dict order): slice (G, s, half), output block
