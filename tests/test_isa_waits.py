@@ -133,3 +133,41 @@ def test_checker_correlates_flag_branches():
     .LBB0_4:
         v_add_f32 v4, v0, v1
         s_endpgm""")
+
+
+@pytest.mark.skipif(shutil.which('hipcc') is None and not os.path.exists('/opt/rocm/bin/hipcc'),
+                    reason='hipcc not available')
+def test_split_reverse_tile_loop_has_no_compiler_vmcnt():
+    """The split-bf16 reverse (X_REV) counts every vector-memory operation of its tile loop itself: the next tile's
+    cos blocks and inputs are inline-asm loads waited by the tile start's counted wait (w1x_kernel.hpp x_next_cos /
+    x_next_issue). A compiler load in the loop brings back a compiler s_waitcnt vmcnt, which does not know the asm
+    operations and drains the weight ring (the round-5 tile-start drain). Only asm waits may appear after the tile
+    loop's header."""
+    import re
+    hipcc = shutil.which('hipcc') or '/opt/rocm/bin/hipcc'
+    tmp = tempfile.mkdtemp(prefix='siren_isa_')
+    try:
+        out = os.path.join(tmp, 'tu_w1x.s')
+        subprocess.check_call([hipcc, '--offload-arch=gfx950', '-O3', '-std=c++17', '-mllvm',
+                               '-pragma-unroll-threshold=1000000', '--cuda-device-only', '-S', '-I',
+                               os.path.join(ROOT, 'include'), '-o', out, os.path.join(CSRC, 'tu_w1x.hip')],
+                              stderr=subprocess.DEVNULL)
+        s = open(out).read()
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    names = re.findall(r'\n(_ZN5siren10w1x_kernelILi3ELi[23]ELi4E\w+):', s)
+    assert len(names) == 2, names
+    for nm in names:
+        i = s.find('\n' + nm + ':')
+        body = [ln.strip() for ln in s[i:s.find('.Lfunc_end', i)].split('\n')]
+        headers = [k for k, ln in enumerate(body) if 'Loop Header' in ln]
+        assert headers, nm
+        in_asm, waits = False, []
+        for k, ln in enumerate(body):
+            if ln.startswith(';;#ASMSTART'):
+                in_asm = True
+            elif ln.startswith(';;#ASMEND'):
+                in_asm = False
+            elif not in_asm and ln.startswith('s_waitcnt') and 'vmcnt' in ln and k > headers[-1]:
+                waits.append(ln)
+        assert not waits, '%s: compiler vmcnt waits in the tile loop: %s' % (nm, waits)
