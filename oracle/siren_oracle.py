@@ -205,7 +205,7 @@ def torch_param_grads(name, x, layers, gt, dtype='float64', **kw):
     total = sum(v.mean() for v in terms.values())
     grads = torch.autograd.grad(total, params, allow_unused=True)
     grads = [torch.zeros_like(p) if g is None else g for g, p in zip(grads, params)]
-    return np.concatenate([g.detach().numpy().reshape(-1) for g in grads]), float(total)
+    return np.concatenate([g.detach().numpy().reshape(-1) for g in grads]), float(total.detach())
 
 
 # ----------------------------------------------------------------------------------------------------------

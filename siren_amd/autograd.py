@@ -59,7 +59,12 @@ class JetState:
     # is requested of one call only keeps speculating for that call and not for the other (one shared cell made the
     # unconsumed call switch the mode off and the consuming call's request switch it on again every step, so each
     # step paid one wasted sweep). Calls of the SAME shape share a key (the cell then tracks the most recent one).
-    MAX_KEYS = 16  # distinct call shapes tracked per module (the oldest is dropped beyond that)
+    # A module called once per step on batches whose size changes every step (ragged point counts) never meets its
+    # recorded key again, so it does not speculate: it runs the plain forward plus the Hessian / Laplacian sweep (the
+    # same results, one more launch per step). Telling that call apart from a second call site of another shape needs
+    # a step boundary the module does not see (a shape-agnostic fallback made two call sites of different shapes
+    # take the record from each other every step).
+    MAX_KEYS = 16  # distinct call shapes tracked per module (the oldest is dropped beyond that, with its cell)
 
     def __init__(self, mode='auto'):
         self.mode = mode
@@ -95,7 +100,10 @@ class JetState:
     def _remember(self, table, key):
         table[key] = True
         while len(table) > self.MAX_KEYS:
-            table.pop(next(iter(table)))
+            old = next(iter(table))
+            table.pop(old)
+            if old not in self._hessian and old not in self._laplace:
+                self._unused.pop(old, None)
 
     def observe_x_gradient_request(self):
         if self.mode == 'auto':
@@ -179,16 +187,17 @@ class SirenSplitFunction(torch.autograd.Function):
         wsx = engine.pack_split(flat)
         # the stored split: the forward keeps a_l / cos(w z_l), the parameter backward is reverse-only
         y, ctx.tws = engine.forward_store_split(wsx, x)
-        # the fp32 image too: a derivative of y (diff_operators.gradient / laplace through siren_node_of) runs on the
-        # fp32 kernels
-        ctx.engine, ctx.jet, ctx.wsx, ctx.ws = engine, jet, wsx, engine.pack(flat)
+        # the fp32 image is packed only when a derivative of y needs it (diff_operators.gradient / laplace through
+        # siren_node_of, an x-only or create_graph backward: the fp32 kernels, _node_ws); the parameter backward of the
+        # image-fit step never does
+        ctx.engine, ctx.jet, ctx.wsx, ctx.ws = engine, jet, wsx, None
         ctx.save_for_backward(x, flat)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, flat = ctx.saved_tensors
-        engine, ws = ctx.engine, ctx.ws
+        engine = ctx.engine
         need_x = ctx.needs_input_grad[2] and _will_execute(ctx, 0)
         need_p = ctx.needs_input_grad[3] and _will_execute(ctx, 1)
         gx = gp = None
@@ -197,8 +206,9 @@ class SirenSplitFunction(torch.autograd.Function):
             if need_p:
                 gx, gp = engine.backward_stored_split(ctx.wsx, x, gy, ctx.tws, want_gx=need_x)
             elif need_x:
-                _, gx = engine.forward_grad(ws, x, gy, want_y=False)
+                _, gx = engine.forward_grad(_node_ws(ctx), x, gy, want_y=False)
             return None, None, gx, gp
+        ws = _node_ws(ctx)
         if need_x:
             if ctx.jet is not None and not need_p:
                 ctx.jet.observe_x_gradient_request()
@@ -617,6 +627,14 @@ class SirenLaplace(torch.autograd.Function):
 _VIEW_NODES = ('ViewBackward0', 'ReshapeAliasBackward0', 'UnsafeViewBackward0')
 
 
+def _node_ws(node):
+    """The packed fp32 workspace of a SirenFunction / SirenJetFunction / SirenSplitFunction node (the split node packs
+    it on first use and keeps it)."""
+    if node.ws is None:
+        node.ws = node.engine.pack(node.saved_tensors[1])
+    return node.ws
+
+
 def siren_node_of(y, x):
     """The SirenFunction / SirenJetFunction node that produced y (its value output, through views only) from a view
     of x, else None."""
@@ -655,7 +673,7 @@ def fused_laplace(y, x):
     pre = getattr(node, 'pre_laplace', None)
     if pre is not None and store and pre[1] is None:
         pre = None  # computed without the jet stores (no parameter graph then); this call wants them
-    lap = SirenLaplace.apply(node.engine, node.ws, xs, flat, store, pre)
+    lap = SirenLaplace.apply(node.engine, _node_ws(node), xs, flat, store, pre)
     if hasattr(node, 'pre_laplace'):
         node.pre_laplace = None
     if getattr(node, 'spec', None) is not None:

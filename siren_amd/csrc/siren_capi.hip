@@ -146,6 +146,21 @@ int64_t wgrad_splits(const siren_cfg* cfg, int64_t target = 256) {
     return s > 0 ? s : 1;
 }
 
+// Grouped launches (grid (S, L, batch)): about two rounds of workgroups, rounded up to whole rounds of the 256 CUs where
+// a split count within 2x of that gives one (32 elements x 3 layers: 5 splits = 480 workgroups ran 1.9 rounds, the
+// last one 88 % idle; 8 splits = 768 = 3 full rounds). SIREN_WGRAD_GROUPED_SPLITS overrides (A/B).
+int64_t grouped_wgrad_splits(const siren_cfg* cfg, int64_t batch) {
+    const int64_t want = std::max<int64_t>(1, wgrad_splits(cfg, 512) / batch);
+    if (const char* e = getenv("SIREN_WGRAD_GROUPED_SPLITS")) {
+        const long v = atol(e);
+        if (v > 0) return v;
+    }
+    const int64_t per = (int64_t)cfg->n_hidden * (cfg->hidden / 256) * (cfg->hidden / 256) * batch;
+    for (int64_t s = want; s <= 2 * want; ++s)
+        if ((s * per) % 256 == 0) return s;
+    return want;
+}
+
 // Edge-layer split (edge_kernel): the first / output layers' gradients reduce the coordinate tiles over their own,
 // finer split into compact slabs [W0 | b0 | Wout | bout] (E floats each), about two CU rounds of workgroups over
 // (split, 256-neuron block, element); edge_reduce_kernel sums them into the parameter order. (Tied to the wgrad
@@ -180,7 +195,7 @@ struct TrainPlan {
         : es(cfg, (n + siren::TILE - 1) / siren::TILE * siren::TILE / 16, batch) {
         n_pad = (n + siren::TILE - 1) / siren::TILE * siren::TILE;
         tiles = n_pad / 16;
-        const int64_t want = batch > 1 ? std::max<int64_t>(1, wgrad_splits(cfg, 512) / batch) : wgrad_splits(cfg);
+        const int64_t want = batch > 1 ? grouped_wgrad_splits(cfg, batch) : wgrad_splits(cfg);
         splits = tiles < want ? tiles : want;
         if (splits < 1) splits = 1;
         tps = std::max<int64_t>(1, (tiles + splits - 1) / splits);  // n == 0: no tiles, one empty split

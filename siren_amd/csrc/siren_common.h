@@ -145,7 +145,14 @@ __device__ __forceinline__ void sincos_fast(float t, float& sn, float& cs) {
 // 2 VALU instead of sincos_fast's 5; the argument's own rounding is one fp32 rounding of w z, like the reference's
 // fl(30 z) (modules.py:34).
 __device__ __forceinline__ void sincos_rev(float u, float& sn, float& cs) {
+#ifndef SIREN_FRACT
+#define SIREN_FRACT 0
+#endif
+#if SIREN_FRACT
+    const float r = __builtin_amdgcn_fractf(u);  // one VALU; [0, 1) instead of [-1/2, 1/2]
+#else
     const float r = u - __builtin_rintf(u);
+#endif
     sn = __builtin_amdgcn_sinf(r);
     cs = __builtin_amdgcn_cosf(r);
 }

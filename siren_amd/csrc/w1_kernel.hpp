@@ -155,6 +155,26 @@ template <int MODE>
 constexpr bool w1_staged() { return W1_STAGE != 0 && w1_mem<MODE>() && !w1_fwd_half(MODE); }
 template <int MODE>
 constexpr bool w1_tiles() { return w1_mem<MODE>() && (MODE & MODE_NOTILE) == 0; }
+// cos(w0 z_0) of the W1 mode is parked in LDS (16 KiB per wave, 16 ds_write_b128 + 16 ds_read_b128 per tile) instead of
+// 64 VGPRs held from the FIRST epilogue to the delta_0 tail: the specialised headline body otherwise needs 517 of the
+// 512 registers and its scratch reloads put compiler vmcnt(0) waits (ring drains) into every tile
+#ifndef W1_C0LDS
+#define W1_C0LDS 1
+#endif
+template <int MODE>
+constexpr bool w1_c0lds() { return W1_C0LDS != 0 && (MODE & MODE_BASE) == MODE_W1; }
+#ifndef W1_ASM_INPUTS
+#define W1_ASM_INPUTS 1
+#endif
+// the next tile's inputs as inline-asm loads retired by the tile's counted waits: the one-wave-per-SIMD modes (W1,
+// STORE, REV). The forward-only modes run two workgroups per CU (the other one covers a drain) in 256 registers, where
+// hipcc reallocated an in-flight asm destination (tools/check_asm_waits.py), so they keep compiler loads, as does the
+// phase-stamp build (MODE_PROF: hipcc copied one before its wait)
+template <int MODE>
+constexpr bool w1_asm_inputs() {
+    return W1_ASM_INPUTS != 0 && !forward_only(MODE & MODE_BASE) && (MODE & MODE_PROF) == 0;
+}
+constexpr int W1_C0FLOATS = WAVES * NB * 256;  // [wave][block][lane] f32x4
 constexpr bool w1_mem_rt(int mode) {
     return (mode & MODE_BASE) == MODE_STORE || (mode & MODE_BASE) == MODE_FWDS || (mode & MODE_BASE) == MODE_REV ||
            (mode & MODE_BASE) == MODE_JETS;
@@ -221,6 +241,8 @@ struct W1State {
     float gyv[MAXO];   // this lane's output cotangent
     float yp[MAXO];    // partial y over this lane's neurons
     f32x4 cq[W1_COS_SLOTS];  // MODE_REV: cos blocks of the next epilogues (slot e % W1_COS_SLOTS, W1_COS_LEAD)
+    f32x4 c0q[(MODE & MODE_BASE) == MODE_REV ? NB : 1];  // MODE_REV: cos(w0 z_0) of the delta_0 tail (loaded at mid NS - 3)
+    f32x4 c0r[w1_c0lds<MODE>() ? NB : 1];  // W1: the parked cos(w0 z_0), read back from LDS during the last slice
     f32x4 tq[2];       // W1_STAGE: the last epilogue's tile blocks, transposed (stored at the start of the next slice)
 };
 
@@ -240,6 +262,7 @@ struct W1Ctx {
     const char* td;     // STORE / REV: the same for the delta tiles
     const char* cs;     // FWDS: wave-uniform lane-major cos base of (tile, wave) (cos_off(tile, wave, LH, 0, 0, 0))
     const char* cbase;  // REV: wave-uniform cos base of (tile, wave) (SGPRs), + 16 * lane per lane
+    const char* cnext;  // REV: the same for the next tile of this workgroup (its first cos blocks load at mid NS - 1)
     unsigned vl, vt;    // this lane's byte offset: 16 lane (coalesced blocks), 4 (4 g 16 + c) (the 64 B pieces)
     unsigned tw, tr;    // W1_STAGE: LDS transpose scratch of the wave, this lane's write / read address
     int64_t lbytes;
@@ -248,6 +271,7 @@ struct W1Ctx {
     int64_t lstride;
     unsigned ring_vaddr;  // LDS byte address of this lane's 16 B in slot 0 of the ring
     unsigned sm_vaddr;    // LDS byte address of the small-parameter block + this lane's 4*g neuron offset
+    unsigned c0_vaddr;    // w1_c0lds: LDS byte address of this lane's 16 B in block 0 of its wave's cos(w0 z_0) park
     unsigned long long* prof;  // MODE_PROF: this wave's stamp row of the current tile (nullptr: not recorded)
     unsigned long long stamp[PROF_EVENTS];  // MODE_PROF: stamps of the current tile (uniform: SGPRs), stored at its end
     // JET: per-lane stream coefficients (stream s = lane & 3)
@@ -275,11 +299,34 @@ __device__ __forceinline__ void ring_issue4(const float* __restrict__ stream, fl
 // cq[E % W1_COS_SLOTS].
 // Issued before a ring issue, so the ring's counted s_waitcnt vmcnt(4) one slice later also covers it.
 template <int E, int LH, int MODE>
-__device__ __forceinline__ void cos_issue(W1State<LH, MODE>& st, const W1Ctx& cx) {
+__device__ __forceinline__ void cos_issue(W1State<LH, MODE>& st, const W1Ctx& cx, const char* base) {
     constexpr int GE = LH + E / NB, BE = E % NB;
     constexpr int LC = GE == LH ? LH : 2 * LH - GE;
     asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(st.cq[E % W1_COS_SLOTS]) : "v"(16u * cx.lane),
-                 "s"(cx.cbase + (LC * NB + BE) * 1024));
+                 "s"(base + (LC * NB + BE) * 1024));
+}
+template <int E, int LH, int MODE>
+__device__ __forceinline__ void cos_issue(W1State<LH, MODE>& st, const W1Ctx& cx) {
+    cos_issue<E, LH, MODE>(st, cx, cx.cbase);
+}
+// MODE_REV: the delta_0 tail's 16 cos(w0 z_0) blocks (layer 0 of this tile's cos buffer), issued at the mid of slice
+// NS - 3 behind its wait and ahead of its ring issue; the mid of slice NS - 2 waits vmcnt(0) anyway (its epilogue's cos
+// block), and that one wait statement names them (one shape on every path: no copies of in-flight registers)
+template <int LH, int MODE>
+__device__ __forceinline__ void c0_issue(W1State<LH, MODE>& st, const W1Ctx& cx) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+        asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(st.c0q[b]) : "v"(16u * cx.lane), "s"(cx.cbase + b * 1024));
+}
+// the wait that retires them, naming every destination (hipcc must not copy one before it)
+template <int N, int LH, int MODE>
+__device__ __forceinline__ void c0_wait(W1State<LH, MODE>& st) {
+    asm volatile("s_waitcnt vmcnt(%16)"
+                 : "+v"(st.c0q[0]), "+v"(st.c0q[1]), "+v"(st.c0q[2]), "+v"(st.c0q[3]), "+v"(st.c0q[4]), "+v"(st.c0q[5]),
+                   "+v"(st.c0q[6]), "+v"(st.c0q[7]), "+v"(st.c0q[8]), "+v"(st.c0q[9]), "+v"(st.c0q[10]), "+v"(st.c0q[11]),
+                   "+v"(st.c0q[12]), "+v"(st.c0q[13]), "+v"(st.c0q[14]), "+v"(st.c0q[15])
+                 : "n"(N)
+                 : "memory");
 }
 
 // ---- epilogue parameters (LDS) -------------------------------------------------------------------------
@@ -396,7 +443,10 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
             st.act[b][r] = sn;
             cs4[r] = cs;
         }
-        if constexpr (!FWD) st.C[0][b] = pin(cs4);
+        if constexpr (w1_c0lds<MODE>())
+            asm volatile("ds_write_b128 %0, %1" ::"v"(cx.c0_vaddr + 1024u * b), "v"(cs4));
+        else if constexpr (!FWD)
+            st.C[0][b] = pin(cs4);
         if constexpr (w1_tiles<MODE>()) w1_tile_put<MODE, 0>(st, cx, cx.ta, 0, b, st.act[b]);
         if constexpr (FWDS) w3_store16(w3_at(cx.cs, b * 1024), cx.vl, cs4);
     } else if constexpr (KIND == EPI_SINCOS) {
@@ -483,8 +533,10 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
                 } else if constexpr (is_rev<MODE>() && S + 2 == NS) {
                     // the last epilogue's cos block (issued W1_COS_LEAD slices earlier) is retired whether or not the next
                     // tile's ring slices were issued behind it: one wait shape on every path (a `more`-dependent
-                    // vmcnt(4) / vmcnt(0) pair compiles into branches the static ISA check cannot correlate)
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    // vmcnt(4) / vmcnt(0) pair compiles into branches the static ISA check cannot correlate); then the
+                    // delta_0 tail's cos blocks
+                    static_assert(NB == 16, "c0_wait names 16 blocks");
+                    c0_wait<0>(st);  // ... and the delta_0 tail's cos blocks (issued at the previous mid)
                 } else if (cx.more) {
                     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
                 } else {
@@ -495,6 +547,15 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
                     constexpr int NEED = S + 1 + (W1_EPI_MEM < 4 ? 1 : 0);
                     if constexpr (NEED < NS) asm volatile("" : "+v"(st.cq[NEED % W1_COS_SLOTS]));
                     if constexpr (S + W1_COS_LEAD < NS) cos_issue<S + W1_COS_LEAD, LH, MODE>(st, cx);
+                    if constexpr (S + 3 == NS) c0_issue<LH, MODE>(st, cx);  // retired by the next mid's vmcnt(0)
+                    // the next tile's first W1_COS_LEAD cos blocks (every epilogue of this tile has run: the last one ran
+                    // in slice NS - 2), behind this mid's wait and ahead of its ring issue: the tile start waits for the
+                    // first of them with a counted vmcnt (no drain of the ring slices in flight)
+                    if constexpr (S + 1 == NS) {
+                        if (cx.more)
+                            static_for<0, W1_COS_LEAD>(
+                                [&](auto E) { cos_issue<decltype(E)::value, LH, MODE>(st, cx, cx.cnext); });
+                    }
                 }
                 __builtin_amdgcn_s_barrier();
                 if (S + 3 < NS || cx.more) {
@@ -531,6 +592,12 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
             for (int i = 0; i < epi_nparams<KIND>(); ++i) asm volatile("" : "+v"(ep.v[i]));
         }
         if constexpr (p == 0) w1_flush<S, LH, MODE>(st, cx);  // the wait above retired the transpose
+        if constexpr (w1_c0lds<MODE>() && S + 1 == NS) {
+            // the last slice reads the parked cos(w0 z_0) back two blocks per pair, behind this pair's wait (the next
+            // pair's counted wait, or the tail's, retires them: 8 MFMAs of latency cover each pair)
+            st.c0r[2 * p] = lds_read4<2 * p * 1024>(cx.c0_vaddr);
+            st.c0r[2 * p + 1] = lds_read4<(2 * p + 1) * 1024>(cx.c0_vaddr);
+        }
         if constexpr (p == EPI_AT && EPI) {
             __builtin_amdgcn_sched_barrier(0);
             w1_epilogue<G, LH, MODE>(st, cx, KB + 1, ep);
@@ -600,7 +667,8 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
     constexpr bool REV = is_rev<MODE>();                     // abuf = lane-major cos buffer, dbuf = delta tiles
     constexpr int NS = npasses<MODE>() * LH * NB;
     constexpr int SMALL4 = (small_floats_ct(LH) + 3) / 4 * 4;
-    __shared__ __attribute__((aligned(16))) float lds[W1_NBUF * SLICE + SMALL4 + (w1_staged<MODE>() ? WAVES * STB_SCRATCH : 0)];
+    __shared__ __attribute__((aligned(16))) float lds[W1_NBUF * SLICE + SMALL4 + (w1_staged<MODE>() ? WAVES * STB_SCRATCH : 0) +
+                                                      (w1_c0lds<MODE>() ? W1_C0FLOATS : 0)];
     W1Ctx cx;
     W1State<LH, MODE> st;
     cx.ring = lds;
@@ -653,6 +721,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
     const unsigned lds_base = (unsigned)(uintptr_t)((__attribute__((address_space(3))) float*)lds);
     cx.ring_vaddr = lds_base + cx.lane * 16;
     cx.sm_vaddr = lds_base + W1_NBUF * SLICE * 4 + 16 * cx.g;
+    cx.c0_vaddr = lds_base + 4u * (W1_NBUF * SLICE + SMALL4 + cx.wave * NB * 256) + 16u * cx.lane;
     cx.lbytes = cx.lstride * 4;
     cx.vl = 16u * cx.lane;
     cx.vt = 4u * (4 * cx.g * 16 + c);
@@ -677,12 +746,43 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
     auto load_inputs = [&](int64_t tile) {
         const int64_t cd = coord_of(tile);
         const bool ok = tile < tiles && cd < n;
+        if constexpr (w1_asm_inputs<MODE>()) {
+            // the next tile's inputs as asm loads into AGPRs ("+a": the zero of an idle lane and the loaded value
+            // share one register, and hipcc has no reason to move an AGPR while it flies; into VGPRs it parked them in
+            // AGPRs right after the issue, tools/check_asm_waits.py). A compiler load would be consumed at the next tile
+            // start behind a compiler vmcnt(0) that drains the ring slices 0..2 already in flight; these are retired by
+            // the tile's counted mid-slice waits long before (any vmcnt(4) two ring issues later)
+#pragma unroll
+            for (int k = 0; k < MAXD; ++k) xn[k] = 0.f;
+#pragma unroll
+            for (int j = 0; j < MAXO; ++j) gn[j] = 0.f;
+            if (ok) {
+                const float* xp = x + cd * d;
+#pragma unroll
+                for (int k = 0; k < MAXD; ++k)
+                    if (k < d && !REV) asm volatile("global_load_dword %0, %1, off offset:%2" : "+a"(xn[k]) : "v"(xp), "i"(4 * k));
+                if (gy != nullptr) {
+                    const float* gp = gy + cd * o;
+#pragma unroll
+                    for (int j = 0; j < MAXO; ++j)
+                        if (j < o) asm volatile("global_load_dword %0, %1, off offset:%2" : "+a"(gn[j]) : "v"(gp), "i"(4 * j));
+                }
+            }
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < MAXD; ++k) xn[k] = (ok && k < d) ? x[cd * d + k] : 0.f;
 #pragma unroll
         for (int j = 0; j < MAXO; ++j) gn[j] = (gy != nullptr && ok && j < o) ? gy[cd * o + j] : 0.f;
     };
     load_inputs(bx);
+    if constexpr (w1_asm_inputs<MODE>()) {
+        static_assert(MAXD == 4 && MAXO == 4, "one wait statement names every input register");
+        asm volatile("s_waitcnt vmcnt(0)"
+                     : "+a"(xn[0]), "+a"(xn[1]), "+a"(xn[2]), "+a"(xn[3]), "+a"(gn[0]), "+a"(gn[1]), "+a"(gn[2]), "+a"(gn[3])
+                     :
+                     : "memory");
+    }
     if constexpr (JET) {
         // jet coefficients on phase-scaled jets: w / s = 2 pi for every layer (jet_sin_rev)
         const float val = js == 0 ? 1.f : 0.f;
@@ -705,8 +805,17 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
     static_assert(NS >= 3, "ring prologue issues three slices");
     ring_issue4(cx.stream, cx.ring, 0, cx.wave, 16u * cx.lane);
     ring_issue4(cx.stream, cx.ring, 1, cx.wave, 16u * cx.lane);
+    if constexpr (REV) {
+        // the first tile's first cos blocks, in the position the next tiles' take (between ring slices 1 and 2): the
+        // tile start then waits for them with one counted shape on every tile
+        cx.cnext = (const char*)(abuf + cos_off(bx, cx.wave, LH, 0, 0, 0));
+        if (bx < tiles) static_for<0, W1_COS_LEAD>([&](auto E) { cos_issue<decltype(E)::value, LH, MODE>(st, cx, cx.cnext); });
+    }
     ring_issue4(cx.stream, cx.ring, 2, cx.wave, 16u * cx.lane);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    if constexpr (REV)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + W1_COS_LEAD) : "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     st.pa0 = lds_read4<0>(cx.ring_vaddr);
     st.pa1 = lds_read4<1024>(cx.ring_vaddr);
@@ -715,6 +824,15 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
     // workgroup grid runs the loop once); the weight ring streams on across tile boundaries ----------------------
 #pragma unroll 1
     for (int64_t tile = bx; tile < tiles; tile += gridDim.x) {
+        if constexpr (REV) {
+            // cos blocks of the first epilogues (SEED blocks 0 .. W1_COS_LEAD - 1), issued at the previous tile's last
+            // mid-slice (the prologue for the first tile) ahead of ring slice 2: block 0 is needed now, blocks 1, 2 at
+            // the next two mid-slice waits
+            static_assert(W1_COS_LEAD == 3, "the tile-start count");
+            asm volatile("s_waitcnt vmcnt(6)" : "+v"(st.cq[0]) : : "memory");
+            cx.cbase = cx.cnext;
+            cx.cnext = (const char*)(abuf + cos_off(tile + gridDim.x, cx.wave, LH, 0, 0, 0));
+        }
         cx.more = tile + gridDim.x < tiles;
         const int64_t coord = coord_of(tile);
         const bool valid = coord < n;
@@ -744,14 +862,6 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
             if constexpr (JETS) cx.cs = (const char*)(dbuf + tbase);  // lane-major, + 16 lane
         }
         if constexpr (FWDS) cx.cs = (const char*)(dbuf + cos_off(tile, cx.wave, LH, 0, 0, 0));
-        if constexpr (REV) {
-            // cos blocks of the first two epilogues (SEED blocks 0, 1); later ones are prefetched by the slices
-            cx.cbase = (const char*)(abuf + cos_off(tile, cx.wave, LH, 0, 0, 0));
-            static_for<0, W1_COS_LEAD>([&](auto E) { cos_issue<decltype(E)::value, LH, MODE>(st, cx); });
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int e = 0; e < W1_COS_LEAD; ++e) asm volatile("" : "+v"(st.cq[e]));
-        }
 
         if constexpr ((MODE & MODE_PROF) != 0) {
             const int64_t it = (tile - bx) / gridDim.x;
@@ -848,9 +958,18 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
             // gx = delta_0 W0 (the LDS W0^T carries s0: cx.inv_s0)
             constexpr int GL = (2 * LH - 1) & 1;
             if constexpr (REV) {
-                const f32x4* c0 = (const f32x4*)(cx.cbase + 16 * cx.lane);
 #pragma unroll
-                for (int rb = 0; rb < NB; ++rb) st.act[rb] = (st.acc[GL][rb] * c0[rb * 64]) * cx.w0;
+                for (int rb = 0; rb < NB; ++rb) st.act[rb] = (st.acc[GL][rb] * st.c0q[rb]) * cx.w0;
+            } else if constexpr (w1_c0lds<MODE>()) {
+                // the parked cos(w0 z_0), read during the last slice; one wait statement names every destination
+                static_assert(NB == 16, "the wait names 16 blocks");
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(st.c0r[0]), "+v"(st.c0r[1]), "+v"(st.c0r[2]), "+v"(st.c0r[3]), "+v"(st.c0r[4]),
+                               "+v"(st.c0r[5]), "+v"(st.c0r[6]), "+v"(st.c0r[7]), "+v"(st.c0r[8]), "+v"(st.c0r[9]),
+                               "+v"(st.c0r[10]), "+v"(st.c0r[11]), "+v"(st.c0r[12]), "+v"(st.c0r[13]), "+v"(st.c0r[14]),
+                               "+v"(st.c0r[15]));
+#pragma unroll
+                for (int rb = 0; rb < NB; ++rb) st.act[rb] = (st.acc[GL][rb] * st.c0r[rb]) * cx.w0;
             } else {
 #pragma unroll
                 for (int rb = 0; rb < NB; ++rb) st.act[rb] = (st.acc[GL][rb] * st.C[0][rb]) * cx.w0;

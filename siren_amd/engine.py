@@ -246,11 +246,24 @@ class SirenEngine:
     def backward_stored_split(self, wsx, x, gy, tws, want_gx=False):
         """Reverse-only backward of the bf16x6 leg from forward_store_split's tws: (gx or None, gparams)."""
         self._require()
+        if not self.split_supported:
+            raise _lib.SirenUnsupported('the split-bf16 kernels cover hidden 256, 3 hidden layers, in_features 2 / 3, '
+                                        'out_features 1, linear output')
         x = self._check_x(x)
         n = x.shape[0]
         gy = gy.contiguous()
         if gy.shape != (n, 1) or gy.dtype != torch.float32 or gy.device != x.device:
             raise ValueError('gy must be fp32 (%d, 1) on the coords device; got %s' % (n, tuple(gy.shape)))
+        # the C side cannot tell a workspace of another n (or forward_store's) from this one: its kernels would read
+        # cos and write deltas / partials out of bounds
+        cnt = ctypes.c_int64()
+        _lib.check(self.lib.siren_train_split_ws_floats(ctypes.byref(self.cfg), n, ctypes.byref(cnt)),
+                   'siren_train_split_ws_floats')
+        if (tws.dtype != torch.float32 or tws.device != x.device or not tws.is_contiguous()
+                or tws.numel() != cnt.value):
+            raise ValueError('tws must be the contiguous fp32 workspace forward_store_split made for these %d coords '
+                             '(%d floats on %s); got %d %s floats on %s'
+                             % (n, cnt.value, x.device, tws.numel(), tws.dtype, tws.device))
         gx = torch.empty(n, self.cfg.d_in, dtype=torch.float32, device=x.device) if want_gx else None
         gp = torch.empty(self.param_count, dtype=torch.float32, device=x.device)
         _lib.check(self.lib.siren_backward_stored_split(ctypes.byref(self.cfg), _ptr(wsx), _ptr(x), n, _ptr(gy),

@@ -201,7 +201,7 @@ def test_layered_video_width_trains(cuda):
             loss = LF.image_mse(None, m({'coords': coords}), {'img': gt})['img_loss']
             loss.backward()
             opt.step()
-            losses.append(float(loss))
+            losses.append(float(loss.detach()))
         assert losses[-1] < 0.5 * losses[0]
     finally:
         for k, v in saved.items():

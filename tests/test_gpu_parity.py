@@ -300,7 +300,7 @@ def test_sdf_losses_vs_reference(cuda, g3, manifest, jet, monkeypatch):
     terms = Lf.sdf(out, {'sdf': to_dev(g3['gt_sdf'], cuda), 'normals': to_dev(g3['gt_normals'], cuda)})
     for k, v in terms.items():
         ref = manifest['G3_sdf_%s_f64' % k]
-        assert abs(float(v) - ref) <= 1e-4 * max(1., abs(ref)), k
+        assert abs(float(v.detach()) - ref) <= 1e-4 * max(1., abs(ref)), k
     total = sum(v.mean() for v in terms.values())
     m.zero_grad()
     total.backward()
@@ -338,7 +338,7 @@ def test_g5_psnr_trajectory(cuda, manifest):
     for _ in range(300):
         out = m({'coords': grid})
         loss = ((out['model_out'] - img) ** 2).mean()
-        losses.append(float(loss))
+        losses.append(float(loss.detach()))
         opt.zero_grad()
         loss.backward()
         opt.step()

@@ -7,7 +7,7 @@ import pytest
 import torch
 
 from oracle import siren_oracle as O
-from conftest import weights_of
+from conftest import forbid_torch_path, weights_of
 
 pytestmark = pytest.mark.gpu
 
@@ -318,6 +318,50 @@ def test_module_precision_bf16x6_training_step(cuda, g1, monkeypatch):
         assert np.max(np.abs(p.grad.cpu().numpy() - ref)) <= 1e-4 * max(np.max(np.abs(ref)), 1e-30) + 1e-12, k
 
 
+@pytest.mark.parametrize('which', ['gradients_mse', 'laplace_mse'])
+def test_module_precision_bf16x6_derivative_losses(cuda, g1, monkeypatch, which):
+    """SingleBVPNet(precision='bf16x6') trained through a derivative loss: the first step reaches the
+    split node (SirenSplitFunction's x-derivative: SirenVJP, or fused_laplace on its node, which packs the fp32 image
+    on first use), later steps the jet / Laplacian modes on the fp32 kernels. Three steps, every device-torch recompute
+    forbidden: the θ-gradients match G1's fp64 golden at each step (no optimizer step in between)."""
+    from siren_amd import loss_functions as Lf, modules
+    forbid_torch_path(monkeypatch)
+    sd = {k[2:]: np.asarray(g1[k]) for k in g1.keys() if k.startswith('w_net.')}
+    m = modules.SingleBVPNet(in_features=2, verbose=False, precision='bf16x6').to(cuda)
+    m.load_state_dict({k: torch.tensor(v) for k, v in sd.items()})
+    coords = to_dev(g1['coords'], cuda)
+    for step in range(3):
+        m.zero_grad()
+        out = m({'coords': coords})
+        if which == 'gradients_mse':
+            loss = Lf.gradients_mse(out, {'gradients': to_dev(g1['gt_gradients'], cuda)})['gradients_loss']
+        else:
+            loss = Lf.laplace_mse(out, {'laplace': to_dev(g1['gt_laplace'], cuda)})['laplace_loss']
+        loss.backward()
+        for k, p in m.named_parameters():
+            ref = g1['G1_%s_grad_%s' % (which, k)]
+            err = np.max(np.abs(p.grad.cpu().numpy() - ref))
+            assert err <= 1e-4 * max(np.max(np.abs(ref)), 1e-30) + 1e-12, (step, k, err)
+
+
+def test_module_precision_bf16x6_retain_graph(cuda, g1):
+    """A second backward over the same bf16x6 training graph (retain_graph=True) reads the stored split workspace
+    again: the θ-gradients of the two passes are bitwise identical."""
+    from siren_amd import loss_functions as Lf, modules
+    sd = {k[2:]: np.asarray(g1[k]) for k in g1.keys() if k.startswith('w_net.')}
+    m = modules.SingleBVPNet(in_features=2, verbose=False, precision='bf16x6').to(cuda)
+    m.load_state_dict({k: torch.tensor(v) for k, v in sd.items()})
+    out = m({'coords': to_dev(g1['coords'], cuda)})
+    loss = Lf.image_mse(None, out, {'img': to_dev(g1['gt_img'], cuda)})['img_loss']
+    m.zero_grad()
+    loss.backward(retain_graph=True)
+    first = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+    m.zero_grad()
+    loss.backward()
+    for k, p in m.named_parameters():
+        assert torch.equal(p.grad, first[k]), k
+
+
 @pytest.mark.parametrize('n,d', [(1, 2), (100, 3), (5000, 2), (70000, 3), (1 << 18, 2)])
 def test_stored_split_matches_recompute(cuda, n, d):
     """The stored bf16x6 split (forward keeps a_l / cos, reverse-only backward) against the recompute form
@@ -380,7 +424,7 @@ def test_g5_psnr_trajectory_bf16x6(cuda, manifest, monkeypatch):
     for _ in range(300):
         out = m({'coords': grid})
         loss = ((out['model_out'] - img) ** 2).mean()
-        losses.append(float(loss))
+        losses.append(float(loss.detach()))
         opt.zero_grad()
         loss.backward()
         opt.step()

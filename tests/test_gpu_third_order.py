@@ -215,7 +215,7 @@ def test_reference_recipe_laplace_mse_hidden512_on_kernels(cuda, monkeypatch):
         out = m({'coords': coords.to(cuda)})
         loss = torch.mean((reference_laplace(out['model_out'], out['model_in']) - gt.to(cuda)) ** 2)
         loss.backward()
-        assert abs(float(loss) - float(loss64)) <= 1e-4 * max(1., float(loss64))
+        assert abs(float(loss.detach()) - float(loss64.detach())) <= 1e-4 * max(1., float(loss64.detach()))
         for (k, p), r in zip(m.named_parameters(), ref):
             r = r.numpy()
             assert np.max(np.abs(p.grad.cpu().numpy() - r)) <= 1e-4 * np.max(np.abs(r)) + 1e-12, k

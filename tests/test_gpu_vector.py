@@ -126,7 +126,7 @@ def test_pml_training_theta_grads_vs_reference(cuda, g6, manifest, monkeypatch, 
         total.backward()
     for k, v in terms.items():
         ref = manifest['G6_%s_%s_f64' % (name, k)]
-        assert abs(float(v) - ref) <= 1e-4 * max(1., abs(ref)), k
+        assert abs(float(v.detach()) - ref) <= 1e-4 * max(1., abs(ref)), k
     gp = torch.cat([p.grad.reshape(-1) for p in m.parameters()]).cpu().numpy()
     ref = pml_ref_grads(g6, tag)
     assert np.max(np.abs(gp - ref)) <= 1e-4 * np.max(np.abs(ref))

@@ -132,7 +132,7 @@ def test_module_image_fit_step_wide(cuda, g4):
     m = SingleBVPNet(out_features=3, in_features=3, hidden_features=512, num_hidden_layers=3, verbose=False).to(cuda)
     out = m({'coords': to_dev(g4['coords'], cuda)})
     loss = LF.image_mse(None, out, {'img': to_dev(g4['gt_img'], cuda)})['img_loss']
-    assert abs(float(loss) - 0.3987086920864164) <= 1e-5
+    assert abs(float(loss.detach()) - 0.3987086920864164) <= 1e-5
     loss.backward()
     for name, p in m.named_parameters():
         ref = g4['G4_image_mse_grad_' + name]

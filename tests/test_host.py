@@ -151,7 +151,7 @@ def test_notebook_siren_api():
     keys = list(s.state_dict().keys())
     assert keys[0] == 'net.0.linear.weight' and keys[-1] == 'net.3.bias'
     assert isinstance(s.net[0], SineLayer) and s.net[0].is_first
-    assert float(s.net[0].linear.weight.abs().max()) <= 0.5
+    assert float(s.net[0].linear.weight.detach().abs().max()) <= 0.5
 
 
 def test_relu_baseline_runs_on_cpu():

@@ -24,8 +24,49 @@ TUS = ['tu_w1.hip', 'tu_w1deep.hip', 'tu_w1nt.hip', 'tu_w0.hip', 'tu_w4.hip', 't
 sys.path.insert(0, os.path.join(ROOT, 'tools'))
 
 
+# kernels whose tile loop must hold no compiler s_waitcnt vmcnt (they count every vector-memory op themselves): the
+# headline W1 bodies (d_in 2 / 3), the general W1 body, the recompute W2 store, the fp32 reverse at every depth (the
+# image / hypernet W2 backward; gx-only REV of the deep and notile forms) and the split-bf16 reverse. A compiler load or scratch reload in the loop brings one back, and it drains the weight ring.
+LOOP_WAIT_FREE = {
+    'tu_w1.hip': [r'_ZN5siren9w1_kernelILi3ELi640E\w+', r'_ZN5siren9w1_kernelILi3ELi896E\w+',
+                  r'_ZN5siren9w1_kernelILi3ELi0E\w+', r'_ZN5siren9w1_kernelILi[123]ELi5E\w+',
+                  r'_ZN5siren9w1_kernelILi[123]ELi1E\w+'],
+    'tu_w1deep.hip': [r'_ZN5siren9w1_kernelILi[45]ELi5E\w+'],
+    'tu_w1nt.hip': [r'_ZN5siren9w1_kernelILi[1-5]ELi37E\w+'],
+    'tu_w1x.hip': [r'_ZN5siren10w1x_kernelILi3ELi[23]ELi4E\w+'],
+}
+
+
+def tile_loop_vmcnt_waits(body):
+    """Compiler (non-asm) s_waitcnt vmcnt in the blocks of a kernel's last depth-1 loop (the persistent tile loop):
+    its header block and every block hipcc marks `in Loop: Header=` that header, the latch included."""
+    import re
+    heads = [re.match(r'(\.LBB\w+):', ln).group(1) for ln in body
+             if 'Loop Header: Depth=1' in ln and re.match(r'\.LBB\w+:', ln)]
+    if not heads:
+        return None
+    hdr = heads[-1]
+    tag = 'Header=' + hdr[2:]  # .LBB5_24 -> 'Header=BB5_24'
+    in_loop = in_asm = False
+    waits = []
+    for ln in body:
+        m = re.match(r'(\.LBB\w+):', ln)
+        if m:
+            in_loop = m.group(1) == hdr or tag + ' ' in ln + ' '
+        elif ln.startswith('; %bb.'):
+            in_loop = tag + ' ' in ln + ' '
+        if ln.startswith(';;#ASMSTART'):
+            in_asm = True
+        elif ln.startswith(';;#ASMEND'):
+            in_asm = False
+        elif in_loop and not in_asm and ln.startswith('s_waitcnt') and 'vmcnt' in ln:
+            waits.append(ln)
+    return waits
+
+
 def _compile_and_check(tu):
-    """(tu, problems) for one translation unit: hipcc to ISA, then the three checks on every kernel in it."""
+    """(tu, problems, loop waits) for one translation unit: hipcc to ISA, then the ISA checks on every kernel in it,
+    and the tile-loop vmcnt scan of its LOOP_WAIT_FREE kernels ({name: [waits]})."""
     import re
     import check_asm_waits as C
     hipcc = shutil.which('hipcc') or '/opt/rocm/bin/hipcc'
@@ -39,7 +80,7 @@ def _compile_and_check(tu):
         s = open(out).read()
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-    bad = []
+    bad, loops = [], {}
     for nm in re.findall(r'\n(_Z\w+):', s):
         i = s.find('\n' + nm + ':')
         j = s.find('.Lfunc_end', i)
@@ -48,16 +89,46 @@ def _compile_and_check(tu):
                  C.check_private(body, nm))
         if probs:
             bad.append('%s %s: %d (first: %s)' % (tu, nm, len(probs), probs[0][1]))
-    return bad
+        if any(re.fullmatch(pat, nm) for pat in LOOP_WAIT_FREE.get(tu, [])):
+            loops[nm] = tile_loop_vmcnt_waits([ln.strip() for ln in body])
+    return bad, loops
+
+
+_RESULTS = {}
+
+
+def _isa_results():
+    """Every TU compiled and checked once per test session (the TUs compile in parallel; tu_w1 takes minutes)."""
+    if not _RESULTS:
+        from concurrent.futures import ProcessPoolExecutor
+        with ProcessPoolExecutor(max_workers=min(8, os.cpu_count() or 2)) as ex:
+            for tu, res in zip(TUS, ex.map(_compile_and_check, TUS)):
+                _RESULTS[tu] = res
+    return _RESULTS
 
 
 @pytest.mark.skipif(shutil.which('hipcc') is None and not os.path.exists('/opt/rocm/bin/hipcc'),
                     reason='hipcc not available')
 def test_no_read_of_inflight_lds_load_registers():
-    from concurrent.futures import ProcessPoolExecutor
-    with ProcessPoolExecutor(max_workers=min(8, os.cpu_count() or 2)) as ex:
-        bad = [b for res in ex.map(_compile_and_check, TUS) for b in res]
+    bad = [b for tu in TUS for b in _isa_results()[tu][0]]
     assert not bad, '\n'.join(bad)
+
+
+@pytest.mark.skipif(shutil.which('hipcc') is None and not os.path.exists('/opt/rocm/bin/hipcc'),
+                    reason='hipcc not available')
+def test_counted_tile_loops_have_no_compiler_vmcnt():
+    """The headline W1 (its cos(w0 z_0) parked in LDS: no spills; the next tile's inputs as asm loads), the general
+    W1, the fp32 reverse (the delta_0 tail's cos blocks prefetched at mid NS - 3, the next tile's first cos blocks at
+    the last mid, a counted tile-start wait) and the split-bf16 reverse count every vector-memory operation of their
+    tile loop themselves. A compiler s_waitcnt vmcnt there does not know the asm operations and drains the weight ring
+    (a scratch reload, or a compiler load consumed at the next tile start)."""
+    res = _isa_results()
+    for tu, pats in LOOP_WAIT_FREE.items():
+        loops = res[tu][1]
+        assert len(loops) >= len(pats), (tu, sorted(loops))
+        for nm, waits in loops.items():
+            assert waits is not None, '%s: no tile loop found' % nm
+            assert not waits, '%s: compiler vmcnt waits in the tile loop: %s' % (nm, waits)
 
 
 def _walk_isa(text):
@@ -133,41 +204,3 @@ def test_checker_correlates_flag_branches():
     .LBB0_4:
         v_add_f32 v4, v0, v1
         s_endpgm""")
-
-
-@pytest.mark.skipif(shutil.which('hipcc') is None and not os.path.exists('/opt/rocm/bin/hipcc'),
-                    reason='hipcc not available')
-def test_split_reverse_tile_loop_has_no_compiler_vmcnt():
-    """The split-bf16 reverse (X_REV) counts every vector-memory operation of its tile loop itself: the next tile's
-    cos blocks and inputs are inline-asm loads waited by the tile start's counted wait (w1x_kernel.hpp x_next_cos /
-    x_next_issue). A compiler load in the loop brings back a compiler s_waitcnt vmcnt, which does not know the asm
-    operations and drains the weight ring (the round-5 tile-start drain). Only asm waits may appear after the tile
-    loop's header."""
-    import re
-    hipcc = shutil.which('hipcc') or '/opt/rocm/bin/hipcc'
-    tmp = tempfile.mkdtemp(prefix='siren_isa_')
-    try:
-        out = os.path.join(tmp, 'tu_w1x.s')
-        subprocess.check_call([hipcc, '--offload-arch=gfx950', '-O3', '-std=c++17', '-mllvm',
-                               '-pragma-unroll-threshold=1000000', '--cuda-device-only', '-S', '-I',
-                               os.path.join(ROOT, 'include'), '-o', out, os.path.join(CSRC, 'tu_w1x.hip')],
-                              stderr=subprocess.DEVNULL)
-        s = open(out).read()
-    finally:
-        shutil.rmtree(tmp, ignore_errors=True)
-    names = re.findall(r'\n(_ZN5siren10w1x_kernelILi3ELi[23]ELi4E\w+):', s)
-    assert len(names) == 2, names
-    for nm in names:
-        i = s.find('\n' + nm + ':')
-        body = [ln.strip() for ln in s[i:s.find('.Lfunc_end', i)].split('\n')]
-        headers = [k for k, ln in enumerate(body) if 'Loop Header' in ln]
-        assert headers, nm
-        in_asm, waits = False, []
-        for k, ln in enumerate(body):
-            if ln.startswith(';;#ASMSTART'):
-                in_asm = True
-            elif ln.startswith(';;#ASMEND'):
-                in_asm = False
-            elif not in_asm and ln.startswith('s_waitcnt') and 'vmcnt' in ln and k > headers[-1]:
-                waits.append(ln)
-        assert not waits, '%s: compiler vmcnt waits in the tile loop: %s' % (nm, waits)
