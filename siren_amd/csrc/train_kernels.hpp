@@ -18,7 +18,11 @@ namespace siren {
 
 constexpr int WG_TILE_FLOATS = H * 16;          // 256 neurons of one 16-coordinate tile (16 KiB)
 constexpr int WG_SLOT = 2 * WG_TILE_FLOATS;     // delta (half-)tile + activation (half-)tile
+// Ring of 32 KiB slots (one 16-coordinate tile each). Round 6 A/B: 4 slots with one barrier per PAIR of tiles (and the
+// pair's ring issue behind the first block's MFMAs) measured neutral to 0.7 % slower (video 12.46 vs 12.38 ms, Poisson
+// 3.25 vs 3.23 ms per launch): the per-tile barrier is not what the kernel waits for.
 constexpr int WG_NBUF = 3;
+
 
 // Ring layout: a staged 1 KiB chunk is 16 neuron rows of 64 B (16 coordinates); row r keeps its coordinate quad c
 // at 16 B position (c + (r >> 1)) & 3. The swizzle is applied by the global side of the load (lane L fills LDS
@@ -49,11 +53,16 @@ __device__ __forceinline__ void wg_issue(const float* __restrict__ dsrc, const f
 // Software-pipelined: a tile's 16 operand reads are issued into the second register set while the previous tile's
 // 256 MFMAs run (the first version waited lgkmcnt(0) on them at the top of every tile, behind the barrier), and
 // the bias gradient accumulates from the delta operands already in registers (no extra LDS row reads).
+// JB = jet_bias at compile time (0 plain tiles; 1 jet tiles, value column 4g; 2 two-stream tiles, columns 4g, 4g + 2;
+// 3 Q8 tile pairs), and the two waves that share a delta row half (wc = 0, 1) each sum the bias of every other block
+// instead of both summing all eight: the runtime 0/1 masks and the duplicate sums were half of the loop's non-MFMA VALU
+// (round 6; the waves meet at every tile's barrier, so the work is split evenly rather than given to one wave).
+template <int JB>
 __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restrict__ abuf,
                                                           const float* __restrict__ dbuf, int64_t n_pad,
                                                           int64_t tps, float* __restrict__ partial, int64_t P,
                                                           int d, int o, int lh, int with_bias, int h,
-                                                          int jet_bias = 0, int64_t bstride_act = 0,
+                                                          int64_t bstride_act = 0,
                                                           int64_t bstride_part = 0) {
     __shared__ __attribute__((aligned(16))) float ring[WG_NBUF * WG_SLOT];
     const ParamOffsets off(d, o, lh, h);
@@ -101,12 +110,17 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
 #pragma unroll
         for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
     // bias partial sums: lane (g, i) accumulates the value columns of delta row 128 wr + 16 rb + i among
-    // coordinates 4g..4g+3 (jet tiles: column 4g only; two-stream tiles: 4g, 4g + 2) -- m1..m3 are exact 0/1 masks
+    // coordinates 4g..4g+3 (jet tiles: column 4g only; two-stream tiles: 4g, 4g + 2)
     float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    // jet_bias 3 (qf_kernel.hpp Q8 tiles: 8 coordinates x 4 streams over a tile pair): the value columns are columns
-    // 0..7 of the even tile of each pair, i.e. lane groups g < 2 of even tiles (mt, per tile)
-    const float m1 = (jet_bias == 1 || jet_bias == 2) ? 0.f : 1.f, m2 = jet_bias == 1 ? 0.f : 1.f, m3 = m1;
+    // JB 3 (qf_kernel.hpp Q8 tiles: 8 coordinates x 4 streams over a tile pair): the value columns are columns 0..7 of
+    // the even tile of each pair, i.e. lane groups g < 2 of even tiles (mt, per tile)
     float mt = 1.f;
+    auto bias_of = [&](const f32x4& v) -> float {
+        if constexpr (JB == 1) return v[0];
+        else if constexpr (JB == 2) return v[0] + v[2];
+        else if constexpr (JB == 3) return mt * ((v[0] + v[2]) + (v[1] + v[3]));
+        else return (v[0] + v[2]) + (v[1] + v[3]);
+    };
 
     f32x4 av[8], bv[8];
     // Operands are reloaded for the next tile as soon as their last MFMA of this tile has issued: A block rb after
@@ -116,10 +130,10 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
     // register of an in-flight load is ever copied -- inline-asm reads are invisible to its bookkeeping,
     // tools/check_asm_waits.py), read slot (k + 1) % 3 unconditionally (stale data after the last tile is never
     // used), and sched_barrier(0) keeps each reload between its block's MFMAs and the next block's.
-    auto block = [&](auto RB, int vn) {
+    auto block = [&](auto RB, int vn, auto BIAS) {
         constexpr int rb = decltype(RB)::value;
         const f32x4 v = av[rb];
-        bs[rb] += mt * ((v[0] + m2 * v[2]) + (m1 * v[1] + m3 * v[3]));
+        if constexpr (decltype(BIAS)::value == 1 + (rb & 1)) bs[rb] += bias_of(v);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -127,9 +141,9 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
         av[rb] = rv[vn + ra + rb * 64];
         __builtin_amdgcn_sched_barrier(0);
     };
-    auto last_block = [&](int vn) {
+    auto last_block = [&](int vn, auto BIAS) {
         const f32x4 v = av[7];
-        bs[7] += mt * ((v[0] + m2 * v[2]) + (m1 * v[1] + m3 * v[3]));
+        if constexpr (decltype(BIAS)::value == 2) bs[7] += bias_of(v);
         av[7] = rv[vn + ra + 7 * 64];
         __builtin_amdgcn_sched_barrier(0);
         // cb pairs outermost (a dependent MFMA two issues behind clears the 16x16x4 f32 latency); B block cb is
@@ -168,29 +182,39 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
             bv[q] = rv[rbv + q * 64];
         }
     }
-    int k = 0;
-    for (int64_t t = t0; t < t1; ++t, ++k) {
-        // tile t + 1 has landed (tile t + 2 may still be in flight); the barrier also retires every wave's reads of
-        // slot k % 3 (tile t, in registers), which the issue of tile t + 3 overwrites
-        if (t + 2 < t1)
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_barrier" ::: "memory");  // also a compiler barrier for the LDS loads
-        wg_issue(dsrc, asrc, ring, t + 3, t1, k + 3, wave, swz, tstride);
-        if (jet_bias == 3) mt = ((t & 1) == 0 && g < 2) ? 1.f : 0.f;
-        const int vn = ((k + 1) % WG_NBUF) * (WG_SLOT / 4);
-        block(std::integral_constant<int, 0>{}, vn);
-        block(std::integral_constant<int, 1>{}, vn);
-        block(std::integral_constant<int, 2>{}, vn);
-        block(std::integral_constant<int, 3>{}, vn);
-        block(std::integral_constant<int, 4>{}, vn);
-        block(std::integral_constant<int, 5>{}, vn);
-        block(std::integral_constant<int, 6>{}, vn);
-        last_block(vn);
-        // every read of this tile's slot is retired before the next barrier (the next issue overwrites it)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
+    auto tiles = [&](auto BIAS) {
+        int k = 0;
+        for (int64_t t = t0; t < t1; ++t, ++k) {
+            // tile t + 1 has landed (tile t + 2 may still be in flight); the barrier also retires every wave's reads of
+            // slot k % 3 (tile t, in registers), which the issue of tile t + 3 overwrites
+            if (t + 2 < t1)
+                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_barrier" ::: "memory");  // also a compiler barrier for the LDS loads
+            wg_issue(dsrc, asrc, ring, t + 3, t1, k + 3, wave, swz, tstride);
+            if (JB == 3) mt = ((t & 1) == 0 && g < 2) ? 1.f : 0.f;
+            const int vn = ((k + 1) % WG_NBUF) * (WG_SLOT / 4);
+            block(std::integral_constant<int, 0>{}, vn, BIAS);
+            block(std::integral_constant<int, 1>{}, vn, BIAS);
+            block(std::integral_constant<int, 2>{}, vn, BIAS);
+            block(std::integral_constant<int, 3>{}, vn, BIAS);
+            block(std::integral_constant<int, 4>{}, vn, BIAS);
+            block(std::integral_constant<int, 5>{}, vn, BIAS);
+            block(std::integral_constant<int, 6>{}, vn, BIAS);
+            last_block(vn, BIAS);
+            // every read of this tile's slot is retired before the next barrier (the next issue overwrites it)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+    };
+    // bias blocks: the even ones summed by the column-half-0 wave, the odd ones by its column-half-1 partner (same delta
+    // rows); BIAS = 0 none, 1 even blocks, 2 odd blocks
+    if (!with_bias)
+        tiles(std::integral_constant<int, 0>{});
+    else if (wc == 0)
+        tiles(std::integral_constant<int, 1>{});
+    else
+        tiles(std::integral_constant<int, 2>{});
 
     float* out = partial + (int64_t)s * P;
     float* dW = out + off.w(l);
@@ -205,10 +229,9 @@ __global__ __launch_bounds__(THREADS, 1) void wgrad_kernel(const float* __restri
     // bias: the value columns of lane group g (jet tiles: columns 0, 4, 8, 12; two-stream tiles: 0, 2, ..., 14),
     // then the four groups of each row combined in a fixed order through the (now idle) ring
     __syncthreads();
-    if (wc == 0) {
 #pragma unroll
-        for (int rb = 0; rb < 8; ++rb) ring[(128 * wr + 16 * rb + i) * 4 + g] = bs[rb];
-    }
+    for (int rb = 0; rb < 8; ++rb)
+        if ((rb & 1) == wc) ring[(128 * wr + 16 * rb + i) * 4 + g] = bs[rb];
     __syncthreads();
     if (qc == 0) {
         const float* rw = ring + threadIdx.x * 4;

@@ -7,8 +7,16 @@ namespace siren {
 void launch_wgrad(dim3 grid, hipStream_t st, const float* abuf, const float* dbuf, int64_t n_pad, int64_t tps,
                   float* partial, int64_t P, int d, int o, int lh, int with_bias, int h, int jet_bias,
                   int64_t bstride_act, int64_t bstride_part) {
-    hipLaunchKernelGGL(wgrad_kernel, grid, dim3(THREADS), 0, st, abuf, dbuf, n_pad, tps, partial, P, d, o, lh,
-                       with_bias, h, jet_bias, bstride_act, bstride_part);
+#define SIREN_WG(JB)                                                                                           \
+    hipLaunchKernelGGL(wgrad_kernel<JB>, grid, dim3(THREADS), 0, st, abuf, dbuf, n_pad, tps, partial, P, d, o, lh, \
+                       with_bias, h, bstride_act, bstride_part)
+    switch (jet_bias) {
+        case 1: SIREN_WG(1); break;
+        case 2: SIREN_WG(2); break;
+        case 3: SIREN_WG(3); break;
+        default: SIREN_WG(0); break;
+    }
+#undef SIREN_WG
 }
 
 #define NOF ((const float*)nullptr)
