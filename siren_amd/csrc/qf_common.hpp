@@ -61,12 +61,26 @@ struct QfCoef {
     float q11, q12, q22;
     float e1, e2;  // own z_3 partial: lo e2 z_12 (e1 = 0), hi e1 z_11 + e2 z_22
     float ca, cb;  // own (2 Q z) row: lo (2 Q z)_2 = q12 z_1 + 2 q22 z_2, hi (2 Q z)_1 = 2 q11 z_1 + q12 z_2
+    float mlo;     // 1 on lo lanes, 0 on hi lanes (zb's t3 term as an fma addend instead of a select)
 };
+
+// sin / cos of w z for the kept reverse's hidden layers: the phase u = z (w / 2 pi) in revolutions, then sincos_rev
+// (3 VALU + 2 transcendental against sincos_fast's 6 + 2 with the w z product; qf_elem runs ~50 VALU per element at
+// one wave per SIMD, where the VALU shares the issue with the f32 MFMAs). The phase is one fp32 rounding of w z / 2 pi,
+// the accuracy class of the phase-scaled W1 family; layer 0 (qf_elem0) keeps sincos_fast: its w0 is arbitrary (3000 in
+// golden G2), and an fp32 phase of thousands of revolutions keeps too few fraction bits. A/B (r06g): qfi_rev_kernel<3>
+// 5.05 -> 4.96 ms per Poisson-recipe step (static VALU 12970 -> 12028 with the select-free zb below).
+__device__ __forceinline__ void qf_sincos(float z, float wl, float& sn, float& cs) {
+    sincos_rev(z * (wl * 0.159154943091895336f), sn, cs);
+}
 
 // one layer's epilogue for one element (row r of block rb): kept streams k0..k2, cotangents ua (tile 0), ub (tile 1)
 // -> a-jet (aa, ab) and z-jet cotangent (za, zb) of this lane's two streams
+// (phase: the hidden layers' qf_sincos; false for layer 0, whose w0 is arbitrary — the serial kernel runs layer 0
+// through here, the interleaved one through qf_elem0, and both must round alike)
 __device__ __forceinline__ void qf_elem(float k0, float k1, float k2, float ua, float ub, float wl, float wl2,
-                                        const QfCoef& q, bool hi, float& aa, float& ab, float& za, float& zb) {
+                                        const QfCoef& q, bool hi, float& aa, float& ab, float& za, float& zb,
+                                        bool phase = true) {
     const float p0 = row_ror8(k0), p1 = row_ror8(k1);
     const float zp = __builtin_fmaf(q.e1, k1, q.e2 * k2);
     const float z3 = zp + row_ror8(zp);
@@ -75,7 +89,10 @@ __device__ __forceinline__ void qf_elem(float k0, float k1, float k2, float ua, 
     const float z1 = hi ? k0 : p0;
     const float z2 = hi ? p1 : k1;
     float sn, cs;
-    sincos_fast(wl * z, sn, cs);
+    if (phase)
+        qf_sincos(z, wl, sn, cs);
+    else
+        sincos_fast(wl * z, sn, cs);
     const float wc = wl * cs, w2s = wl2 * sn;
     const float qz = __builtin_fmaf(z1, __builtin_fmaf(q.q11, z1, q.q12 * z2), (q.q22 * z2) * z2);  // z^T Q z
     const float lin = __builtin_fmaf(q.ca, z1, q.cb * z2);                                       // (2 Q z)_own
@@ -83,7 +100,7 @@ __device__ __forceinline__ void qf_elem(float k0, float k1, float k2, float ua, 
     aa = hi ? wc * z1 : sn;                                       // a_1 | a_0
     ab = hi ? __builtin_fmaf(wc, z3, -w2s * qz) : wc * z2;        // a_3 | a_2
     const float t3 = w2s * (lin * u3);                            // w^2 s (2 Q z)_i u_3
-    zb = hi ? wc * ub : __builtin_fmaf(wc, ub, -t3);              // zb_3 | zb_2
+    zb = __builtin_fmaf(wc, ub, -(t3 * q.mlo));                   // zb_3 | zb_2 (hi: fma with -0 = the product)
     const float K = __builtin_fmaf(w2s, z3, (wl2 * wc) * qz);     // w^2 s z_3 + w^3 c z^T Q z
     const float t0 = __builtin_fmaf(w2s, __builtin_fmaf(pa, z1, ub * z2), u3 * K);
     za = __builtin_fmaf(wc, ua, -(hi ? t3 : t0));                 // zb_1 | zb_0
@@ -104,7 +121,7 @@ __device__ __forceinline__ void qf_elem0(float z, float z1, float z2, float ua, 
     aa = hi ? wc * z1 : sn;                                       // a_1 | a_0
     ab = hi ? __builtin_fmaf(wc, 0.f, -w2s * qz) : wc * z2;       // a_3 | a_2   (z_3 = 0)
     const float t3 = w2s * (lin * u3);
-    zb = hi ? wc * ub : __builtin_fmaf(wc, ub, -t3);              // zb_3 | zb_2
+    zb = __builtin_fmaf(wc, ub, -(t3 * q.mlo));                   // zb_3 | zb_2
     const float K = __builtin_fmaf(w2s, 0.f, (wl2 * wc) * qz);
     const float t0 = __builtin_fmaf(w2s, __builtin_fmaf(pa, z1, ub * z2), u3 * K);
     za = __builtin_fmaf(wc, ua, -(hi ? t3 : t0));                 // zb_1 | zb_0

@@ -52,6 +52,7 @@ __global__ __launch_bounds__(THREADS, 1) void qf_rev_kernel(const float* __restr
         q.e2 = hi ? q.q22 : q.q12;
         q.ca = hi ? 2.f * q.q11 : q.q12;
         q.cb = hi ? q.q12 : 2.f * q.q22;
+        q.mlo = hi ? 0.f : 1.f;
     }
     __syncthreads();
     // the ring starts at the first reverse slice (the stream's transposed layers)
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(THREADS, 1) void qf_rev_kernel(const float* __restr
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float ea, eb, za, zb;
-                qf_elem(kc.k[0][r], kc.k[1][r], kc.k[2][r], ua[r], ub[r], wl, wl2, q, hi, ea, eb, za, zb);
+                qf_elem(kc.k[0][r], kc.k[1][r], kc.k[2][r], ua[r], ub[r], wl, wl2, q, hi, ea, eb, za, zb, !rebuild);
                 aa[r] = ea;
                 ab[r] = eb;
                 act[0][rb][r] = za;

@@ -326,6 +326,7 @@ __global__ __launch_bounds__(THREADS, 1) void qfi_rev_kernel(const float* __rest
         q.e2 = cx.hi ? q.q22 : q.q12;
         q.ca = cx.hi ? 2.f * q.q11 : q.q12;
         q.cb = cx.hi ? q.q12 : 2.f * q.q22;
+        q.mlo = cx.hi ? 0.f : 1.f;
     }
 #pragma unroll
     for (int j = 0; j < MAXO; ++j) {

@@ -131,6 +131,9 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
 // Why the instruction count matters: an f32 MFMA (v_mfma_f32_16x16x4_f32) shares the SIMD's vector issue with
 // VALU — a filler VALU is never hidden behind it (tools/micro/mfma_valu_overlap: the first costs ~14 cycles, each
 // further ~4.5) — so every epilogue instruction is paid in full: W1 70.1% -> 76.4% of the fp32 MFMA peak.
+// (Round 6 A/B: the reduction in revolutions, u = t / 2 pi rounded once and r = u - rint(u), is 3 VALU but 4.0e-6
+// instead of 3.7e-7 on |t| <= 100 — the fp32 phase loses the bits its integer part takes — and at the first layer's
+// w0 = 3000 (golden G2) it broke the 1e-4 third-order bar; tools/micro/sincos_accuracy.hip.)
 __device__ __forceinline__ void sincos_fast(float t, float& sn, float& cs) {
     const float q = __builtin_rintf(t * 0.159154943091895336f);
     float r = __builtin_fmaf(-q, 6.28318548202514648f, t);
