@@ -548,16 +548,33 @@ __global__ __launch_bounds__(THREADS, 1) void w3i_kernel(const float* __restrict
     {
         constexpr int GL = (2 * LH - 1) & 1;
         const char* sa0 = cx.sa;
+        // The blocks' spill / kept loads run PD blocks ahead of their use (issued before the previous blocks'
+        // stores, which pin the order): loaded at the use, each block waited for its own loads behind the stores of
+        // the block before, one memory latency per block of every tile's serial tail (round 6)
+        constexpr int PD = 4;
+        f32x4 tz[NB], tc[NB], ts[NB];
+        auto tail_load = [&](int rb) {
+            tz[rb] = *(const f32x4*)(cx.wsp + w3_spill_off(0, 1, rb) + 16 * cx.lane);
+            if constexpr (KEPT) {
+                tc[rb] = *(const f32x4*)(cx.kc + rb * 1024 + 16 * cx.lane);
+                const float* p = (const float*)sa0 + rb * 256 + 4 * cx.g * 16 + c;
+                ts[rb] = f32x4{p[0], p[16], p[32], p[48]};
+            } else {
+                tc[rb] = *(const f32x4*)(cx.wsp + w3_spill_off(0, 0, rb) + 16 * cx.lane);  // z_0 (sin / cos at use)
+            }
+        };
+#pragma unroll
+        for (int rb = 0; rb < PD; ++rb) tail_load(rb);
 #pragma unroll
         for (int rb = 0; rb < NB; ++rb) {
-            const f32x4 zd = *(const f32x4*)(cx.wsp + w3_spill_off(0, 1, rb) + 16 * cx.lane);
+            if (rb + PD < NB) tail_load(rb + PD);
+            const f32x4 zd = tz[rb];
             f32x4 sn, cs;
             if constexpr (KEPT) {
-                cs = *(const f32x4*)(cx.kc + rb * 1024 + 16 * cx.lane);
-                const float* p = (const float*)sa0 + rb * 256 + 4 * cx.g * 16 + c;
-                sn = f32x4{p[0], p[16], p[32], p[48]};
+                cs = tc[rb];
+                sn = ts[rb];
             } else {
-                w3_sincos4(w0 * *(const f32x4*)(cx.wsp + w3_spill_off(0, 0, rb) + 16 * cx.lane), sn, cs);
+                w3_sincos4(w0 * tc[rb], sn, cs);
             }
             const f32x4 wc = w0 * cs;
             const f32x4 adb = st.acct[GL][rb];

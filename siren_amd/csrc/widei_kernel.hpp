@@ -391,10 +391,18 @@ __global__ __launch_bounds__(THREADS, 1) void widei_kernel(const float* __restri
         }
     } else {
         // delta_0 = u_0 . cos(w0 z_0) . w0 (cos_0 from the scratch), its tile, gx = delta_0 W0
+        // cos_0 blocks loaded PD blocks ahead of their use (issued before the previous blocks' tile stores): loaded at
+        // the use, every block waited for its own load behind the stores, 32 serial memory latencies in every tile's
+        // tail (round 6)
         float q[MAXD] = {0.f, 0.f, 0.f, 0.f};
+        constexpr int PD = 8;
+        f32x4 c0s[WNB];
+#pragma unroll
+        for (int rb = 0; rb < PD; ++rb) c0s[rb] = *(const f32x4*)(cx.cs + rb * 1024 + 16 * cx.lane);
 #pragma unroll
         for (int rb = 0; rb < WNB; ++rb) {
-            const f32x4 c0 = *(const f32x4*)(cx.cs + rb * 1024 + 16 * cx.lane);
+            if (rb + PD < WNB) c0s[rb + PD] = *(const f32x4*)(cx.cs + (rb + PD) * 1024 + 16 * cx.lane);
+            const f32x4 c0 = c0s[rb];
             const f32x4 dl = (st.acc[GL][rb] * c0) * w0;
             store_block(tp, rb, dl);
 #pragma unroll
