@@ -155,26 +155,16 @@ template <int MODE>
 constexpr bool w1_staged() { return W1_STAGE != 0 && w1_mem<MODE>() && !w1_fwd_half(MODE); }
 template <int MODE>
 constexpr bool w1_tiles() { return w1_mem<MODE>() && (MODE & MODE_NOTILE) == 0; }
-// cos(w0 z_0) of the W1 mode is parked in LDS (16 KiB per wave, 16 ds_write_b128 + 16 ds_read_b128 per tile) instead of
-// 64 VGPRs held from the FIRST epilogue to the delta_0 tail: the specialised headline body otherwise needs 517 of the
-// 512 registers and its scratch reloads put compiler vmcnt(0) waits (ring drains) into every tile
-#ifndef W1_C0LDS
-#define W1_C0LDS 1
-#endif
-template <int MODE>
-constexpr bool w1_c0lds() { return W1_C0LDS != 0 && (MODE & MODE_BASE) == MODE_W1; }
-#ifndef W1_ASM_INPUTS
-#define W1_ASM_INPUTS 1
-#endif
-// the next tile's inputs as inline-asm loads retired by the tile's counted waits: the one-wave-per-SIMD modes (W1,
-// STORE, REV). The forward-only modes run two workgroups per CU (the other one covers a drain) in 256 registers, where
-// hipcc reallocated an in-flight asm destination (tools/check_asm_waits.py), so they keep compiler loads, as does the
-// phase-stamp build (MODE_PROF: hipcc copied one before its wait)
+// the next tile's inputs as inline-asm loads retired by the tile's counted waits: the memory modes at one wave per SIMD
+// (STORE, REV). The forward-only modes run two workgroups per CU (the other one covers a drain) in 256 registers, where
+// hipcc reallocated an in-flight asm destination (tools/check_asm_waits.py), so they keep compiler loads. So does the W1
+// mode: its headline body is spill-free only with cos(w0 z_0) parked in LDS, and that body, with these loads, measured
+// 0.1-0.8 % slower than the spilling one on four same-box A/Bs — the spill reloads' drains hit a
+// ring slice that has mostly landed.
 template <int MODE>
 constexpr bool w1_asm_inputs() {
-    return W1_ASM_INPUTS != 0 && !forward_only(MODE & MODE_BASE) && (MODE & MODE_PROF) == 0;
+    return ((MODE & MODE_BASE) == MODE_STORE || (MODE & MODE_BASE) == MODE_REV) && (MODE & MODE_PROF) == 0;
 }
-constexpr int W1_C0FLOATS = WAVES * NB * 256;  // [wave][block][lane] f32x4
 constexpr bool w1_mem_rt(int mode) {
     return (mode & MODE_BASE) == MODE_STORE || (mode & MODE_BASE) == MODE_FWDS || (mode & MODE_BASE) == MODE_REV ||
            (mode & MODE_BASE) == MODE_JETS;
@@ -242,7 +232,6 @@ struct W1State {
     float yp[MAXO];    // partial y over this lane's neurons
     f32x4 cq[W1_COS_SLOTS];  // MODE_REV: cos blocks of the next epilogues (slot e % W1_COS_SLOTS, W1_COS_LEAD)
     f32x4 c0q[(MODE & MODE_BASE) == MODE_REV ? NB : 1];  // MODE_REV: cos(w0 z_0) of the delta_0 tail (loaded at mid NS - 3)
-    f32x4 c0r[w1_c0lds<MODE>() ? NB : 1];  // W1: the parked cos(w0 z_0), read back from LDS during the last slice
     f32x4 tq[2];       // W1_STAGE: the last epilogue's tile blocks, transposed (stored at the start of the next slice)
 };
 
@@ -271,7 +260,6 @@ struct W1Ctx {
     int64_t lstride;
     unsigned ring_vaddr;  // LDS byte address of this lane's 16 B in slot 0 of the ring
     unsigned sm_vaddr;    // LDS byte address of the small-parameter block + this lane's 4*g neuron offset
-    unsigned c0_vaddr;    // w1_c0lds: LDS byte address of this lane's 16 B in block 0 of its wave's cos(w0 z_0) park
     unsigned long long* prof;  // MODE_PROF: this wave's stamp row of the current tile (nullptr: not recorded)
     unsigned long long stamp[PROF_EVENTS];  // MODE_PROF: stamps of the current tile (uniform: SGPRs), stored at its end
     // JET: per-lane stream coefficients (stream s = lane & 3)
@@ -443,10 +431,7 @@ __device__ __forceinline__ void w1_epilogue(W1State<LH, MODE>& st, const W1Ctx& 
             st.act[b][r] = sn;
             cs4[r] = cs;
         }
-        if constexpr (w1_c0lds<MODE>())
-            asm volatile("ds_write_b128 %0, %1" ::"v"(cx.c0_vaddr + 1024u * b), "v"(cs4));
-        else if constexpr (!FWD)
-            st.C[0][b] = pin(cs4);
+        if constexpr (!FWD) st.C[0][b] = pin(cs4);
         if constexpr (w1_tiles<MODE>()) w1_tile_put<MODE, 0>(st, cx, cx.ta, 0, b, st.act[b]);
         if constexpr (FWDS) w3_store16(w3_at(cx.cs, b * 1024), cx.vl, cs4);
     } else if constexpr (KIND == EPI_SINCOS) {
@@ -592,12 +577,6 @@ __device__ __forceinline__ void w1_slice(W1State<LH, MODE>& st, const W1Ctx& cx)
             for (int i = 0; i < epi_nparams<KIND>(); ++i) asm volatile("" : "+v"(ep.v[i]));
         }
         if constexpr (p == 0) w1_flush<S, LH, MODE>(st, cx);  // the wait above retired the transpose
-        if constexpr (w1_c0lds<MODE>() && S + 1 == NS) {
-            // the last slice reads the parked cos(w0 z_0) back two blocks per pair, behind this pair's wait (the next
-            // pair's counted wait, or the tail's, retires them: 8 MFMAs of latency cover each pair)
-            st.c0r[2 * p] = lds_read4<2 * p * 1024>(cx.c0_vaddr);
-            st.c0r[2 * p + 1] = lds_read4<(2 * p + 1) * 1024>(cx.c0_vaddr);
-        }
         if constexpr (p == EPI_AT && EPI) {
             __builtin_amdgcn_sched_barrier(0);
             w1_epilogue<G, LH, MODE>(st, cx, KB + 1, ep);
@@ -667,8 +646,7 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
     constexpr bool REV = is_rev<MODE>();                     // abuf = lane-major cos buffer, dbuf = delta tiles
     constexpr int NS = npasses<MODE>() * LH * NB;
     constexpr int SMALL4 = (small_floats_ct(LH) + 3) / 4 * 4;
-    __shared__ __attribute__((aligned(16))) float lds[W1_NBUF * SLICE + SMALL4 + (w1_staged<MODE>() ? WAVES * STB_SCRATCH : 0) +
-                                                      (w1_c0lds<MODE>() ? W1_C0FLOATS : 0)];
+    __shared__ __attribute__((aligned(16))) float lds[W1_NBUF * SLICE + SMALL4 + (w1_staged<MODE>() ? WAVES * STB_SCRATCH : 0)];
     W1Ctx cx;
     W1State<LH, MODE> st;
     cx.ring = lds;
@@ -721,7 +699,6 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
     const unsigned lds_base = (unsigned)(uintptr_t)((__attribute__((address_space(3))) float*)lds);
     cx.ring_vaddr = lds_base + cx.lane * 16;
     cx.sm_vaddr = lds_base + W1_NBUF * SLICE * 4 + 16 * cx.g;
-    cx.c0_vaddr = lds_base + 4u * (W1_NBUF * SLICE + SMALL4 + cx.wave * NB * 256) + 16u * cx.lane;
     cx.lbytes = cx.lstride * 4;
     cx.vl = 16u * cx.lane;
     cx.vt = 4u * (4 * cx.g * 16 + c);
@@ -960,16 +937,6 @@ __global__ __launch_bounds__(THREADS, forward_only(MODE & MODE_BASE) ? 2 : 1) vo
             if constexpr (REV) {
 #pragma unroll
                 for (int rb = 0; rb < NB; ++rb) st.act[rb] = (st.acc[GL][rb] * st.c0q[rb]) * cx.w0;
-            } else if constexpr (w1_c0lds<MODE>()) {
-                // the parked cos(w0 z_0), read during the last slice; one wait statement names every destination
-                static_assert(NB == 16, "the wait names 16 blocks");
-                asm volatile("s_waitcnt lgkmcnt(0)"
-                             : "+v"(st.c0r[0]), "+v"(st.c0r[1]), "+v"(st.c0r[2]), "+v"(st.c0r[3]), "+v"(st.c0r[4]),
-                               "+v"(st.c0r[5]), "+v"(st.c0r[6]), "+v"(st.c0r[7]), "+v"(st.c0r[8]), "+v"(st.c0r[9]),
-                               "+v"(st.c0r[10]), "+v"(st.c0r[11]), "+v"(st.c0r[12]), "+v"(st.c0r[13]), "+v"(st.c0r[14]),
-                               "+v"(st.c0r[15]));
-#pragma unroll
-                for (int rb = 0; rb < NB; ++rb) st.act[rb] = (st.acc[GL][rb] * st.c0r[rb]) * cx.w0;
             } else {
 #pragma unroll
                 for (int rb = 0; rb < NB; ++rb) st.act[rb] = (st.acc[GL][rb] * st.C[0][rb]) * cx.w0;

@@ -25,12 +25,11 @@ sys.path.insert(0, os.path.join(ROOT, 'tools'))
 
 
 # kernels whose tile loop must hold no compiler s_waitcnt vmcnt (they count every vector-memory op themselves): the
-# headline W1 bodies (d_in 2 / 3), the general W1 body, the recompute W2 store, the fp32 reverse at every depth (the
-# image / hypernet W2 backward; gx-only REV of the deep and notile forms) and the split-bf16 reverse. A compiler load or scratch reload in the loop brings one back, and it drains the weight ring.
+# recompute W2 store, the fp32 reverse at every depth (the image / hypernet W2 backward; gx-only REV of the deep and
+# notile forms) and the split-bf16 reverse. (The headline W1 body is not among them: its spill-free form measured slower,
+# DESIGN.md §3.1.) A compiler load or scratch reload in the loop brings one back, and it drains the weight ring.
 LOOP_WAIT_FREE = {
-    'tu_w1.hip': [r'_ZN5siren9w1_kernelILi3ELi640E\w+', r'_ZN5siren9w1_kernelILi3ELi896E\w+',
-                  r'_ZN5siren9w1_kernelILi3ELi0E\w+', r'_ZN5siren9w1_kernelILi[123]ELi5E\w+',
-                  r'_ZN5siren9w1_kernelILi[123]ELi1E\w+'],
+    'tu_w1.hip': [r'_ZN5siren9w1_kernelILi[123]ELi5E\w+', r'_ZN5siren9w1_kernelILi[123]ELi1E\w+'],
     'tu_w1deep.hip': [r'_ZN5siren9w1_kernelILi[45]ELi5E\w+'],
     'tu_w1nt.hip': [r'_ZN5siren9w1_kernelILi[1-5]ELi37E\w+'],
     'tu_w1x.hip': [r'_ZN5siren10w1x_kernelILi3ELi[23]ELi4E\w+'],
@@ -117,10 +116,9 @@ def test_no_read_of_inflight_lds_load_registers():
 @pytest.mark.skipif(shutil.which('hipcc') is None and not os.path.exists('/opt/rocm/bin/hipcc'),
                     reason='hipcc not available')
 def test_counted_tile_loops_have_no_compiler_vmcnt():
-    """The headline W1 (its cos(w0 z_0) parked in LDS: no spills; the next tile's inputs as asm loads), the general
-    W1, the fp32 reverse (the delta_0 tail's cos blocks prefetched at mid NS - 3, the next tile's first cos blocks at
-    the last mid, a counted tile-start wait) and the split-bf16 reverse count every vector-memory operation of their
-    tile loop themselves. A compiler s_waitcnt vmcnt there does not know the asm operations and drains the weight ring
+    """The recompute W2 store (the next tile's inputs as asm loads), the fp32 reverse (also the delta_0 tail's cos
+    blocks prefetched at mid NS - 3, the next tile's first cos blocks at the last mid, a counted tile-start wait) and
+    the split-bf16 reverse count every vector-memory operation of their tile loop themselves. A compiler s_waitcnt vmcnt there does not know the asm operations and drains the weight ring
     (a scratch reload, or a compiler load consumed at the next tile start)."""
     res = _isa_results()
     for tu, pats in LOOP_WAIT_FREE.items():
