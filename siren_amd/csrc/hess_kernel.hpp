@@ -150,9 +150,9 @@ __global__ __launch_bounds__(THREADS, 1) void hess_kernel(const float* __restric
             const f32x4 t0 = hi ? acc[0][rb] : acc[0][rb] + *(const f32x4*)(bl + 16 * rb);
             if constexpr (KEEP) {
                 float* kpl = kept + hess_kept_off(ngroups, lh, l, grp, 0, 0, le);
-                *(f32x4*)(kpl + rb * 768) = t0;
-                *(f32x4*)(kpl + rb * 768 + 256) = acc[1][rb];
-                *(f32x4*)(kpl + rb * 768 + 512) = acc[2][rb];
+                st_tile((f32x4*)(kpl + rb * 768), t0);
+                st_tile((f32x4*)(kpl + rb * 768 + 256), acc[1][rb]);
+                st_tile((f32x4*)(kpl + rb * 768 + 512), acc[2][rb]);
             }
             hess_sin(t0, acc[1][rb], acc[2][rb], w, hi, act[0][rb], act[1][rb], act[2][rb]);
         }

@@ -392,12 +392,28 @@ __device__ __forceinline__ gf32x4_t* gmem4(float* p) { return (gf32x4_t*)p; }
 
 // STORE-mode writers: element (neuron 16*rb + 4*g + r, coord c) of a 16-coordinate tile lives at
 // neuron*16 + c, so lane (g, c) writes 4 floats 64 B apart per block; p already points at 4*g*16 + c (global memory).
+// Stores of the tiles / kept jets / cos buffers a LATER kernel reads back carry the nontemporal hint (global_store ...
+// nt): gigabytes per launch that no workgroup of the writing kernel re-reads, streamed past L2 instead of allocated in
+// it, where the weight ring every CU re-reads lives. A/B (round 6, profile_paths kernel totals): qfi_rev_kernel<3>
+// 4.96 -> 4.39 ms, w3i_kernel<3,1,1> 5.91 -> 5.51 ms, jets / split forward and reverse -1 %, the consumers (wgrad,
+// edge) unchanged within 1 %; the wgrad's own operand loads with nt measured neutral-to-worse (+1 % video) and stay
+// plain. SIREN_STORE_NT=0 restores plain stores (the A/B baseline).
+#ifndef SIREN_STORE_NT
+#define SIREN_STORE_NT 1
+#endif
+template <typename T, typename P>
+__device__ __forceinline__ void st_tile(P* p, const T& v) {
+    if constexpr (SIREN_STORE_NT != 0)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
 __device__ __forceinline__ void store_block(float* p, int rb, const f32x4& v) {
     gfloat* q = gmem(p) + 16 * rb * 16;
-    q[0] = v[0];
-    q[16] = v[1];
-    q[32] = v[2];
-    q[48] = v[3];
+    st_tile(q, v[0]);
+    st_tile(q + 16, v[1]);
+    st_tile(q + 32, v[2]);
+    st_tile(q + 48, v[3]);
 }
 // The same block as ONE coalesced global_store_dwordx4 per lane (1 KiB per instruction instead of four scattered
 // dword stores: epilogue store tails are store-ISSUE-bound, MI355X_MICROARCH.md), transposed through a per-wave LDS
@@ -412,7 +428,7 @@ __device__ __forceinline__ void store_block4(float* tile, int rb, const f32x4& v
     for (int r = 0; r < 4; ++r) scr[(4 * g + r) * STB_ROW + c] = v[r];
     const int n = lane >> 2, q = lane & 3;
     const f32x4 w = *(const f32x4*)(scr + n * STB_ROW + 4 * q);
-    *(f32x4*)(tile + rb * 256 + n * 16 + 4 * q) = w;
+    st_tile((f32x4*)(tile + rb * 256 + n * 16 + 4 * q), w);
 }
 __device__ __forceinline__ void store_tile(float* p, const f32x4 (&v)[NB]) {
 #pragma unroll

@@ -5,6 +5,13 @@
 #pragma once
 #include "siren_common.h"
 
+// the nontemporal hint of the epilogue stores (siren_common.h st_tile: SIREN_STORE_NT)
+#if SIREN_STORE_NT != 0
+#define SIREN_STPOL " nt"
+#else
+#define SIREN_STPOL ""
+#endif
+
 namespace siren {
 
 // Every epilogue load / store is in saddr form: a wave-uniform base in SGPRs, made opaque right before its use (hipcc
@@ -18,16 +25,16 @@ __device__ __forceinline__ const char* w3_at(const char* base, int64_t off) {
 // store reads them late; gfx940+ store-data hazard). hipcc inserts those for its own stores, not for inline asm — without
 // it the coordinates of lanes 12..15 of every 16-lane row came back wrong once the allocator reused a stored register.
 __device__ __forceinline__ void w3_store16(const char* base, unsigned voff, const f32x4& v) {
-    asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" ::"v"(voff), "v"(v), "s"(base));
+    asm volatile("global_store_dwordx4 %0, %1, %2" SIREN_STPOL "\n\ts_nop 1" ::"v"(voff), "v"(v), "s"(base));
 }
 // The same block as the four 64 B pieces at the lane's (4 g 16 + c) offset (voff = 4 (4 g 16 + c); what store_block
 // writes), one counted instruction each
 __device__ __forceinline__ void w3_store_tile(const char* base, unsigned voff, const f32x4& v) {
     asm volatile(
-        "global_store_dword %0, %1, %5\n\t"
-        "global_store_dword %0, %2, %5 offset:64\n\t"
-        "global_store_dword %0, %3, %5 offset:128\n\t"
-        "global_store_dword %0, %4, %5 offset:192\n\t"
+        "global_store_dword %0, %1, %5" SIREN_STPOL "\n\t"
+        "global_store_dword %0, %2, %5 offset:64" SIREN_STPOL "\n\t"
+        "global_store_dword %0, %3, %5 offset:128" SIREN_STPOL "\n\t"
+        "global_store_dword %0, %4, %5 offset:192" SIREN_STPOL "\n\t"
         "s_nop 1" ::"v"(voff),
         "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "s"(base));
 }
@@ -57,7 +64,7 @@ __device__ __forceinline__ void w3_stage_store(const char* base, const f32x4& v,
         "ds_write_b32 %1, %5 offset:240\n\t"
         "ds_read_b128 %0, %6\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
-        "global_store_dwordx4 %7, %0, %8\n\t"
+        "global_store_dwordx4 %7, %0, %8" SIREN_STPOL "\n\t"
         "s_nop 1"
         : "=&v"(t)
         : "v"(tw), "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(tr), "v"(voff), "s"(base));

@@ -11,6 +11,7 @@ FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -mllvm -pragma-unroll-threshold=1
 objs=""
 skip=""
 for tu in "$@"; do
+  while [ $(jobs -r | wc -l) -ge ${VB_JOBS:-6} ]; do wait -n; done
   /opt/rocm/bin/hipcc $FL -c -I $R/include -o $O/$tu.o $R/siren_amd/csrc/$tu.hip &
   objs="$objs $O/$tu.o"; skip="$skip $tu"
 done
