@@ -83,7 +83,7 @@ __device__ __forceinline__ void qfi_reload_issue(QfiState<LH>& st, const QfiCtx&
         constexpr int G = E / NB, B = E % NB, L = LH - G;
 #pragma unroll
         for (int t = 0; t < 3; ++t)
-            w3_load16(st.pk[E % 3][t], w3_at(cx.kb, (int64_t)(L - 1) * cx.kl + (B * 3 + t) * 1024), cx.vl);
+            w3_load16_once(st.pk[E % 3][t], w3_at(cx.kb, (int64_t)(L - 1) * cx.kl + (B * 3 + t) * 1024), cx.vl);
     }
 }
 template <int E, int LH>

@@ -73,4 +73,9 @@ __device__ __forceinline__ void w3_stage_store(const char* base, const f32x4& v,
 __device__ __forceinline__ void w3_load16(f32x4& r, const char* base, unsigned voff) {
     asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(r) : "v"(voff), "s"(base));
 }
+// the same with the nontemporal hint, for data read exactly once: the kept Hessian reverse's kept-jet reloads
+// (A/B round 6: qfi_rev_kernel<3> -2.6 %; neutral on w3i / widei / the fp32 reverse, which keep w3_load16)
+__device__ __forceinline__ void w3_load16_once(f32x4& r, const char* base, unsigned voff) {
+    asm volatile("global_load_dwordx4 %0, %1, %2 nt" : "=v"(r) : "v"(voff), "s"(base));
+}
 }  // namespace siren

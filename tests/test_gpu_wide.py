@@ -257,7 +257,7 @@ def test_g9_second_order_losses_at_hidden512_vs_reference(cuda, g9, manifest, ca
             key = 'B_sdf_grad_'
             for k, t in terms.items():
                 ref = manifest['G9_sdf_%s_f64' % k]
-                assert abs(float(t.mean()) - ref) <= 1e-4 * max(1., abs(ref)), k
+                assert abs(float(t.mean().detach()) - ref) <= 1e-4 * max(1., abs(ref)), k
         sum(t.mean() for t in terms.values()).backward()
         for k, p in m.named_parameters():
             ref = g9[key + k]
