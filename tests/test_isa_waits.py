@@ -17,7 +17,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, 'siren_amd', 'csrc')
-TUS = ['tu_w1.hip', 'tu_w1deep.hip', 'tu_w1nt.hip', 'tu_w0.hip', 'tu_w4.hip', 'tu_w3.hip', 'tu_wide.hip', 'tu_jet.hip', 'tu_wide_jet.hip',
+TUS = ['tu_w1.hip', 'tu_w1deep.hip', 'tu_widei_fb.hip', 'tu_w1nt.hip', 'tu_w0.hip', 'tu_w4.hip', 'tu_w3.hip', 'tu_wide.hip', 'tu_jet.hip', 'tu_wide_jet.hip',
        'tu_train.hip', 'tu_w1x.hip', 'tu_hess.hip', 'tu_w3i_tt.hip', 'tu_w3i_tf.hip', 'tu_w3i_ft.hip', 'tu_w3i_ff.hip',
        'tu_qfi.hip', 'tu_widei_fa.hip', 'tu_widei_ra.hip']
 
@@ -33,6 +33,17 @@ LOOP_WAIT_FREE = {
     'tu_w1deep.hip': [r'_ZN5siren9w1_kernelILi[45]ELi5E\w+'],
     'tu_w1nt.hip': [r'_ZN5siren9w1_kernelILi[1-5]ELi37E\w+'],
     'tu_w1x.hip': [r'_ZN5siren10w1x_kernelILi3ELi[23]ELi4E\w+'],
+}
+
+
+# kernels whose 16-byte stores are all tiles / kept jets / spill slots read back by a later kernel (or a later phase):
+# every global_store_dwordx4 must carry the nontemporal hint (without it they evict the weight image
+# from L2; qfi 4.96 -> 4.39 ms, w3i 5.91 -> 5.51 ms with it)
+NT_STORE_KERNELS = {
+    'tu_qfi.hip': [r'_ZN5siren14qfi_rev_kernelILi\dE\w+'],
+    'tu_w3i_tt.hip': [r'_ZN5siren10w3i_kernelILi\dELb1ELb1E\w+'],
+    'tu_hess.hip': [r'_ZN5siren11hess_kernelILb1E\w+'],
+    'tu_widei_fb.hip': [r'_ZN5siren12widei_kernel\w+'],
 }
 
 
@@ -79,7 +90,7 @@ def _compile_and_check(tu):
         s = open(out).read()
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-    bad, loops = [], {}
+    bad, loops, plain = [], {}, {}
     for nm in re.findall(r'\n(_Z\w+):', s):
         i = s.find('\n' + nm + ':')
         j = s.find('.Lfunc_end', i)
@@ -90,7 +101,10 @@ def _compile_and_check(tu):
             bad.append('%s %s: %d (first: %s)' % (tu, nm, len(probs), probs[0][1]))
         if any(re.fullmatch(pat, nm) for pat in LOOP_WAIT_FREE.get(tu, [])):
             loops[nm] = tile_loop_vmcnt_waits([ln.strip() for ln in body])
-    return bad, loops
+        if any(re.fullmatch(pat, nm) for pat in NT_STORE_KERNELS.get(tu, [])):
+            st = [ln.strip() for ln in body if ln.strip().startswith('global_store_dwordx4')]
+            plain[nm] = (len(st), [ln for ln in st if not re.search(r'\bnt\b', ln)])
+    return bad, loops, plain
 
 
 _RESULTS = {}
@@ -202,3 +216,16 @@ def test_checker_correlates_flag_branches():
     .LBB0_4:
         v_add_f32 v4, v0, v1
         s_endpgm""")
+
+
+@pytest.mark.skipif(shutil.which('hipcc') is None and not os.path.exists('/opt/rocm/bin/hipcc'),
+                    reason='hipcc not available')
+def test_tile_stores_are_nontemporal():
+    """The store-heavy kernels' 16-byte tile / kept-jet stores carry the nontemporal hint (SIREN_STORE_NT)."""
+    res = _isa_results()
+    for tu, pats in NT_STORE_KERNELS.items():
+        plain = res[tu][2]
+        assert plain, (tu, 'no kernel matched', pats)
+        for nm, (n, bad) in plain.items():
+            assert n > 0, '%s: no 16-byte stores found' % nm
+            assert not bad, '%s: %d of %d stores without nt (first: %s)' % (nm, len(bad), n, bad[0])
